@@ -1,0 +1,217 @@
+"""ORACLE — CPU restatement of the reference PnP-PDS hot path.  TEST INFRASTRUCTURE ONLY.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may
+import this module, and only as the checker / the timed CPU baseline.  The product
+path (``pnp-pds_amd/``) never imports it and fails loudly without its HIP library.
+
+Pinning: every function here is checked in ``tests/test_oracle_golden.py`` against
+golden vectors produced by importing the reference itself in the build container
+(``tests/golden/make_golden.py``; fixtures in ``tests/golden/*.npz``).
+
+Semantics follow the reference file:line cited on each function, including its
+mixed precision: the denoiser runs in float32 (models/denoiser.py:37) while the
+dual variables live in float64 numpy arrays (iteration.py:23-29).
+"""
+from __future__ import annotations
+
+import time
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+LEAKY_SLOPE = 0.01
+
+
+# ---------------------------------------------------------------------------
+# Observation operators (operators.py:7-79)
+# ---------------------------------------------------------------------------
+def _kernel_spectrum(h: np.ndarray, shape) -> np.ndarray:
+    """FFT of h placed circularly so that tap (a, b) sits at offset (a - m, b - m)."""
+    H, W = shape
+    kh, kw = h.shape
+    hp = np.zeros((H, W), np.float64)
+    for a in range(kh):
+        for b in range(kw):
+            if h[a, b] != 0.0:
+                hp[(a - kh // 2) % H, (b - kw // 2) % W] += h[a, b]
+    return np.fft.fft2(hp)
+
+
+def blur(x: np.ndarray, h: np.ndarray) -> np.ndarray:
+    """Φx — operators.py:7-22.  The reference's wrap-pad + FFT + crop equals the centred
+    circular convolution  y[i,j] = Σ_ab h[a,b] x[(i-a+m) mod H, (j-b+m) mod W]."""
+    A = _kernel_spectrum(h, x.shape[-2:])
+    return np.real(np.fft.ifft2(np.fft.fft2(np.asarray(x, np.float64)) * A))
+
+
+def adj_blur(x: np.ndarray, h: np.ndarray) -> np.ndarray:
+    """Φᵀx — operators.py:24-38: circular correlation  y[i,j] = Σ_ab h[a,b] x[(i+a-m), (j+b-m)]."""
+    A = _kernel_spectrum(h, x.shape[-2:])
+    return np.real(np.fft.ifft2(np.fft.fft2(np.asarray(x, np.float64)) * np.conj(A)))
+
+
+def sampling_mask(H: int, W: int, r: float) -> np.ndarray:
+    """Keep-mask of operators.py:40-58: round(H·W·(1-r)) pixels dropped, chosen by
+    RandomState(1234).permutation(H·W), shared by all channels.  Returns uint8 [H, W]."""
+    cnt = round(H * W * (1 - r))
+    q = np.random.RandomState(seed=1234).permutation(H * W)[:cnt]
+    m = np.ones(H * W, np.uint8)
+    m[q] = 0
+    return m.reshape(H, W)
+
+
+def random_sampling(x: np.ndarray, r: float) -> np.ndarray:
+    """operators.py:40-58 (self-adjoint); returns float64 like the reference."""
+    m = sampling_mask(x.shape[-2], x.shape[-1], r)
+    return np.asarray(x, np.float64) * m
+
+
+def observation_operators(kind: str, h: np.ndarray | None = None, r: float = 0.8):
+    """(phi, adj_phi) — operators.py:60-79."""
+    if kind == "blur":
+        return (lambda x: blur(x, h)), (lambda x: adj_blur(x, h))
+    if kind == "random_sampling":
+        f = lambda x: random_sampling(x, r)  # noqa: E731
+        return f, f
+    if kind == "Id":
+        return (lambda x: x), (lambda x: x)
+    raise ValueError(kind)
+
+
+# ---------------------------------------------------------------------------
+# Proximal operators (operators.py:94-115) and metrics (utils/utils_eval.py:4-7)
+# ---------------------------------------------------------------------------
+def proj_l1_ball(x, alpha_s, sp_nl, r=1):
+    """operators.py:94-100: Euclidean projection onto {‖s‖₁ ≤ η}, η = α_s·N·sp_nl·r/2,
+    with θ = max(0, max_k (S_k − η)/k) over |x| sorted descending."""
+    eta = alpha_s * x.size * sp_nl * r * 0.5
+    a = np.abs(np.ravel(x))
+    srt = np.sort(a)[::-1]
+    theta = np.max((np.cumsum(srt) - eta) / np.arange(1, a.size + 1))
+    theta = max(theta, 0.0)
+    return (np.fmax(a - theta, 0) * np.sign(np.ravel(x))).reshape(x.shape)
+
+
+def proj_l2_ball(x, alpha_n, gaussian_nl, sp_nl, x_0, r=1):
+    """operators.py:102-108: projection onto the ball B(x_0, ε), ε = sqrt(N(1-sp_nl))·r·α_n·σ."""
+    eps = np.sqrt(x.size * (1 - sp_nl)) * r * alpha_n * gaussian_nl
+    d = x - x_0
+    nrm = np.linalg.norm(d)
+    if nrm > eps:
+        return x_0 + eps * d / nrm
+    return np.copy(x)
+
+
+def prox_gkl(x, gamma, alpha, x_0):
+    """operators.py:114-115 (generalised-KL prox), elementwise."""
+    t = x - gamma * alpha
+    return 0.5 * (t + np.sqrt(np.square(t) + 4 * gamma * x_0))
+
+
+def psnr(x_true, x):
+    """utils/utils_eval.py:4-7 (data_range 1, float64 MSE)."""
+    mse = np.mean((np.asarray(x_true, np.float64) - np.asarray(x, np.float64)) ** 2)
+    return 10 * np.log10(1.0 / mse)
+
+
+# ---------------------------------------------------------------------------
+# Denoiser (models/denoiser.py:34-46, models/basic_models.py:25-38,
+#           KAIR variant models/network_dncnn.py:42-77)
+# ---------------------------------------------------------------------------
+class OracleDenoiser:
+    """Forward of the conv stack on torch-CPU in float32.
+
+    ``emulate_fp16=True`` rounds every conv's input activations and weights to fp16
+    (fp32 accumulation, fp16 storage of hidden activations) — the device numerics.
+    """
+
+    def __init__(self, weights, emulate_fp16: bool = False):
+        self.w = weights
+        self.emulate_fp16 = emulate_fp16
+        self.tw = [torch.from_numpy(np.ascontiguousarray(a, np.float32)) for a in weights.weights]
+        self.tb = [torch.from_numpy(np.ascontiguousarray(b, np.float32)) for b in weights.biases]
+        if emulate_fp16:
+            self.tw = [t.half().float() for t in self.tw]
+
+    @torch.no_grad()
+    def forward_batch(self, x: np.ndarray) -> np.ndarray:
+        """x: [B, C, H, W] -> [B, C, H, W] float32."""
+        xin = torch.from_numpy(np.ascontiguousarray(x, np.float32))
+        if self.w.clamp_io:
+            xin = xin.clamp(0, 1)
+        h = xin
+        n = len(self.tw)
+        for i in range(n):
+            if self.emulate_fp16:
+                h = h.half().float()
+            h = F.conv2d(h, self.tw[i], self.tb[i], padding=1)
+            if i < n - 1:
+                h = F.leaky_relu(h, LEAKY_SLOPE) if self.w.act == 0 else F.relu(h)
+        out = h + xin if self.w.residual > 0 else xin - h
+        if self.w.clamp_io:
+            out = out.clamp(0, 1)
+        return out.numpy()
+
+    def denoise(self, x: np.ndarray) -> np.ndarray:
+        """Reference call shape: (C,H,W) for RGB, (H,W) for gray (denoiser.py:35-36)."""
+        if x.ndim == 2:
+            return self.forward_batch(x[None, None])[0, 0]
+        return self.forward_batch(x[None])[0]
+
+
+# ---------------------------------------------------------------------------
+# test_iter (iteration.py:10-196), methods A/B/C-Proposed and comparisonB-2
+# ---------------------------------------------------------------------------
+METHOD_ALIASES = {"ours-A": "A-Proposed", "ours-B": "B-Proposed", "ours-C": "C-Proposed"}
+
+
+def test_iter(x_0, x_obsrv, x_true, phi, adj_phi, gamma1, gamma2, alpha_s, alpha_n, myLambda,
+              m1, m2, gammaInADMMStep1, gaussian_nl, sp_nl, poisson_alpha, denoiser, max_iter,
+              method="A-Proposed", ch=3, r=1, ssim_fn=None):
+    """Restatement of iteration.test_iter for the hot-path methods.  ``denoiser`` is an
+    OracleDenoiser (the reference builds one from ``path_prox``, iteration.py:40-41)."""
+    method = METHOD_ALIASES.get(method, method)
+    x_n = x_0
+    y_n = np.zeros(x_0.shape)
+    s_n = np.zeros(x_0.shape)
+    z_n = np.zeros(x_0.shape)
+    c = np.zeros(max_iter)
+    psnr_data = np.zeros(max_iter)
+    ssim_data = np.zeros(max_iter)
+    t0 = time.perf_counter()
+    for i in range(max_iter):
+        x_prev = x_n
+        s_prev = s_n
+        if method == "A-Proposed":                                        # iteration.py:48-52
+            x_n = denoiser.denoise(x_n - gamma1 * adj_phi(y_n))
+            y_n = y_n + gamma2 * phi(2 * x_n - x_prev)
+            y_n = y_n - gamma2 * proj_l2_ball(y_n / gamma2, alpha_n, gaussian_nl, sp_nl, x_obsrv)
+        elif method == "B-Proposed":                                      # iteration.py:53-58
+            x_n = denoiser.denoise(x_n - gamma1 * adj_phi(y_n))
+            s_n = proj_l1_ball(s_n - gamma1 * y_n, alpha_s, sp_nl, r)
+            y_n = y_n + gamma2 * (phi(2 * x_n - x_prev) + 2 * s_n - s_prev)
+            y_n = y_n - gamma2 * proj_l2_ball(y_n / gamma2, alpha_n, gaussian_nl, sp_nl, x_obsrv, r)
+        elif method == "C-Proposed":                                      # iteration.py:59-63
+            x_n = denoiser.denoise(x_n - gamma1 * adj_phi(y_n))
+            y_n = y_n + gamma2 * phi(2 * x_n - x_prev)
+            y_n = y_n - gamma2 * prox_gkl(y_n / gamma2, myLambda / gamma2, poisson_alpha, x_obsrv)
+        elif method == "comparisonB-2":                                   # iteration.py:127-132
+            x_n = np.ones(s_n.shape)                                      # admm.py:30-36
+            for _ in range(m1):
+                x_n = x_n - 1 / gamma1 * adj_phi(phi(x_n) + s_n - z_n + y_n)
+                x_n = denoiser.denoise(x_n)
+            s_n = np.ones(x_n.shape)                                      # admm.py:38-44
+            for _ in range(m2):
+                s_n = s_n - 1 / gamma1 * (phi(x_n) + s_n - z_n + y_n)
+                s_n = proj_l1_ball(s_n, alpha_s, sp_nl)
+            z_n = proj_l2_ball(phi(x_n) + s_n + y_n, alpha_n, gaussian_nl, sp_nl, x_obsrv)
+            y_n = y_n + phi(x_n) + s_n - z_n
+        else:
+            raise ValueError(f"Unknown method: {method}")
+        c[i] = np.linalg.norm((x_n - x_prev).flatten(), 2) / np.linalg.norm(x_prev.flatten(), 2)
+        psnr_data[i] = psnr(x_true, x_n)
+        if ssim_fn is not None:
+            ssim_data[i] = ssim_fn(x_true, x_n)
+    avg = (time.perf_counter() - t0) / max(max_iter, 1)
+    return x_n, s_n + 0.5, c, psnr_data, ssim_data, avg

@@ -1,0 +1,193 @@
+"""Generate golden vectors by IMPORTING THE REFERENCE (build container only).
+
+    python tests/golden/make_golden.py [/root/reference]
+
+The reference's hot path imports on CPU with four runtime shims and no
+edits to /root/reference:
+  1. ``bm3d`` (iteration.py:3, BM3D comparison methods only)  -> empty module
+  2. ``skimage.metrics.structural_similarity`` (utils_eval.py:2) -> stub returning 0.0
+     (SSIM is therefore *unpinned*)
+  3. ``models.denoiser.load_checkpoint`` (denoiser.py:18-21) -> copies our converted npz
+     weights (pnp-pds_amd/weights, produced by the data-only reader) into the reference's
+     own ``simple_CNN``; the legacy pickle is never unpickled
+  4. ``torch.cuda.synchronize`` (iteration.py:192) -> no-op (no GPU here)
+Everything else — operators.py, models/basic_models.py, algorithm/admm.py,
+iteration.test_iter, utils/utils_noise.py — runs as shipped.
+
+Outputs (inputs + expected outputs, nothing else) go to tests/golden/*.npz.
+"""
+import os
+import sys
+import time
+import types
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.abspath(os.path.join(HERE, "..", ".."))
+sys.path.insert(0, os.path.join(REPO, "pnp-pds_amd"))
+from pnppds.weights import DenoiserWeights, WEIGHTS_DIR  # noqa: E402
+
+
+def synthetic_image(C, H, W, seed):
+    """Deterministic structured test image in [0,1]: gradients, sinusoids, rectangles."""
+    rng = np.random.RandomState(seed)
+    yy, xx = np.meshgrid(np.linspace(0, 1, H), np.linspace(0, 1, W), indexing="ij")
+    img = np.zeros((C, H, W), np.float64)
+    for c in range(C):
+        f1, f2, ph = rng.uniform(1, 6), rng.uniform(1, 6), rng.uniform(0, 6.28)
+        img[c] = 0.45 + 0.25 * np.sin(2 * np.pi * f1 * xx + ph) * np.cos(2 * np.pi * f2 * yy) + 0.2 * (xx - 0.5)
+        for _ in range(4):
+            y0, x0 = rng.randint(0, H - H // 4), rng.randint(0, W - W // 4)
+            img[c, y0:y0 + rng.randint(4, H // 4), x0:x0 + rng.randint(4, W // 4)] += rng.uniform(-0.3, 0.3)
+    return np.clip(img, 0, 1).astype(np.float32)
+
+
+def install_shims(ref_root):
+    sys.modules["bm3d"] = types.ModuleType("bm3d")
+    sk = types.ModuleType("skimage")
+    skm = types.ModuleType("skimage.metrics")
+    skm.structural_similarity = lambda **kw: 0.0
+    sk.metrics = skm
+    sys.modules["skimage"] = sk
+    sys.modules["skimage.metrics"] = skm
+    sys.path.insert(0, ref_root)
+    import torch
+    torch.cuda.synchronize = lambda *a, **k: None
+    import models.denoiser as md
+
+    def load_checkpoint(model, file_name):
+        stem = os.path.splitext(os.path.basename(file_name))[0]
+        w = DenoiserWeights.load_npz(os.path.join(WEIGHTS_DIR, stem + ".npz"))
+        sd = {"in_conv.weight": w.weights[0], "in_conv.bias": w.biases[0],
+              "out_conv.weight": w.weights[-1], "out_conv.bias": w.biases[-1]}
+        for i in range(1, w.depth - 1):
+            sd[f"conv_list.{i-1}.weight"] = w.weights[i]
+            sd[f"conv_list.{i-1}.bias"] = w.biases[i]
+        model.module.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+        return model
+
+    md.load_checkpoint = load_checkpoint
+
+
+def degrade(x_true, phi, Id, deg_op, gaussian_nl, sp_nl, poisson_noise, poisson_alpha):
+    """main.py:49-64 verbatim semantics, using the reference's own utils_noise."""
+    from utils.utils_noise import add_gaussian_noise, add_salt_and_pepper_noise, apply_poisson_noise
+    obs = phi(x_true)
+    obs = add_gaussian_noise(obs, gaussian_nl, Id if deg_op in ("blur", "Id") else phi)
+    if poisson_noise:
+        obs = apply_poisson_noise(obs, poisson_alpha)
+    obs = add_salt_and_pepper_noise(obs, sp_nl, Id if deg_op in ("blur", "Id") else phi)
+    x0 = np.copy(obs)
+    if poisson_noise:
+        x0 = x0 / poisson_alpha
+    return obs, x0
+
+
+def main(ref_root="/root/reference"):
+    install_shims(ref_root)
+    import torch
+    import operators as op
+    import iteration
+    from models.denoiser import Denoiser
+    from models.network_dncnn import DnCNN
+    from utils.utils_eval import eval_psnr
+
+    path_kernel = os.path.join(ref_root, "blur_models", "blur_1.mat")
+    nn_dir = os.path.join(ref_root, "nn")
+    h = __import__("scipy.io").io.loadmat(path_kernel)["blur"]
+    rng = np.random.default_rng(20261015)
+    out = {}
+
+    # ---- G1: observation operators -------------------------------------------------
+    ops = {"h": h}
+    for tag, shape in (("rgb64", (3, 64, 64)), ("gray64", (64, 64)), ("gray256", (256, 256)), ("rgb48x80", (3, 48, 80))):
+        x = rng.standard_normal(shape)
+        ops[f"x_{tag}"] = x
+        for kind, rr in (("blur", 0.8), ("random_sampling", 0.8), ("random_sampling", 0.5)):
+            if kind == "random_sampling" and (tag == "gray256" or (len(shape) == 3 and shape[0] != 3)):
+                continue
+            phi, adj = op.get_observation_operators(kind, path_kernel, rr)
+            key = kind if kind == "blur" else f"rs{int(rr*10)}"
+            ops[f"phi_{key}_{tag}"] = phi(x)
+            ops[f"adj_{key}_{tag}"] = adj(x)
+    # ---- G2: proximal operators ----------------------------------------------------------
+    v = rng.standard_normal((3, 64, 64)) * 0.1
+    x0 = rng.uniform(0, 1, (3, 64, 64))
+    ops["prox_v"], ops["prox_x0"] = v, x0
+    for nl, a in ((0.01, 0.95), (10.0, 1.0)):     # outside / inside the ball
+        ops[f"l2_{nl}_{a}"] = op.proj_l2_ball(x0 + v, a, nl, 0.1, x0, 0.8)
+    for sp in (0.0, 0.01, 0.1, 0.5):
+        ops[f"l1_{sp}"] = op.proj_l1_ball(v, 0.95, sp, 0.8)
+    ops["l1_inside"] = op.proj_l1_ball(v * 1e-4, 0.95, 0.1, 1)
+    ops["gkl"] = op.prox_GKL(v * 10, 0.5, 300.0, np.round(x0 * 300))
+    ops["psnr"] = np.array([eval_psnr(x0, x0 + v)])
+    np.savez_compressed(os.path.join(HERE, "ops.npz"), **ops)
+    print("ops.npz", len(ops))
+
+    # ---- G3: denoisers --------------------------------------------------------------
+    den = {}
+    for ch, name in ((3, "DnCNN_nobn_nch_3_nlev_0.01"), (1, "DnCNN_nobn_nch_1_nlev_0.01")):
+        d = Denoiser(os.path.join(nn_dir, name + ".pth"), ch)
+        clean = synthetic_image(ch, 64, 64, seed=ch)
+        xin = (clean + 0.03 * rng.standard_normal(clean.shape)).astype(np.float32)
+        xin[:, :4, :4] = -0.2          # exercise the input clamp (denoiser.py:40)
+        xin[:, -4:, -4:] = 1.3
+        if ch == 1:
+            xin = xin[0]
+        den[f"in_{name}"] = xin
+        den[f"out_{name}"] = d.denoise(xin)
+    for ch, name, nb in ((3, "dncnn_color_blind", 20), (1, "dncnn_15", 17)):
+        net = DnCNN(in_nc=ch, out_nc=ch, nc=64, nb=nb, act_mode="R", model_path=os.path.join(nn_dir, name + ".pth"))
+        xin = synthetic_image(ch, 64, 64, seed=10 + ch) + 0.05 * rng.standard_normal((ch, 64, 64)).astype(np.float32)
+        with torch.no_grad():
+            o = net(torch.from_numpy(xin.astype(np.float32)).unsqueeze(0))[0].numpy()
+        den[f"in_{name}"], den[f"out_{name}"] = xin.astype(np.float32), o
+    np.savez_compressed(os.path.join(HERE, "denoiser.npz"), **den)
+    print("denoiser.npz", len(den))
+
+    # ---- G4 / G6: test_iter trajectories ------------------------------------------------
+    cases = [
+        # name,      method,        deg_op,            ch, sigma, sp_nl, poisson, g1,     g2,          a_n,  a_s,  lam, r,   iters, m1, m2
+        ("A_blur",   "A-Proposed",  "blur",            3, 0.01, 0.0, False, 0.99,   0.99,        0.95, 1.0,  1.0, 0.8, 5, 15, 15),
+        ("A_id",     "A-Proposed",  "Id",              3, 0.01, 0.0, False, 0.99,   0.99,        0.95, 1.0,  1.0, 0.8, 5, 15, 15),
+        ("A_rs",     "A-Proposed",  "random_sampling", 3, 0.01, 0.0, False, 0.99,   0.99,        0.95, 1.0,  1.0, 0.8, 5, 15, 15),
+        ("A_gray",   "A-Proposed",  "Id",              1, 0.01, 0.0, False, 0.99,   0.99,        0.95, 1.0,  1.0, 0.8, 5, 15, 15),
+        ("B_blur",   "B-Proposed",  "blur",            3, 0.01, 0.1, False, 1.0,    0.49,        0.95, 0.95, 1.0, 0.8, 5, 15, 15),
+        ("C_rs",     "C-Proposed",  "random_sampling", 3, 0.0,  0.0, True,  0.00035, 1 / 0.00035, 1.0, 1.0,  1.0, 0.5, 5, 15, 15),
+        ("C_blur",   "C-Proposed",  "blur",            3, 0.0,  0.0, True,  0.00055, 1786.0,      1.0, 1.0,  1.0, 0.8, 5, 15, 15),
+        ("ADMM_B2",  "comparisonB-2", "blur",          3, 0.01, 0.1, False, 0.99,   0.99,        0.95, 0.95, 1.0, 0.8, 1, 2, 2),
+    ]
+    for (name, method, deg, ch, sig, sp, pois, g1, g2, an, as_, lam, r, iters, m1, m2) in cases:
+        phi, adj = op.get_observation_operators(deg, path_kernel, r)
+        Id, _ = op.get_observation_operators("Id", path_kernel, r)
+        xt = synthetic_image(ch, 64, 64, seed=100 + len(name))
+        if ch == 1:
+            xt = xt[0]
+        obs, x0 = degrade(xt, phi, Id, deg, sig, sp, pois, 300)
+        arch = f"DnCNN_nobn_nch_{ch}_nlev_0.01"
+        t = time.perf_counter()
+        res = iteration.test_iter(x0, obs, xt, phi, adj, g1, g2, as_, an, lam, m1, m2, 0.1, sig, sp, 300,
+                                  os.path.join(nn_dir, arch + ".pth"), iters, method, ch, r)
+        xs, ss, c, ps, _ssim, _t = res
+        np.savez_compressed(os.path.join(HERE, f"iter_{name}.npz"), x_true=xt, x_obs=obs, x_0=x0,
+                            x_out=xs, s_out=ss, c=c, psnr=ps,
+                            params=np.array([g1, g2, as_, an, lam, m1, m2, 0.1, sig, sp, 300, iters, ch, r]),
+                            method=np.array(method), deg_op=np.array(deg), arch=np.array(arch))
+        print(f"iter_{name}.npz  psnr {ps[0]:.3f} -> {ps[-1]:.3f}  ({time.perf_counter()-t:.1f}s)")
+
+    # ---- G5: long run at 256^2 (pins the 0.01 dB target) ---------------------------------
+    phi, adj = op.get_observation_operators("blur", path_kernel, 0.8)
+    Id, _ = op.get_observation_operators("Id", path_kernel, 0.8)
+    xt = synthetic_image(3, 256, 256, seed=7)
+    obs, x0 = degrade(xt, phi, Id, "blur", 0.01, 0.0, False, 300)
+    t = time.perf_counter()
+    res = iteration.test_iter(x0, obs, xt, phi, adj, 0.99, 0.99, 1.0, 0.95, 1.0, 15, 15, 0.1, 0.01, 0.0, 300,
+                              os.path.join(nn_dir, "DnCNN_nobn_nch_3_nlev_0.01.pth"), 120, "A-Proposed", 3, 0.8)
+    np.savez_compressed(os.path.join(HERE, "long_A_blur_256.npz"), x_true=xt, x_obs=obs.astype(np.float32),
+                        x_out=res[0].astype(np.float16), c=res[2], psnr=res[3])
+    print(f"long_A_blur_256.npz psnr {res[3][0]:.3f} -> {res[3][-1]:.3f} ({time.perf_counter()-t:.1f}s)")
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:])
