@@ -1,0 +1,213 @@
+"""Benchmark: PnP-PDS iterations/s on batch=256 RGB 256x256 (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--size S]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
+
+A "step" is one PnP-PDS iteration (iteration.py:48-52, ours-A with the blur operator,
+blur_1.mat, sigma=0.01, real DnCNN_nobn_nch_3_nlev_0.01 weights) over a batch of 256
+synthetic RGB 256x256 images per GPU, inputs resident in HBM.  Images are independent, so
+ranks process disjoint shards with no data-path collective (weak scaling: 256 images per
+GPU).  ``value`` = image-iterations/s over the whole job (sum over ranks / max rank time).
+
+Also reported: ``roofline`` of the dominant kernel (conv_body, MFMA-bound: algorithmic
+FLOPs / HIP-event duration vs the fp16 dense MFMA peak), HBM fractions of the fused
+prox/operator kernels, PSNR delta vs the CPU oracle on image 0, and ``cpu_baseline``: the
+oracle restatement of the reference's test_iter timed on this host (rank 0, N=1 only).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "pnp-pds_amd"))
+sys.path.insert(0, REPO)
+
+METRIC = "PDS iters/sec, batch=256 RGB 256×256, 1/2/4/8 GPU; PSNR Δ vs ref"
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
+FP16_PEAK_TFLOPS = 2500.0      # dense fp16/bf16 MFMA (spec, no sparsity)
+ARCH = "DnCNN_nobn_nch_3_nlev_0.01"
+GAMMA1 = GAMMA2 = 0.99         # main.py:144-147 / ideas/param_memo.py:7
+ALPHA_N = 0.95
+SIGMA = 0.01
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def synthetic_batch(B, C, H, W, seed):
+    """Structured synthetic images in [0,1] (gradients, sinusoids, rectangles), float32."""
+    rng = np.random.default_rng(seed)
+    yy, xx = np.meshgrid(np.linspace(0, 1, H, dtype=np.float32), np.linspace(0, 1, W, dtype=np.float32),
+                         indexing="ij")
+    out = np.empty((B, C, H, W), np.float32)
+    for b in range(B):
+        f = rng.uniform(1, 6, (C, 2)).astype(np.float32)
+        ph = rng.uniform(0, 6.28, C).astype(np.float32)
+        for c in range(C):
+            img = 0.45 + 0.25 * np.sin(2 * np.pi * f[c, 0] * xx + ph[c]) * np.cos(2 * np.pi * f[c, 1] * yy) \
+                + 0.2 * (xx - 0.5)
+            for _ in range(3):
+                y0, x0 = rng.integers(0, H - H // 4), rng.integers(0, W - W // 4)
+                img[y0:y0 + rng.integers(4, H // 4), x0:x0 + rng.integers(4, W // 4)] += rng.uniform(-0.3, 0.3)
+            out[b, c] = np.clip(img, 0, 1)
+    return out
+
+
+def conv_flops_per_launch(B, H, W):
+    return 2.0 * 64 * 64 * 9 * B * H * W
+
+
+def prox_bytes(B, C, H, W):
+    """Algorithmic HBM bytes per launch of the fused ours-A passes."""
+    n = B * C * H * W
+    npx = B * H * W
+    return {
+        "k1_primal_pre": 4 * n * 3 + 8 * npx,      # read x, y; write u32; write u16 (8 B/pixel)
+        "k2_dual": 4 * n * 6,                      # read x+, x, y, xobs, xtrue; write v
+        "k3_dual": 4 * n * 3,                      # read v, xobs; write y
+    }
+
+
+def cpu_baseline(x_true, x_obs, h, budget_s, max_iter):
+    """Oracle restatement of test_iter (numpy FFT + torch-CPU conv, all host cores) on image 0."""
+    import torch
+    from oracle import pnp_oracle as O
+    from pnppds.weights import resolve_weights
+    torch.set_num_threads(os.cpu_count() or 1)
+    den = O.OracleDenoiser(resolve_weights(ARCH, 3))
+    phi, adj = O.observation_operators("blur", h)
+    xo = x_obs.astype(np.float64)
+    O.test_iter(xo, xo, x_true, phi, adj, GAMMA1, GAMMA2, 1.0, ALPHA_N, 1.0, 15, 15, 0.1, SIGMA, 0.0, 300, den, 1,
+                "A-Proposed", 3, 0.8)                                            # warm-up
+    t = time.perf_counter()                                                      # size the sample
+    O.test_iter(xo, xo, x_true, phi, adj, GAMMA1, GAMMA2, 1.0, ALPHA_N, 1.0, 15, 15, 0.1, SIGMA, 0.0, 300, den, 2,
+                "A-Proposed", 3, 0.8)
+    per = (time.perf_counter() - t) / 2
+    n_total = int(min(max_iter, max(2, budget_s / per)))
+    t = time.perf_counter()
+    res = O.test_iter(xo, xo, x_true, phi, adj, GAMMA1, GAMMA2, 1.0, ALPHA_N, 1.0, 15, 15, 0.1, SIGMA, 0.0, 300,
+                      den, n_total, "A-Proposed", 3, 0.8)
+    el = time.perf_counter() - t
+    return n_total / el, n_total, res[3], torch.get_num_threads()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=256, help="images per GPU")
+    ap.add_argument("--size", type=int, default=256)
+    ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU-baseline work")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--profile", type=int, default=1, help="HIP-event per-kernel timing in the timed region")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", init_method="env://")
+    from pnppds import _lib
+    from pnppds.iteration import make_params
+    from pnppds.operators import load_blur_kernel
+    from pnppds.weights import resolve_weights
+
+    B, C, H, W = args.batch, 3, args.size, args.size
+    K, Wm = args.steps, args.warmup
+    ctx = _lib.Context(local)
+    ctx.set_denoiser(resolve_weights(ARCH, 3))
+    h = load_blur_kernel("blur_1")
+    ctx.set_operator(_lib.OP_BLUR, h=h)
+
+    # ---- synthetic inputs, degraded on the device: x_obs = Phi(x_true) + sigma * n -------------
+    t0 = time.perf_counter()
+    x_true = synthetic_batch(B, C, H, W, seed=1000 * rank + 1)
+    d_true = torch.from_numpy(x_true).cuda(local)
+    d_obs = torch.empty_like(d_true)
+    ctx.op_phi(d_true.data_ptr(), d_obs.data_ptr(), B, C, H, W)
+    ctx.synchronize()
+    gen = torch.Generator(device=f"cuda:{local}").manual_seed(1234 + rank)
+    d_obs += SIGMA * torch.randn(d_obs.shape, device=f"cuda:{local}", generator=gen)
+    torch.cuda.synchronize()
+    log(f"[rank {rank}] inputs ready in {time.perf_counter() - t0:.1f}s")
+
+    cap = Wm + K
+    prm = make_params(GAMMA1, GAMMA2, 1.0, ALPHA_N, 1.0, 15, 15, 0.1, SIGMA, 0.0, 300, 0.8, True)
+    ctx.solver_setup(_lib.METHOD_A, prm, B, C, H, W, cap)
+    ctx.solver_load_device(d_obs.data_ptr(), d_obs.data_ptr(), d_true.data_ptr())   # x_0 = x_obs (main.py:62)
+    ctx.solver_iterate(Wm)
+    ctx.synchronize()
+    torch.cuda.synchronize()
+
+    # ---- timed region ------------------------------------------------------------------------
+    if args.profile:
+        ctx.profile_enable(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    ctx.solver_iterate(K)
+    ctx.synchronize()
+    torch.cuda.synchronize()
+    t_el = time.perf_counter() - t_start
+    if world > 1:
+        dist.barrier()
+        tt = torch.tensor([t_el], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t_el = float(tt.item())
+    prof = ctx.profile_read() if args.profile else {}
+    x_out, s_out, c_hist, psnr_hist = ctx.solver_fetch()
+
+    value = B * world * K / t_el
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": round(value, 2), "unit": "image-iterations/s",
+            "n_gpus": world, "steps": K, "warmup": Wm,
+            "ms_per_step": round(1e3 * t_el / K, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "fp16-mfma/fp32-acc+state",
+            "data": "synthetic structured RGB images, x_obs = blur_1(x_true) + 0.01 N(0,1) on device; real "
+                    "DnCNN_nobn_nch_3_nlev_0.01 weights",
+            "config": {"workload": f"ours-A (A-Proposed) blur, batch={B}/GPU RGB {H}x{W}", "global_batch": B * world,
+                       "image": f"{C}x{H}x{W}", "deg_op": "blur_1", "method": "ours-A",
+                       "parallelism": f"dp{world} (independent image shards, no collective)"},
+            "batch_iters_per_s": round(K / t_el, 3),
+        }
+        if prof:
+            kt = {k: round(v[0], 4) for k, v in prof.items()}
+            line["kernel_ms"] = kt
+            body_ms = prof["conv_body"][0]
+            fl = conv_flops_per_launch(B, H, W)
+            ach = fl / (body_ms * 1e-3) / 1e12
+            line["roofline"] = {"kernel": "conv_body (64->64 3x3 implicit GEMM, fp16 MFMA)", "bound": "mfma",
+                                "achieved": round(ach, 1), "peak": FP16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                                "frac": round(ach / FP16_PEAK_TFLOPS, 4), "traffic": None,
+                                "flops_per_launch": fl}
+            pb = prox_bytes(B, C, H, W)
+            line["prox_hbm"] = {k: {"GB/s": round(pb[k] / (prof[k][0] * 1e-3) / 1e9, 1),
+                                    "frac": round(pb[k] / (prof[k][0] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+                                for k in pb if k in prof}
+        line["psnr_img0_db"] = [round(float(psnr_hist[0, 0]), 4), round(float(psnr_hist[0, cap - 1]), 4)]
+        if world == 1 and not args.no_cpu_baseline:
+            rate, n_cpu, ps_cpu, thr = cpu_baseline(x_true[0], d_obs[0].cpu().numpy(), h, args.cpu_budget, cap)
+            line["cpu_baseline"] = {"value": round(rate, 3), "unit": "image-iterations/s", "cores": thr,
+                                    "kind": "port",
+                                    "sample": f"oracle test_iter (numpy FFT blur + torch-CPU conv), image 0, "
+                                              f"{n_cpu} iterations after 1 warm-up"}
+            line["psnr_delta_db_vs_oracle"] = round(float(np.max(np.abs(ps_cpu - psnr_hist[0, :n_cpu]))), 5)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

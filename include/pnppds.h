@@ -1,0 +1,156 @@
+/*
+ * pnppds.h — C ABI of the MI355X-native PnP-PDS inner loop (libpnppds.so).
+ *
+ * Drop-in boundary for the reference's solver path (yodai49/PnP-PDS):
+ *   iteration.test_iter            iteration.py:10-196       -> pnp_run / pnp_solver_*
+ *   get_observation_operators      operators.py:60-79        -> pnp_set_operator
+ *   Denoiser(file_name, ch)        models/denoiser.py:9-32   -> pnp_set_denoiser
+ *   Denoiser.denoise / apply_model models/denoiser.py:14-46  -> pnp_op_denoise
+ *   get_blur_operator / _adj_      operators.py:7-38         -> pnp_op_phi / pnp_op_adj_phi
+ *   get_random_sampling_operator   operators.py:40-58        -> pnp_op_phi / pnp_op_adj_phi
+ *   proj_l2_ball                   operators.py:102-108      -> pnp_op_proj_l2_ball
+ *   proj_l1_ball                   operators.py:94-100       -> pnp_op_proj_l1_ball
+ *   prox_GKL                       operators.py:114-115      -> pnp_op_prox_gkl
+ *   eval_psnr                      utils/utils_eval.py:4-7   -> pnp_op_psnr
+ *
+ * Conventions
+ *   - Images are B x C x H x W, C-contiguous float32 (the reference's (C,H,W) numpy
+ *     layout with a leading batch axis).  C in {1, 3} (any C <= 4 works).
+ *   - Host pointers are borrowed for the duration of the call; the library copies.
+ *   - Device pointers (pnp_op_*) are hipMalloc'd memory on the context's device.
+ *   - Every entry returns PNP_OK (0) or a negative PNP_E_* code; pnp_last_error()
+ *     returns a message for the last failure on that context (or the thread, if the
+ *     context is NULL).
+ *   - A context is bound to one device and is not thread-safe.  Different contexts
+ *     may be driven from different host threads (one per GPU).
+ *   - No CPU fallback: without a usable HIP device every compute entry fails.
+ */
+#ifndef PNPPDS_H
+#define PNPPDS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PNP_ABI_VERSION 1
+
+typedef struct pnp_ctx pnp_ctx;
+
+enum pnp_status {
+  PNP_OK = 0,
+  PNP_E_ARG = -1,         /* bad argument / shape                                     */
+  PNP_E_UNSUPPORTED = -2, /* method / operator / denoiser shape not supported          */
+  PNP_E_HIP = -3,         /* HIP runtime error (message has the hipError string)      */
+  PNP_E_OOM = -4,         /* device allocation failed                                 */
+  PNP_E_STATE = -5        /* call out of order (e.g. iterate before load)             */
+};
+
+/* iteration.py:48-63 ('A-Proposed' / 'B-Proposed' / 'C-Proposed'; README: ours-A/B/C)
+ * and iteration.py:127-132 ('comparisonB-2', ADMM inner steps of algorithm/admm.py)   */
+enum pnp_method {
+  PNP_METHOD_A = 0,       /* Gaussian noise, l2-ball data constraint                  */
+  PNP_METHOD_B = 1,       /* Gaussian + sparse noise, l2 ball + l1 ball on s           */
+  PNP_METHOD_C = 2,       /* Poisson noise, generalised-KL prox                       */
+  PNP_METHOD_ADMM_B2 = 3  /* comparisonB-2                                            */
+};
+
+/* operators.py:60-79 */
+enum pnp_operator_kind {
+  PNP_OP_ID = 0,
+  PNP_OP_BLUR = 1,            /* centred circular convolution with h (kh x kw)        */
+  PNP_OP_RANDOM_SAMPLING = 2  /* pointwise 0/1 keep-mask shared by all channels      */
+};
+
+enum pnp_activation { PNP_ACT_LEAKY_RELU = 0 /* slope 0.01 */, PNP_ACT_RELU = 1 };
+
+enum pnp_precision {
+  PNP_PREC_FP16 = 0  /* fp16 MFMA operands, fp32 accumulation (default)            */
+};
+
+/* Scalar parameters of iteration.test_iter (iteration.py:10), same names/meaning. */
+typedef struct pnp_params {
+  double gamma1, gamma2;          /* PDS step sizes                                   */
+  double alpha_s, alpha_n;        /* l1-ball / l2-ball radius factors                  */
+  double my_lambda;               /* GKL weight (C-Proposed)                           */
+  int32_t m1, m2;                 /* ADMM inner iterations (comparisonB-2)             */
+  double gamma_in_admm_step1;     /* unused by the supported methods (kept for parity) */
+  double gaussian_nl, sp_nl;      /* sigma, salt-and-pepper rate                       */
+  double poisson_alpha;           /* Poisson scale                                     */
+  double r;                       /* sampling rate; also scales the B-method balls     */
+  int32_t record_metrics;         /* 1: c_n and PSNR every iteration (iteration.py:187-188) */
+} pnp_params;
+
+/* ---- library / context -------------------------------------------------------- */
+int pnp_abi_version(void);
+int pnp_device_count(int* count);
+int pnp_create(int device, pnp_ctx** out);
+int pnp_destroy(pnp_ctx* ctx);
+const char* pnp_last_error(const pnp_ctx* ctx);
+int pnp_synchronize(pnp_ctx* ctx);
+
+/* Denoiser (models/denoiser.py:23-32 + basic_models.py:8-38, or the KAIR DnCNN of
+ * network_dncnn.py:42-77).  `params` = [w0, b0, w1, b1, ...] in forward order, each
+ * w_i in PyTorch layout (cout, cin, 3, 3) float32.  Layer 0: channels -> width, the
+ * last layer: width -> channels, all others width -> width.  Only width == 64.
+ * residual_sign: +1 => out = net(x) + x (simple_CNN), -1 => out = x - net(x) (KAIR).
+ * clamp_io: 1 => clamp input and output to [0,1] (denoiser.py:40,42).            */
+int pnp_set_denoiser(pnp_ctx* ctx, int channels, int depth, int width, const float* params,
+                     size_t n_params, int activation, int residual_sign, int clamp_io);
+int pnp_set_precision(pnp_ctx* ctx, int precision);
+
+/* Observation operator (operators.py:60-79).  BLUR: h is kh x kw float64 row-major
+ * (blur_models/blur_1.mat: 19x19); RANDOM_SAMPLING: keep_mask is H x W uint8 (1 keeps
+ * the pixel; the reference drops RandomState(1234).permutation(H*W)[:round(H*W*(1-r))]).
+ * ID: both NULL.                                                                  */
+int pnp_set_operator(pnp_ctx* ctx, int kind, const double* h, int kh, int kw,
+                     const uint8_t* keep_mask, int H, int W);
+
+/* ---- whole solver (iteration.test_iter) ---------------------------------------- */
+/* Batched test_iter: B independent images.  x0/xobs: B*C*H*W float32; xtrue may be
+ * NULL (then psnr_out is NaN).  Outputs (any may be NULL): x_out, s_out (= s + 0.5 as
+ * iteration.py:196 returns), c_out and psnr_out (B x max_iter float64, row-major),
+ * avg_time_s = wall seconds per iteration on the device.                            */
+int pnp_run(pnp_ctx* ctx, int method, const pnp_params* params, int B, int C, int H, int W,
+            const float* x0, const float* xobs, const float* xtrue, int max_iter,
+            float* x_out, float* s_out, double* c_out, double* psnr_out, double* avg_time_s);
+
+/* Staged form of pnp_run, with state resident in HBM between calls (bench / drivers). */
+int pnp_solver_setup(pnp_ctx* ctx, int method, const pnp_params* params, int B, int C, int H,
+                     int W, int metrics_capacity);
+int pnp_solver_load(pnp_ctx* ctx, const float* x0, const float* xobs, const float* xtrue);
+int pnp_solver_load_device(pnp_ctx* ctx, const float* d_x0, const float* d_xobs,
+                           const float* d_xtrue);
+int pnp_solver_iterate(pnp_ctx* ctx, int n_iter);   /* enqueue only (async) */
+int pnp_solver_fetch(pnp_ctx* ctx, float* x_out, float* s_out, double* c_out, double* psnr_out);
+int pnp_solver_iterations_done(pnp_ctx* ctx, int* n);
+/* Device pointers of the solver's primal / dual state (read-only views, B*C*H*W). */
+int pnp_solver_state(pnp_ctx* ctx, const float** d_x, const float** d_y, const float** d_s);
+
+/* Per-kernel timing of the last iterate() call: fills up to `cap` entries of
+ * name/avg-ms pairs measured with hipEvents on the solver stream (profiling aid).   */
+int pnp_profile_enable(pnp_ctx* ctx, int enable);
+int pnp_profile_read(pnp_ctx* ctx, int cap, const char** names, double* avg_ms, int* calls, int* n);
+
+/* ---- single operators on device pointers (stream NULL => context stream) -------- */
+int pnp_op_phi(pnp_ctx* ctx, const float* x, float* y, int B, int C, int H, int W, void* stream);
+int pnp_op_adj_phi(pnp_ctx* ctx, const float* x, float* y, int B, int C, int H, int W, void* stream);
+/* per image b (n elements each): out = P_{B(x0_b, eps)}(x_b), eps = sqrt(n(1-sp_nl)) r alpha_n sigma */
+int pnp_op_proj_l2_ball(pnp_ctx* ctx, const float* x, const float* x0, float* out, int B, int64_t n,
+                        double alpha_n, double gaussian_nl, double sp_nl, double r, void* stream);
+/* per image: projection onto {|s|_1 <= alpha_s * n * sp_nl * r / 2} */
+int pnp_op_proj_l1_ball(pnp_ctx* ctx, const float* x, float* out, int B, int64_t n, double alpha_s,
+                        double sp_nl, double r, void* stream);
+int pnp_op_prox_gkl(pnp_ctx* ctx, const float* x, const float* x0, float* out, int64_t count,
+                    double gamma, double alpha, void* stream);
+int pnp_op_denoise(pnp_ctx* ctx, const float* x, float* out, int B, int C, int H, int W, void* stream);
+/* psnr_out: host array of B doubles (synchronous). */
+int pnp_op_psnr(pnp_ctx* ctx, const float* x_true, const float* x, int B, int64_t n, double* psnr_out,
+                void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PNPPDS_H */

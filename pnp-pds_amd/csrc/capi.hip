@@ -1,0 +1,770 @@
+// C ABI (include/pnppds.h): device context, denoiser/operator state and the on-device
+// PnP-PDS solver loop.  Host orchestration only; kernels live in ops.hip / conv.hip.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/pnppds.h"
+#include "kernels.h"
+
+
+using namespace pnp;
+
+namespace {
+
+thread_local std::string g_thread_err;
+
+struct PnpError {
+  int code;
+};
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  long long geom = -1;   // zero-border buffers: the (B,H,W) their padding was zeroed for
+};
+
+struct ProfEntry {
+  const char* name;
+  hipEvent_t a, b;
+};
+
+}  // namespace
+
+struct pnp_ctx {
+  int device = 0;
+  int num_cus = 256;
+  hipStream_t stream = nullptr;
+  std::string err;
+  std::vector<DevBuf*> owned;
+
+  // denoiser
+  int den_C = 0, den_depth = 0, den_act = 0, den_residual = 1, den_clamp = 1;
+  bool den_ready = false;
+  DevBuf head_w, head_b, body_w, body_b, tail_w, tail_b;
+
+  // operator
+  int op_kind = PNP_OP_ID;
+  int op_H = 0, op_W = 0;
+  int op_ntaps = 0, op_R = 0;
+  DevBuf taps_fwd, taps_adj, mask;
+
+  // solver
+  int method = -1, B = 0, C = 0, H = 0, W = 0, cap = 0, it = 0;
+  bool loaded = false, has_true = false;
+  pnp_params prm{};
+  int cur = 0;
+  DevBuf x[2], y, s, w, xobs, xtrue, u32, u16, act[2], partials, metrics, theta;
+
+  // scratch for single ops
+  DevBuf scr_u32, scr_u16, scr_act[2], scr_part, scr_theta;
+
+  // profiling
+  bool prof = false;
+  std::vector<ProfEntry> prof_log;
+  std::vector<hipEvent_t> ev_pool;
+  size_t ev_used = 0;
+};
+
+namespace {
+
+void fail(pnp_ctx* ctx, int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  if (ctx) ctx->err = buf;
+  g_thread_err = buf;
+  throw PnpError{code};
+}
+
+#define HIPCHK(ctx, expr)                                                                     \
+  do {                                                                                        \
+    hipError_t e_ = (expr);                                                                   \
+    if (e_ != hipSuccess) fail(ctx, PNP_E_HIP, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), \
+                               __FILE__, __LINE__);                                           \
+  } while (0)
+
+void check_launch(pnp_ctx* ctx, const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) fail(ctx, PNP_E_HIP, "launch %s: %s", what, hipGetErrorString(e));
+}
+
+template <class F>
+int guarded(pnp_ctx* ctx, F&& f) {
+  try {
+    if (ctx) {
+      hipError_t e = hipSetDevice(ctx->device);
+      if (e != hipSuccess) fail(ctx, PNP_E_HIP, "hipSetDevice(%d): %s", ctx->device, hipGetErrorString(e));
+    }
+    f();
+    return PNP_OK;
+  } catch (const PnpError& e) {
+    return e.code;
+  } catch (const std::exception& e) {
+    if (ctx) ctx->err = e.what();
+    g_thread_err = e.what();
+    return PNP_E_ARG;
+  }
+}
+
+void ensure(pnp_ctx* ctx, DevBuf& b, size_t bytes, bool zero = false) {
+  if (bytes == 0) bytes = 16;
+  if (b.p && b.bytes >= bytes) return;
+  if (b.p) {
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    HIPCHK(ctx, hipFree(b.p));
+    b.p = nullptr;
+    b.bytes = 0;
+  }
+  hipError_t e = hipMalloc(&b.p, bytes);
+  if (e != hipSuccess) fail(ctx, PNP_E_OOM, "hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
+  b.bytes = bytes;
+  b.geom = -1;
+  if (zero) HIPCHK(ctx, hipMemsetAsync(b.p, 0, bytes, ctx->stream));
+}
+
+void release(DevBuf& b) {
+  if (b.p) (void)hipFree(b.p);
+  b.p = nullptr;
+  b.bytes = 0;
+}
+
+template <class T>
+T* P(DevBuf& b) {
+  return reinterpret_cast<T*>(b.p);
+}
+
+hipStream_t pick_stream(pnp_ctx* ctx, void* stream) {
+  return stream ? reinterpret_cast<hipStream_t>(stream) : ctx->stream;
+}
+
+// -------- profiling (hipEvents around each launch group on the solver stream) ---------
+hipEvent_t next_event(pnp_ctx* ctx) {
+  if (ctx->ev_used == ctx->ev_pool.size()) {
+    hipEvent_t e;
+    HIPCHK(ctx, hipEventCreate(&e));
+    ctx->ev_pool.push_back(e);
+  }
+  return ctx->ev_pool[ctx->ev_used++];
+}
+
+struct ProfScope {
+  pnp_ctx* ctx;
+  const char* name;
+  hipStream_t st;
+  hipEvent_t a = nullptr;
+  ProfScope(pnp_ctx* c, const char* n, hipStream_t s) : ctx(c), name(n), st(s) {
+    if (ctx->prof) {
+      a = next_event(ctx);
+      HIPCHK(ctx, hipEventRecord(a, st));
+    }
+  }
+  ~ProfScope() noexcept(false) {
+    if (ctx->prof) {
+      hipEvent_t b = next_event(ctx);
+      HIPCHK(ctx, hipEventRecord(b, st));
+      ctx->prof_log.push_back({name, a, b});
+    }
+  }
+};
+
+// -------- operator descriptor --------------------------------------------------------
+OpDesc op_desc(pnp_ctx* ctx) {
+  OpDesc d;
+  d.kind = ctx->op_kind;
+  d.taps_fwd = P<const int4>(ctx->taps_fwd);
+  d.taps_adj = P<const int4>(ctx->taps_adj);
+  d.ntaps = ctx->op_ntaps;
+  d.R = ctx->op_R;
+  d.mask = P<const uint8_t>(ctx->mask);
+  return d;
+}
+
+void check_operator_shape(pnp_ctx* ctx, int H, int W) {
+  if (ctx->op_kind == PNP_OP_RANDOM_SAMPLING && (H != ctx->op_H || W != ctx->op_W))
+    fail(ctx, PNP_E_ARG, "random_sampling mask is %dx%d, image is %dx%d", ctx->op_H, ctx->op_W, H, W);
+  if (ctx->op_kind == PNP_OP_BLUR && (H < 1 || W < 1))
+    fail(ctx, PNP_E_ARG, "bad image size");
+}
+
+// -------- denoiser forward: u16 (padded NHWC4) + u32 (NCHW) -> xout --------------------
+size_t act_bytes(int B, int H, int W, int ch) {
+  // + slack: partial tiles read up to 8 rows / 34 pixels past the last image
+  return ((size_t)B * (H + 2) * (W + 2) + (size_t)10 * (W + 2) + 64) * ch * sizeof(half_t);
+}
+
+void run_denoiser(pnp_ctx* ctx, const half_t* u16, const float* u32, float* xout, DevBuf (&act)[2], int B, int H,
+                  int W, hipStream_t st) {
+  if (!ctx->den_ready) fail(ctx, PNP_E_STATE, "denoiser not set (pnp_set_denoiser)");
+  const ConvShape s = make_conv_shape(B, H, W);
+  {
+    ProfScope ps(ctx, "conv_head", st);
+    launch_conv_head(u16, P<half_t>(act[0]), ctx->head_w.p, P<float>(ctx->head_b), s, ctx->den_act, ctx->num_cus,
+                     st);
+    check_launch(ctx, "conv_head");
+  }
+  int cur = 0;
+  const size_t wstride = kBodyWBytes;
+  for (int l = 0; l < ctx->den_depth - 2; ++l) {
+    ProfScope ps(ctx, "conv_body", st);
+    launch_conv_body(P<half_t>(act[cur]), P<half_t>(act[cur ^ 1]), (const char*)ctx->body_w.p + l * wstride,
+                     P<float>(ctx->body_b) + l * kWidth, s, ctx->den_act, ctx->num_cus, st);
+    check_launch(ctx, "conv_body");
+    cur ^= 1;
+  }
+  {
+    ProfScope ps(ctx, "conv_tail", st);
+    launch_conv_tail(P<half_t>(act[cur]), u32, xout, ctx->tail_w.p, P<float>(ctx->tail_b), s, ctx->den_C,
+                     ctx->den_residual, ctx->den_clamp, ctx->num_cus, st);
+    check_launch(ctx, "conv_tail");
+  }
+}
+
+// Padded activation images: the one-pixel border must be zero for the geometry in use.
+// Kernels never write the border, so a buffer is zeroed once per (B, H, W) it serves;
+// reusing it for another geometry (whose border lands on stale interior data) re-zeroes.
+void ensure_padded(pnp_ctx* ctx, DevBuf& b, int B, int H, int W, int ch, hipStream_t st) {
+  const size_t bytes = act_bytes(B, H, W, ch);
+  const long long geom = ((long long)B << 40) ^ ((long long)H << 20) ^ (long long)W;
+  ensure(ctx, b, bytes);
+  if (b.geom != geom) {
+    HIPCHK(ctx, hipMemsetAsync(b.p, 0, bytes, st));
+    b.geom = geom;
+  }
+}
+
+void ensure_act(pnp_ctx* ctx, DevBuf (&act)[2], int B, int H, int W, hipStream_t st) {
+  for (int i = 0; i < 2; ++i) ensure_padded(ctx, act[i], B, H, W, kWidth, st);
+}
+
+// -------- one solver iteration -------------------------------------------------------
+double l2_eps(pnp_ctx* ctx, size_t n) {
+  const pnp_params& p = ctx->prm;
+  const double r = ctx->method == PNP_METHOD_B ? p.r : 1.0;   // A passes no r (iteration.py:52)
+  return std::sqrt((double)n * (1.0 - p.sp_nl)) * r * p.alpha_n * p.gaussian_nl;
+}
+
+void solver_iteration(pnp_ctx* ctx) {
+  hipStream_t st = ctx->stream;
+  const pnp_params& p = ctx->prm;
+  const int B = ctx->B, C = ctx->C, H = ctx->H, W = ctx->W;
+  const size_t n = (size_t)C * H * W;
+  const OpDesc od = op_desc(ctx);
+  float* xo = P<float>(ctx->x[ctx->cur]);
+  float* xn = P<float>(ctx->x[ctx->cur ^ 1]);
+  const bool mb = ctx->method == PNP_METHOD_B;
+  const int record = p.record_metrics && ctx->it < ctx->cap;
+  {
+    ProfScope ps(ctx, "k1_primal_pre", st);
+    launch_k1(od.kind, xo, P<float>(ctx->y), P<float>(ctx->s), P<float>(ctx->u32), P<half_t>(ctx->u16),
+              P<float>(ctx->w), od, B, C, H, W, (float)p.gamma1, ctx->den_clamp, mb, st);
+    check_launch(ctx, "k1");
+  }
+  if (mb) {
+    ProfScope ps(ctx, "l1_select", st);
+    const double eta = p.alpha_s * (double)n * p.sp_nl * p.r * 0.5;   // operators.py:96
+    launch_l1_select(P<float>(ctx->w), P<float>(ctx->theta), B, n, eta, st);
+    check_launch(ctx, "l1_select");
+  }
+  run_denoiser(ctx, P<half_t>(ctx->u16), P<float>(ctx->u32), xn, ctx->act, B, H, W, st);
+  {
+    ProfScope ps(ctx, "k2_dual", st);
+    const double gkl_gamma = p.my_lambda / p.gamma2;   // iteration.py:63
+    launch_k2(od.kind, ctx->method, xn, xo, P<float>(ctx->y), P<float>(ctx->xobs),
+              ctx->has_true ? P<float>(ctx->xtrue) : nullptr, P<float>(ctx->s), P<float>(ctx->w),
+              P<float>(ctx->theta), P<double>(ctx->partials), od, B, C, H, W, p.gamma2, gkl_gamma,
+              p.poisson_alpha, record, st);
+    check_launch(ctx, "k2");
+  }
+  {
+    ProfScope ps(ctx, "k3_dual", st);
+    launch_k3(ctx->method, P<float>(ctx->y), P<float>(ctx->xobs), P<double>(ctx->partials), B, C, H, W, p.gamma2,
+              l2_eps(ctx, n), P<double>(ctx->metrics), ctx->it, ctx->cap, record, ctx->has_true, st);
+    check_launch(ctx, "k3");
+  }
+  ctx->cur ^= 1;
+  ctx->it += 1;
+}
+
+void solver_setup(pnp_ctx* ctx, int method, const pnp_params* params, int B, int C, int H, int W, int cap) {
+  if (!params) fail(ctx, PNP_E_ARG, "params is NULL");
+  if (method < PNP_METHOD_A || method > PNP_METHOD_C)
+    fail(ctx, PNP_E_UNSUPPORTED, "method %d not supported on device", method);
+  if (B < 1 || C < 1 || C > kMaxC || H < 1 || W < 1) fail(ctx, PNP_E_ARG, "bad shape B=%d C=%d H=%d W=%d", B, C, H, W);
+  if (!ctx->den_ready) fail(ctx, PNP_E_STATE, "denoiser not set");
+  if (ctx->den_C != C) fail(ctx, PNP_E_ARG, "denoiser has %d channels, images have %d", ctx->den_C, C);
+  check_operator_shape(ctx, H, W);
+  if (ctx->op_kind == PNP_OP_BLUR && (ctx->op_R > H || ctx->op_R > W))
+    fail(ctx, PNP_E_ARG, "blur kernel radius %d larger than the image", ctx->op_R);
+  if (params->gamma2 == 0.0) fail(ctx, PNP_E_ARG, "gamma2 must be non-zero");
+  ctx->method = method;
+  ctx->prm = *params;
+  ctx->B = B; ctx->C = C; ctx->H = H; ctx->W = W;
+  ctx->cap = std::max(cap, 0);
+  const size_t N = (size_t)B * C * H * W, fb = N * sizeof(float);
+  for (int i = 0; i < 2; ++i) ensure(ctx, ctx->x[i], fb);
+  ensure(ctx, ctx->y, fb);
+  ensure(ctx, ctx->s, fb);
+  ensure(ctx, ctx->xobs, fb);
+  ensure(ctx, ctx->xtrue, fb);
+  ensure(ctx, ctx->u32, fb);
+  if (method == PNP_METHOD_B) ensure(ctx, ctx->w, fb);
+  ensure_padded(ctx, ctx->u16, B, H, W, 4, ctx->stream);
+  ensure_act(ctx, ctx->act, B, H, W, ctx->stream);
+  ensure(ctx, ctx->partials, (size_t)B * partial_tiles(H, W) * 4 * sizeof(double));
+  ensure(ctx, ctx->metrics, (size_t)B * std::max(ctx->cap, 1) * 2 * sizeof(double));
+  ensure(ctx, ctx->theta, (size_t)B * sizeof(float));
+  ctx->loaded = false;
+  ctx->it = 0;
+}
+
+void solver_reset_state(pnp_ctx* ctx) {
+  const size_t fb = (size_t)ctx->B * ctx->C * ctx->H * ctx->W * sizeof(float);
+  HIPCHK(ctx, hipMemsetAsync(ctx->y.p, 0, fb, ctx->stream));          // iteration.py:24
+  HIPCHK(ctx, hipMemsetAsync(ctx->s.p, 0, fb, ctx->stream));          // iteration.py:27
+  if (ctx->cap) {
+    std::vector<double> nanbuf((size_t)ctx->B * ctx->cap * 2, std::nan(""));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->metrics.p, nanbuf.data(), nanbuf.size() * sizeof(double), hipMemcpyHostToDevice,
+                               ctx->stream));
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  }
+  ctx->cur = 0;
+  ctx->it = 0;
+  ctx->loaded = true;
+}
+
+void solver_fetch(pnp_ctx* ctx, float* x_out, float* s_out, double* c_out, double* psnr_out) {
+  if (!ctx->loaded) fail(ctx, PNP_E_STATE, "solver not loaded");
+  const size_t N = (size_t)ctx->B * ctx->C * ctx->H * ctx->W;
+  HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  if (x_out) HIPCHK(ctx, hipMemcpy(x_out, ctx->x[ctx->cur].p, N * sizeof(float), hipMemcpyDeviceToHost));
+  if (s_out) {
+    HIPCHK(ctx, hipMemcpy(s_out, ctx->s.p, N * sizeof(float), hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < N; ++i) s_out[i] += 0.5f;                // iteration.py:196
+  }
+  if ((c_out || psnr_out) && ctx->cap) {
+    std::vector<double> m((size_t)ctx->B * ctx->cap * 2);
+    HIPCHK(ctx, hipMemcpy(m.data(), ctx->metrics.p, m.size() * sizeof(double), hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < (size_t)ctx->B * ctx->cap; ++i) {
+      if (c_out) c_out[i] = m[2 * i];
+      if (psnr_out) psnr_out[i] = m[2 * i + 1];
+    }
+  }
+}
+
+}  // namespace
+
+// =====================================================================================
+// extern "C"
+// =====================================================================================
+extern "C" {
+
+int pnp_abi_version(void) { return PNP_ABI_VERSION; }
+
+int pnp_device_count(int* count) {
+  return guarded(nullptr, [&] {
+    if (!count) fail(nullptr, PNP_E_ARG, "count is NULL");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) fail(nullptr, PNP_E_HIP, "hipGetDeviceCount: %s", hipGetErrorString(e));
+    *count = n;
+  });
+}
+
+int pnp_create(int device, pnp_ctx** out) {
+  return guarded(nullptr, [&] {
+    if (!out) fail(nullptr, PNP_E_ARG, "out is NULL");
+    *out = nullptr;
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n == 0)
+      fail(nullptr, PNP_E_HIP, "no HIP device available (%s)", hipGetErrorString(e));
+    if (device < 0 || device >= n) fail(nullptr, PNP_E_ARG, "device %d out of range (%d devices)", device, n);
+    auto* ctx = new pnp_ctx();
+    ctx->device = device;
+    try {
+      HIPCHK(ctx, hipSetDevice(device));
+      hipDeviceProp_t prop;
+      HIPCHK(ctx, hipGetDeviceProperties(&prop, device));
+      if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        fail(ctx, PNP_E_UNSUPPORTED, "device %d is %s; this library is built for gfx950 only", device,
+             prop.gcnArchName);
+      ctx->num_cus = prop.multiProcessorCount;
+      HIPCHK(ctx, hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+      HIPCHK(ctx, conv_kernels_init());
+    } catch (const PnpError&) {
+      g_thread_err = ctx->err;
+      delete ctx;
+      throw;
+    }
+    *out = ctx;
+  });
+}
+
+int pnp_destroy(pnp_ctx* ctx) {
+  if (!ctx) return PNP_OK;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  DevBuf* bufs[] = {&ctx->head_w, &ctx->head_b, &ctx->body_w, &ctx->body_b, &ctx->tail_w, &ctx->tail_b,
+                    &ctx->taps_fwd, &ctx->taps_adj, &ctx->mask, &ctx->x[0], &ctx->x[1], &ctx->y, &ctx->s,
+                    &ctx->w, &ctx->xobs, &ctx->xtrue, &ctx->u32, &ctx->u16, &ctx->act[0], &ctx->act[1],
+                    &ctx->partials, &ctx->metrics, &ctx->theta, &ctx->scr_u32, &ctx->scr_u16,
+                    &ctx->scr_act[0], &ctx->scr_act[1], &ctx->scr_part, &ctx->scr_theta};
+  for (DevBuf* b : bufs) release(*b);
+  for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+  return PNP_OK;
+}
+
+const char* pnp_last_error(const pnp_ctx* ctx) { return ctx ? ctx->err.c_str() : g_thread_err.c_str(); }
+
+int pnp_synchronize(pnp_ctx* ctx) {
+  if (!ctx) return PNP_E_ARG;
+  return guarded(ctx, [&] { HIPCHK(ctx, hipStreamSynchronize(ctx->stream)); });
+}
+
+int pnp_set_precision(pnp_ctx* ctx, int precision) {
+  if (!ctx) return PNP_E_ARG;
+  return guarded(ctx, [&] {
+    if (precision != PNP_PREC_FP16) fail(ctx, PNP_E_UNSUPPORTED, "precision %d not supported", precision);
+  });
+}
+
+int pnp_set_denoiser(pnp_ctx* ctx, int channels, int depth, int width, const float* params, size_t n_params,
+                     int activation, int residual_sign, int clamp_io) {
+  if (!ctx) return PNP_E_ARG;
+  return guarded(ctx, [&] {
+    if (width != kWidth) fail(ctx, PNP_E_UNSUPPORTED, "width %d unsupported (only 64)", width);
+    if (channels < 1 || channels > kMaxC) fail(ctx, PNP_E_UNSUPPORTED, "channels %d unsupported (1..4)", channels);
+    if (depth < 3) fail(ctx, PNP_E_UNSUPPORTED, "depth %d < 3", depth);
+    if (activation != PNP_ACT_LEAKY_RELU && activation != PNP_ACT_RELU) fail(ctx, PNP_E_ARG, "bad activation");
+    if (residual_sign != 1 && residual_sign != -1) fail(ctx, PNP_E_ARG, "residual_sign must be +1 or -1");
+    const size_t n_head = (size_t)kWidth * channels * 9 + kWidth;
+    const size_t n_body = (size_t)kWidth * kWidth * 9 + kWidth;
+    const size_t n_tail = (size_t)channels * kWidth * 9 + channels;
+    const size_t expect = n_head + (size_t)(depth - 2) * n_body + n_tail;
+    if (!params || n_params != expect)
+      fail(ctx, PNP_E_ARG, "expected %zu parameters for C=%d depth=%d, got %zu", expect, channels, depth, n_params);
+    const float* p = params;
+    std::vector<uint16_t> hw(kHeadWBytes / 2), bw((size_t)(depth - 2) * kBodyWBytes / 2), tw(kTailWBytes / 2);
+    std::vector<float> hb(kWidth), bb((size_t)(depth - 2) * kWidth), tb(kMaxC, 0.f);
+    pack_head_weights(p, channels, hw.data());
+    std::memcpy(hb.data(), p + kWidth * channels * 9, kWidth * sizeof(float));
+    p += n_head;
+    for (int l = 0; l < depth - 2; ++l) {
+      pack_body_weights(p, bw.data() + (size_t)l * kBodyWBytes / 2);
+      std::memcpy(bb.data() + (size_t)l * kWidth, p + kWidth * kWidth * 9, kWidth * sizeof(float));
+      p += n_body;
+    }
+    pack_tail_weights(p, channels, tw.data());
+    std::memcpy(tb.data(), p + channels * kWidth * 9, channels * sizeof(float));
+    ensure(ctx, ctx->head_w, hw.size() * 2);
+    ensure(ctx, ctx->head_b, hb.size() * 4);
+    ensure(ctx, ctx->body_w, bw.size() * 2);
+    ensure(ctx, ctx->body_b, bb.size() * 4);
+    ensure(ctx, ctx->tail_w, tw.size() * 2);
+    ensure(ctx, ctx->tail_b, tb.size() * 4);
+    HIPCHK(ctx, hipMemcpy(ctx->head_w.p, hw.data(), hw.size() * 2, hipMemcpyHostToDevice));
+    HIPCHK(ctx, hipMemcpy(ctx->head_b.p, hb.data(), hb.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(ctx, hipMemcpy(ctx->body_w.p, bw.data(), bw.size() * 2, hipMemcpyHostToDevice));
+    HIPCHK(ctx, hipMemcpy(ctx->body_b.p, bb.data(), bb.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(ctx, hipMemcpy(ctx->tail_w.p, tw.data(), tw.size() * 2, hipMemcpyHostToDevice));
+    HIPCHK(ctx, hipMemcpy(ctx->tail_b.p, tb.data(), tb.size() * 4, hipMemcpyHostToDevice));
+    ctx->den_C = channels;
+    ctx->den_depth = depth;
+    ctx->den_act = activation;
+    ctx->den_residual = residual_sign;
+    ctx->den_clamp = clamp_io ? 1 : 0;
+    ctx->den_ready = true;
+  });
+}
+
+int pnp_set_operator(pnp_ctx* ctx, int kind, const double* h, int kh, int kw, const uint8_t* keep_mask, int H,
+                     int W) {
+  if (!ctx) return PNP_E_ARG;
+  return guarded(ctx, [&] {
+    if (kind == PNP_OP_ID) {
+      ctx->op_kind = kind;
+      return;
+    }
+    if (kind == PNP_OP_BLUR) {
+      if (!h || kh < 1 || kw < 1) fail(ctx, PNP_E_ARG, "blur needs a kernel");
+      if (kh != kw) fail(ctx, PNP_E_UNSUPPORTED, "blur kernel must be square (operators.py:9 uses h.shape[0])");
+      // operators.py:7-38: Phi   y[i,j] = sum h[a,b] x[i - a + mf, j - b + mf], mf = (l-1)//2
+      //                    Phi^T y[i,j] = sum h[a,b] x[i + a - ma, j + b - ma], ma = l//2
+      const int l = kh, mf = (l - 1) / 2, ma = l / 2;
+      std::vector<int4> fwd, adj;
+      int R = 0;
+      for (int a = 0; a < kh; ++a)
+        for (int b = 0; b < kw; ++b) {
+          const double v = h[a * kw + b];
+          if (v == 0.0) continue;
+          const float fv = (float)v;
+          int bits;
+          std::memcpy(&bits, &fv, 4);
+          fwd.push_back(make_int4(mf - a, mf - b, bits, 0));
+          adj.push_back(make_int4(a - ma, b - ma, bits, 0));
+          R = std::max({R, std::abs(mf - a), std::abs(mf - b), std::abs(a - ma), std::abs(b - ma)});
+        }
+      if (R > 16) fail(ctx, PNP_E_UNSUPPORTED, "blur support radius %d > 16", R);
+      if (fwd.empty()) fwd.push_back(make_int4(0, 0, 0, 0)), adj.push_back(make_int4(0, 0, 0, 0));
+      ensure(ctx, ctx->taps_fwd, fwd.size() * sizeof(int4));
+      ensure(ctx, ctx->taps_adj, adj.size() * sizeof(int4));
+      HIPCHK(ctx, hipMemcpy(ctx->taps_fwd.p, fwd.data(), fwd.size() * sizeof(int4), hipMemcpyHostToDevice));
+      HIPCHK(ctx, hipMemcpy(ctx->taps_adj.p, adj.data(), adj.size() * sizeof(int4), hipMemcpyHostToDevice));
+      ctx->op_ntaps = (int)fwd.size();
+      ctx->op_R = R;
+      ctx->op_kind = kind;
+      return;
+    }
+    if (kind == PNP_OP_RANDOM_SAMPLING) {
+      if (!keep_mask || H < 1 || W < 1) fail(ctx, PNP_E_ARG, "random_sampling needs an HxW keep mask");
+      ensure(ctx, ctx->mask, (size_t)H * W);
+      HIPCHK(ctx, hipMemcpy(ctx->mask.p, keep_mask, (size_t)H * W, hipMemcpyHostToDevice));
+      ctx->op_H = H;
+      ctx->op_W = W;
+      ctx->op_kind = kind;
+      return;
+    }
+    fail(ctx, PNP_E_UNSUPPORTED, "operator kind %d", kind);
+  });
+}
+
+int pnp_solver_setup(pnp_ctx* ctx, int method, const pnp_params* params, int B, int C, int H, int W,
+                     int metrics_capacity) {
+  if (!ctx) return PNP_E_ARG;
+  return guarded(ctx, [&] { solver_setup(ctx, method, params, B, C, H, W, metrics_capacity); });
+}
+
+int pnp_solver_load(pnp_ctx* ctx, const float* x0, const float* xobs, const float* xtrue) {
+  if (!ctx) return PNP_E_ARG;
+  return guarded(ctx, [&] {
+    if (ctx->method < 0) fail(ctx, PNP_E_STATE, "pnp_solver_setup first");
+    if (!x0 || !xobs) fail(ctx, PNP_E_ARG, "x0 and xobs are required");
+    const size_t fb = (size_t)ctx->B * ctx->C * ctx->H * ctx->W * sizeof(float);
+    HIPCHK(ctx, hipMemcpy(ctx->x[0].p, x0, fb, hipMemcpyHostToDevice));
+    HIPCHK(ctx, hipMemcpy(ctx->xobs.p, xobs, fb, hipMemcpyHostToDevice));
+    ctx->has_true = xtrue != nullptr;
+    if (xtrue) HIPCHK(ctx, hipMemcpy(ctx->xtrue.p, xtrue, fb, hipMemcpyHostToDevice));
+    solver_reset_state(ctx);
+  });
+}
+
+int pnp_solver_load_device(pnp_ctx* ctx, const float* d_x0, const float* d_xobs, const float* d_xtrue) {
+  if (!ctx) return PNP_E_ARG;
+  return guarded(ctx, [&] {
+    if (ctx->method < 0) fail(ctx, PNP_E_STATE, "pnp_solver_setup first");
+    if (!d_x0 || !d_xobs) fail(ctx, PNP_E_ARG, "x0 and xobs are required");
+    const size_t fb = (size_t)ctx->B * ctx->C * ctx->H * ctx->W * sizeof(float);
+    HIPCHK(ctx, hipMemcpyAsync(ctx->x[0].p, d_x0, fb, hipMemcpyDeviceToDevice, ctx->stream));
+    HIPCHK(ctx, hipMemcpyAsync(ctx->xobs.p, d_xobs, fb, hipMemcpyDeviceToDevice, ctx->stream));
+    ctx->has_true = d_xtrue != nullptr;
+    if (d_xtrue) HIPCHK(ctx, hipMemcpyAsync(ctx->xtrue.p, d_xtrue, fb, hipMemcpyDeviceToDevice, ctx->stream));
+    solver_reset_state(ctx);
+  });
+}
+
+int pnp_solver_iterate(pnp_ctx* ctx, int n_iter) {
+  if (!ctx) return PNP_E_ARG;
+  return guarded(ctx, [&] {
+    if (!ctx->loaded) fail(ctx, PNP_E_STATE, "pnp_solver_load first");
+    if (n_iter < 0) fail(ctx, PNP_E_ARG, "n_iter < 0");
+    if (ctx->prof) {
+      ctx->prof_log.clear();
+      ctx->ev_used = 0;
+    }
+    for (int i = 0; i < n_iter; ++i) solver_iteration(ctx);
+  });
+}
+
+int pnp_solver_fetch(pnp_ctx* ctx, float* x_out, float* s_out, double* c_out, double* psnr_out) {
+  if (!ctx) return PNP_E_ARG;
+  return guarded(ctx, [&] { solver_fetch(ctx, x_out, s_out, c_out, psnr_out); });
+}
+
+int pnp_solver_iterations_done(pnp_ctx* ctx, int* n) {
+  if (!ctx || !n) return PNP_E_ARG;
+  *n = ctx->it;
+  return PNP_OK;
+}
+
+int pnp_solver_state(pnp_ctx* ctx, const float** d_x, const float** d_y, const float** d_s) {
+  if (!ctx) return PNP_E_ARG;
+  return guarded(ctx, [&] {
+    if (!ctx->loaded) fail(ctx, PNP_E_STATE, "solver not loaded");
+    if (d_x) *d_x = P<const float>(ctx->x[ctx->cur]);
+    if (d_y) *d_y = P<const float>(ctx->y);
+    if (d_s) *d_s = P<const float>(ctx->s);
+  });
+}
+
+int pnp_run(pnp_ctx* ctx, int method, const pnp_params* params, int B, int C, int H, int W, const float* x0,
+            const float* xobs, const float* xtrue, int max_iter, float* x_out, float* s_out, double* c_out,
+            double* psnr_out, double* avg_time_s) {
+  if (!ctx) return PNP_E_ARG;
+  return guarded(ctx, [&] {
+    if (max_iter < 0) fail(ctx, PNP_E_ARG, "max_iter < 0");
+    solver_setup(ctx, method, params, B, C, H, W, max_iter);
+    if (!x0 || !xobs) fail(ctx, PNP_E_ARG, "x0 and xobs are required");
+    const size_t fb = (size_t)B * C * H * W * sizeof(float);
+    HIPCHK(ctx, hipMemcpy(ctx->x[0].p, x0, fb, hipMemcpyHostToDevice));
+    HIPCHK(ctx, hipMemcpy(ctx->xobs.p, xobs, fb, hipMemcpyHostToDevice));
+    ctx->has_true = xtrue != nullptr;
+    if (xtrue) HIPCHK(ctx, hipMemcpy(ctx->xtrue.p, xtrue, fb, hipMemcpyHostToDevice));
+    solver_reset_state(ctx);
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int i = 0; i < max_iter; ++i) solver_iteration(ctx);
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (avg_time_s) *avg_time_s = max_iter ? dt / max_iter : 0.0;
+    solver_fetch(ctx, x_out, s_out, c_out, psnr_out);
+  });
+}
+
+int pnp_profile_enable(pnp_ctx* ctx, int enable) {
+  if (!ctx) return PNP_E_ARG;
+  ctx->prof = enable != 0;
+  ctx->prof_log.clear();
+  ctx->ev_used = 0;
+  return PNP_OK;
+}
+
+int pnp_profile_read(pnp_ctx* ctx, int cap, const char** names, double* avg_ms, int* calls, int* n) {
+  if (!ctx || !n) return PNP_E_ARG;
+  return guarded(ctx, [&] {
+    HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+    std::vector<std::string> keys;
+    std::vector<double> tot;
+    std::vector<int> cnt;
+    for (const ProfEntry& e : ctx->prof_log) {
+      float ms = 0;
+      HIPCHK(ctx, hipEventElapsedTime(&ms, e.a, e.b));
+      size_t k = 0;
+      while (k < keys.size() && keys[k] != e.name) ++k;
+      if (k == keys.size()) { keys.push_back(e.name); tot.push_back(0); cnt.push_back(0); }
+      tot[k] += ms;
+      cnt[k] += 1;
+    }
+    const int m = (int)keys.size();
+    for (int i = 0; i < m && i < cap; ++i) {
+      if (names) {
+        // names point at string literals from ProfScope (static storage)
+        for (const ProfEntry& e : ctx->prof_log)
+          if (keys[i] == e.name) { names[i] = e.name; break; }
+      }
+      if (avg_ms) avg_ms[i] = tot[i] / cnt[i];
+      if (calls) calls[i] = cnt[i];
+    }
+    *n = m;
+  });
+}
+
+// ---- single operators ------------------------------------------------------------------
+int pnp_op_phi(pnp_ctx* ctx, const float* x, float* y, int B, int C, int H, int W, void* stream) {
+  if (!ctx) return PNP_E_ARG;
+  return guarded(ctx, [&] {
+    if (!x || !y || B < 1 || C < 1 || H < 1 || W < 1) fail(ctx, PNP_E_ARG, "bad arguments");
+    check_operator_shape(ctx, H, W);
+    launch_op_phi(ctx->op_kind, 0, x, y, op_desc(ctx), B * C, H, W, pick_stream(ctx, stream));
+    check_launch(ctx, "op_phi");
+  });
+}
+
+int pnp_op_adj_phi(pnp_ctx* ctx, const float* x, float* y, int B, int C, int H, int W, void* stream) {
+  if (!ctx) return PNP_E_ARG;
+  return guarded(ctx, [&] {
+    if (!x || !y || B < 1 || C < 1 || H < 1 || W < 1) fail(ctx, PNP_E_ARG, "bad arguments");
+    check_operator_shape(ctx, H, W);
+    launch_op_phi(ctx->op_kind, 1, x, y, op_desc(ctx), B * C, H, W, pick_stream(ctx, stream));
+    check_launch(ctx, "op_adj_phi");
+  });
+}
+
+int pnp_op_proj_l2_ball(pnp_ctx* ctx, const float* x, const float* x0, float* out, int B, int64_t n,
+                        double alpha_n, double gaussian_nl, double sp_nl, double r, void* stream) {
+  if (!ctx) return PNP_E_ARG;
+  return guarded(ctx, [&] {
+    if (!x || !x0 || !out || B < 1 || n < 1) fail(ctx, PNP_E_ARG, "bad arguments");
+    ensure(ctx, ctx->scr_part, (size_t)B * chunk_count((size_t)n) * sizeof(double));
+    const double eps = std::sqrt((double)n * (1.0 - sp_nl)) * r * alpha_n * gaussian_nl;   // operators.py:104
+    launch_l2_proj(x, x0, out, P<double>(ctx->scr_part), B, (size_t)n, eps, pick_stream(ctx, stream));
+    check_launch(ctx, "l2_proj");
+  });
+}
+
+int pnp_op_proj_l1_ball(pnp_ctx* ctx, const float* x, float* out, int B, int64_t n, double alpha_s, double sp_nl,
+                        double r, void* stream) {
+  if (!ctx) return PNP_E_ARG;
+  return guarded(ctx, [&] {
+    if (!x || !out || B < 1 || n < 1) fail(ctx, PNP_E_ARG, "bad arguments");
+    ensure(ctx, ctx->scr_theta, (size_t)B * sizeof(float));
+    const double eta = alpha_s * (double)n * sp_nl * r * 0.5;    // operators.py:96
+    hipStream_t st = pick_stream(ctx, stream);
+    launch_l1_select(x, P<float>(ctx->scr_theta), B, (size_t)n, eta, st);
+    check_launch(ctx, "l1_select");
+    launch_shrink(x, out, P<float>(ctx->scr_theta), B, (size_t)n, st);
+    check_launch(ctx, "shrink");
+  });
+}
+
+int pnp_op_prox_gkl(pnp_ctx* ctx, const float* x, const float* x0, float* out, int64_t count, double gamma,
+                    double alpha, void* stream) {
+  if (!ctx) return PNP_E_ARG;
+  return guarded(ctx, [&] {
+    if (!x || !x0 || !out || count < 0) fail(ctx, PNP_E_ARG, "bad arguments");
+    if (count == 0) return;
+    launch_gkl(x, x0, out, (size_t)count, gamma, alpha, pick_stream(ctx, stream));
+    check_launch(ctx, "gkl");
+  });
+}
+
+int pnp_op_denoise(pnp_ctx* ctx, const float* x, float* out, int B, int C, int H, int W, void* stream) {
+  if (!ctx) return PNP_E_ARG;
+  return guarded(ctx, [&] {
+    if (!x || !out || B < 1 || H < 1 || W < 1) fail(ctx, PNP_E_ARG, "bad arguments");
+    if (!ctx->den_ready) fail(ctx, PNP_E_STATE, "denoiser not set");
+    if (C != ctx->den_C) fail(ctx, PNP_E_ARG, "denoiser has %d channels, input has %d", ctx->den_C, C);
+    hipStream_t st = pick_stream(ctx, stream);
+    ensure(ctx, ctx->scr_u32, (size_t)B * C * H * W * sizeof(float));
+    ensure_padded(ctx, ctx->scr_u16, B, H, W, 4, st);
+    ensure_act(ctx, ctx->scr_act, B, H, W, st);
+    launch_pack_input(x, P<float>(ctx->scr_u32), P<half_t>(ctx->scr_u16), B, C, H, W, ctx->den_clamp, st);
+    check_launch(ctx, "pack_input");
+    run_denoiser(ctx, P<half_t>(ctx->scr_u16), P<float>(ctx->scr_u32), out, ctx->scr_act, B, H, W, st);
+  });
+}
+
+int pnp_op_psnr(pnp_ctx* ctx, const float* x_true, const float* x, int B, int64_t n, double* psnr_out,
+                void* stream) {
+  if (!ctx) return PNP_E_ARG;
+  return guarded(ctx, [&] {
+    if (!x_true || !x || !psnr_out || B < 1 || n < 1) fail(ctx, PNP_E_ARG, "bad arguments");
+    const int chunks = chunk_count((size_t)n);
+    ensure(ctx, ctx->scr_part, (size_t)B * chunks * sizeof(double));
+    hipStream_t st = pick_stream(ctx, stream);
+    launch_sqdiff(x_true, x, P<double>(ctx->scr_part), B, (size_t)n, st);
+    check_launch(ctx, "sqdiff");
+    std::vector<double> part((size_t)B * chunks);
+    HIPCHK(ctx, hipMemcpyAsync(part.data(), ctx->scr_part.p, part.size() * sizeof(double), hipMemcpyDeviceToHost,
+                               st));
+    HIPCHK(ctx, hipStreamSynchronize(st));
+    for (int b = 0; b < B; ++b) {
+      double s = 0;
+      for (int k = 0; k < chunks; ++k) s += part[(size_t)b * chunks + k];
+      psnr_out[b] = 10.0 * std::log10(1.0 / (s / (double)n));       // utils_eval.py:4-7
+    }
+  });
+}
+
+}  // extern "C"

@@ -1,0 +1,77 @@
+// Shared definitions for the PnP-PDS HIP kernels (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+typedef _Float16 half_t;
+typedef _Float16 half4_t __attribute__((ext_vector_type(4)));
+typedef _Float16 half8_t __attribute__((ext_vector_type(8)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+namespace pnp {
+
+constexpr int kWave = 64;
+constexpr int kWidth = 64;             // hidden channels of the denoiser
+constexpr int kMaxC = 4;               // image channels handled by head/tail (C <= 4)
+
+// ---- denoiser activation layout (HBM) ------------------------------------------------
+// Hidden activations: fp16 [B][H+2][W+2][64] ("padded NHWC64"): a zero border of one
+// pixel implements conv padding=1 with no boundary branches; 128 B per pixel.
+// Head input:         fp16 [B][H+2][W+2][4]  ("padded NHWC4"), channels >= C are zero.
+// Conv tiles: 8 output rows x 32 output columns; halo tile 10 x 34 pixels.
+constexpr int kTileH = 8;
+constexpr int kTileW = 32;
+constexpr int kHaloH = kTileH + 2;
+constexpr int kHaloW = kTileW + 2;
+constexpr int kHaloPix = kHaloH * kHaloW;          // 340
+constexpr int kBodyKSteps = 36;                    // 9 taps x 64 cin / 16
+constexpr int kBodyWBytes = kBodyKSteps * 2 * kWave * 16;   // 73728: [s][m][lane][8 x f16]
+constexpr int kHeadKSteps = 3;                     // 9 taps x 4 ch = 36 -> 48 / 16
+constexpr int kHeadWBytes = kHeadKSteps * 2 * kWave * 16;   // 6144
+constexpr int kTailKSteps = 18;                    // 9 taps x 64 cin / 32
+constexpr int kTailWBytes = kTailKSteps * kWave * 16;       // 18432: [s][lane][8 x f16]
+
+// Row i (0..31) of a 32x32x16 MFMA A-tile <-> output channel within the 32-channel
+// M-tile, chosen so that accumulator register r of lane-half h holds channel 16h + r
+// (C/D map: row = (r&3) + 8*(r>>2) + 4*h).  Each lane then owns 16 consecutive
+// output channels of one pixel -> two 16-byte stores in the epilogue.
+__host__ __device__ inline int mfma32_row_to_channel(int i) {
+  return 16 * ((i >> 2) & 1) + (i & 3) + 4 * (i >> 3);
+}
+
+// LDS image of a halo tile (hidden activations): pixel p occupies 128 B; its eight
+// 16-B channel chunks are XOR-swizzled by ((p >> 1) & 7) so that the 16-lane groups of
+// a ds_read_b128 over 16 consecutive pixels hit 16 distinct bank slots.
+__device__ __forceinline__ int halo_chunk_offset(int p, int chunk) {
+  return p * 128 + 16 * (chunk ^ ((p >> 1) & 7));
+}
+
+__device__ __forceinline__ float act_fn(float v, int act) {
+  return act == 0 ? (v > 0.f ? v : 0.01f * v) : (v > 0.f ? v : 0.f);
+}
+
+// ---- block reductions ------------------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Sum over a 256-thread block in a fixed order (deterministic); result valid in all threads.
+template <typename T, int NT = 256>
+__device__ __forceinline__ T block_sum(T v, T* scratch /* >= NT/64 */) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) scratch[w] = v;
+  __syncthreads();
+  T s = 0;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) s += scratch[i];
+  return s;
+}
+
+}  // namespace pnp

@@ -1,0 +1,63 @@
+// Launch interface between the host orchestration (capi.hip) and the kernels
+// (conv.hip: denoiser, ops.hip: operators / proxes / fused dual passes).
+#pragma once
+#include "common.h"
+
+namespace pnp {
+
+// ---- denoiser (conv.hip) -----------------------------------------------------------
+struct ConvShape {
+  int B, H, W;       // image size (unpadded)
+  int Hp, Wp;        // padded (H+2, W+2)
+  int tiles_x, tiles_y, tiles;
+};
+ConvShape make_conv_shape(int B, int H, int W);
+hipError_t conv_kernels_init();
+void pack_body_weights(const float* W, uint16_t* out);
+void pack_head_weights(const float* W, int C, uint16_t* out);
+void pack_tail_weights(const float* W, int C, uint16_t* out);
+void launch_conv_head(const half_t* in4, half_t* out, const void* w, const float* bias, const ConvShape& s,
+                      int act, int num_cus, hipStream_t st);
+void launch_conv_body(const half_t* in, half_t* out, const void* w, const float* bias, const ConvShape& s,
+                      int act, int num_cus, hipStream_t st);
+void launch_conv_tail(const half_t* in, const float* xin, float* xout, const void* w, const float* bias,
+                      const ConvShape& s, int C, int residual_sign, int clamp_out, int num_cus, hipStream_t st);
+
+// ---- operators / proxes (ops.hip) ----------------------------------------------------
+enum { OP_ID = 0, OP_BLUR = 1, OP_MASK = 2 };
+enum { M_A = 0, M_B = 1, M_C = 2 };
+
+struct OpDesc {
+  int kind;
+  const int4* taps_fwd;   // {oy, ox, float bits of w, 0}: Phi:   y[i,j] += w x[i+oy, j+ox] (periodic)
+  const int4* taps_adj;   //                               Phi^T: y[i,j] += w x[i+oy, j+ox]
+  int ntaps;
+  int R;                  // max |offset| (halo radius), <= 16
+  const uint8_t* mask;    // H*W keep-mask (random_sampling)
+};
+
+void launch_k1(int kind, const float* x, const float* y, const float* s, float* u32, half_t* u16, float* w,
+               const OpDesc& op, int B, int C, int H, int W, float gamma1, int clamp_in, int method_b,
+               hipStream_t st);
+void launch_k2(int kind, int method, const float* xn, const float* xo, float* y, const float* xobs,
+               const float* xtrue, float* s, const float* w, const float* theta, double* partials,
+               const OpDesc& op, int B, int C, int H, int W, double gamma2, double gkl_gamma, double gkl_alpha,
+               int record, hipStream_t st);
+void launch_k3(int method, float* y, const float* xobs, const double* partials, int B, int C, int H, int W,
+               double gamma2, double eps, double* metrics, int it, int cap, int record, int has_true,
+               hipStream_t st);
+int partial_tiles(int H, int W);
+int chunk_count(size_t n);
+void launch_l1_select(const float* v, float* theta, int B, size_t n, double eta, hipStream_t st);
+void launch_op_phi(int kind, int adj, const float* x, float* out, const OpDesc& op, int BC, int H, int W,
+                   hipStream_t st);
+void launch_l2_proj(const float* x, const float* x0, float* out, double* partials, int B, size_t n, double eps,
+                    hipStream_t st);
+void launch_sqdiff(const float* a, const float* c, double* partials, int B, size_t n, hipStream_t st);
+void launch_shrink(const float* v, float* out, const float* theta, int B, size_t n, hipStream_t st);
+void launch_gkl(const float* x, const float* x0, float* out, size_t count, double gamma, double alpha,
+                hipStream_t st);
+void launch_pack_input(const float* x, float* u32, half_t* u16, int B, int C, int H, int W, int clamp_in,
+                       hipStream_t st);
+
+}  // namespace pnp

@@ -1,0 +1,610 @@
+// Observation operators, proximal operators and the fused primal/dual passes of one
+// PnP-PDS iteration (iteration.py:48-63), for gfx950.
+//
+// State arrays are fp32 B x C x H x W (NCHW).  One iteration is
+//   K1  primal_pre : u = [clamp](x - g1 * Phi^T y)            -> u32 (NCHW) + u16 (padded NHWC4)
+//                    (B) w = s - g1 * y
+//   L1  l1_select  : (B) per-image l1-ball threshold theta       (operators.py:94-100)
+//   D   denoiser   : x+ = D(u)                                    (conv.hip)
+//   K2  dual_a     : v = y + g2 (Phi(2x+ - x) [+ 2 s+ - s]),  s+ = shrink(w, theta)
+//                    A/B: y <- v,  per-tile partial sums of (v/g2 - xobs)^2 and the metrics
+//                    C:   y <- v - g2 proxGKL(v/g2)  (operators.py:114-115), fully elementwise
+//   K3  dual_b     : A/B: y <- v - g2 P_ball(v/g2)              (operators.py:102-108)
+//                    + per-image c_n / PSNR (iteration.py:187-188, utils_eval.py:4-7)
+//
+// Phi for 'blur' is the 19x19 centred circular convolution of operators.py:7-22 (its
+// FFT form is exactly a periodic stencil), done here as an LDS-tiled stencil over the
+// kernel's non-zero taps with wrap-around halo loads; Phi^T is the correlation
+// (operators.py:24-38).  'random_sampling' is a pointwise keep-mask (operators.py:40-58).
+#include "kernels.h"
+
+namespace pnp {
+
+constexpr int kST = 32;                 // square pixel tile of the elementwise passes
+constexpr int kMaxR = 16;
+constexpr int kLdsW = kST + 2 * kMaxR;  // 64
+
+__device__ __forceinline__ int wrapi(int v, int n) {
+  v %= n;
+  return v < 0 ? v + n : v;
+}
+
+// Fill an (kST+2R)^2 LDS tile of one plane, with periodic wrap (the reference's 'wrap'
+// padding, operators.py:12,17,27,32).  F(k) returns the source value at linear index k.
+template <class F>
+__device__ __forceinline__ void fill_halo(float* lds, int LW, int i0, int j0, int R, int H, int W, F val) {
+  const int n = LW * LW;
+  for (int q = threadIdx.x; q < n; q += 256) {
+    const int ly = q / LW, lx = q - ly * LW;
+    const int gi = wrapi(i0 - R + ly, H), gj = wrapi(j0 - R + lx, W);
+    lds[q] = val((size_t)gi * W + gj);
+  }
+}
+
+// Thread (tx = tid&31, tg = tid>>5) computes pixels (i0 + 4tg + r, j0 + tx), r = 0..3.
+__device__ __forceinline__ void stencil4(const float* lds, int LW, int R, const int4* __restrict__ taps,
+                                         int ntaps, float (&acc)[4]) {
+  const int tx = threadIdx.x & 31, tg = threadIdx.x >> 5;
+  acc[0] = acc[1] = acc[2] = acc[3] = 0.f;
+  const float* base = lds + (4 * tg + R) * LW + tx + R;
+  for (int t = 0; t < ntaps; ++t) {
+    const int4 tp = taps[t];
+    const float w = __int_as_float(tp.z);
+    const float* p = base + tp.x * LW + tp.y;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc[r] = fmaf(w, p[r * LW], acc[r]);
+  }
+}
+
+// =====================================================================================
+// K1: primal step input  (iteration.py:50/55/61 first half; denoiser.py:35-40)
+// grid (tiles_x*tiles_y, B), 256 threads
+// =====================================================================================
+template <int KIND>
+__global__ __launch_bounds__(256) void k1_primal_pre(const float* __restrict__ x, const float* __restrict__ y,
+                                                      const float* __restrict__ s, float* __restrict__ u32,
+                                                      half_t* __restrict__ u16, float* __restrict__ w,
+                                                      OpDesc op, int C, int H, int W, int tiles_x,
+                                                      float gamma1, int clamp_in, int method_b) {
+  __shared__ float lds[kLdsW * kLdsW];
+  const int tile = blockIdx.x, b = blockIdx.y;
+  const int ty = tile / tiles_x;
+  const int i0 = ty * kST, j0 = (tile - ty * tiles_x) * kST;
+  const int tx = threadIdx.x & 31, tg = threadIdx.x >> 5;
+  const size_t plane = (size_t)H * W;
+  float g[kMaxC][4];
+#pragma unroll
+  for (int c = 0; c < kMaxC; ++c) {
+    if (c >= C) break;
+    const float* yp = y + ((size_t)b * C + c) * plane;
+    if (KIND == OP_BLUR) {
+      const int LW = kST + 2 * op.R;
+      __syncthreads();
+      fill_halo(lds, LW, i0, j0, op.R, H, W, [&](size_t k) { return yp[k]; });
+      __syncthreads();
+      stencil4(lds, LW, op.R, op.taps_adj, op.ntaps, g[c]);
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = i0 + 4 * tg + r, j = j0 + tx;
+        float v = 0.f;
+        if (i < H && j < W) {
+          v = yp[(size_t)i * W + j];
+          if (KIND == OP_MASK) v *= (float)op.mask[(size_t)i * W + j];
+        }
+        g[c][r] = v;
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = i0 + 4 * tg + r, j = j0 + tx;
+    if (i >= H || j >= W) continue;
+    half4_t h4 = {0, 0, 0, 0};
+#pragma unroll
+    for (int c = 0; c < kMaxC; ++c) {
+      if (c >= C) break;
+      const size_t idx = ((size_t)b * C + c) * plane + (size_t)i * W + j;
+      float u = x[idx] - gamma1 * g[c][r];
+      if (clamp_in) u = fminf(fmaxf(u, 0.f), 1.f);
+      u32[idx] = u;
+      h4[c] = (half_t)u;
+      if (method_b) w[idx] = s[idx] - gamma1 * y[idx];
+    }
+    *reinterpret_cast<half4_t*>(u16 + (((size_t)b * (H + 2) + i + 1) * (W + 2) + j + 1) * 4) = h4;
+  }
+}
+
+// =====================================================================================
+// K2: dual ascent with Phi and over-relaxation (iteration.py:51/57/62), fused with the
+// l1-ball shrink (B), the GKL prox (C), and the per-tile metric / norm partial sums.
+// partials: [B][tiles][4] = { sum (v/g2 - xobs)^2, sum (x+ - x)^2, sum x^2, sum (xt - x+)^2 }
+// =====================================================================================
+template <int KIND, int METHOD>
+__global__ __launch_bounds__(256) void k2_dual(const float* __restrict__ xn, const float* __restrict__ xo,
+                                                float* __restrict__ y, const float* __restrict__ xobs,
+                                                const float* __restrict__ xtrue, float* __restrict__ s,
+                                                const float* __restrict__ w, const float* __restrict__ theta,
+                                                double* __restrict__ partials, OpDesc op, int C, int H, int W,
+                                                int tiles_x, int tiles, double gamma2, double gkl_gamma,
+                                                double gkl_alpha, int record) {
+  __shared__ float lds[kLdsW * kLdsW];
+  __shared__ double red[4];
+  const int tile = blockIdx.x, b = blockIdx.y;
+  const int ty = tile / tiles_x;
+  const int i0 = ty * kST, j0 = (tile - ty * tiles_x) * kST;
+  const int tx = threadIdx.x & 31, tg = threadIdx.x >> 5;
+  const size_t plane = (size_t)H * W;
+  float g[kMaxC][4];
+#pragma unroll
+  for (int c = 0; c < kMaxC; ++c) {
+    if (c >= C) break;
+    const float* xnp = xn + ((size_t)b * C + c) * plane;
+    const float* xop = xo + ((size_t)b * C + c) * plane;
+    if (KIND == OP_BLUR) {
+      const int LW = kST + 2 * op.R;
+      __syncthreads();
+      fill_halo(lds, LW, i0, j0, op.R, H, W, [&](size_t k) { return 2.f * xnp[k] - xop[k]; });
+      __syncthreads();
+      stencil4(lds, LW, op.R, op.taps_fwd, op.ntaps, g[c]);
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = i0 + 4 * tg + r, j = j0 + tx;
+        float v = 0.f;
+        if (i < H && j < W) {
+          const size_t k = (size_t)i * W + j;
+          v = 2.f * xnp[k] - xop[k];
+          if (KIND == OP_MASK) v *= (float)op.mask[k];
+        }
+        g[c][r] = v;
+      }
+    }
+  }
+  double d2 = 0, e2 = 0, n2 = 0, t2 = 0;
+  const float th = METHOD == M_B ? theta[b] : 0.f;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = i0 + 4 * tg + r, j = j0 + tx;
+    if (i >= H || j >= W) continue;
+#pragma unroll
+    for (int c = 0; c < kMaxC; ++c) {
+      if (c >= C) break;
+      const size_t idx = ((size_t)b * C + c) * plane + (size_t)i * W + j;
+      double gv = g[c][r];
+      if (METHOD == M_B) {
+        const float wv = w[idx];
+        const float sp = copysignf(fmaxf(fabsf(wv) - th, 0.f), wv);   // operators.py:98
+        gv += 2.0 * (double)sp - (double)s[idx];
+        s[idx] = sp;
+      }
+      const double v = (double)y[idx] + gamma2 * gv;
+      const double ob = xobs[idx];
+      if (METHOD == M_C) {
+        const double vv = v / gamma2;
+        const double tt = vv - gkl_gamma * gkl_alpha;
+        const double p = 0.5 * (tt + sqrt(tt * tt + 4.0 * gkl_gamma * ob));
+        y[idx] = (float)(v - gamma2 * p);
+      } else {
+        y[idx] = (float)v;
+        const double dd = v / gamma2 - ob;
+        d2 += dd * dd;
+      }
+      if (record) {
+        const double a = xn[idx], o = xo[idx];
+        e2 += (a - o) * (a - o);
+        n2 += o * o;
+        if (xtrue) {
+          const double q = (double)xtrue[idx] - a;
+          t2 += q * q;
+        }
+      }
+    }
+  }
+  d2 = block_sum(d2, red);
+  e2 = block_sum(e2, red);
+  n2 = block_sum(n2, red);
+  t2 = block_sum(t2, red);
+  if (threadIdx.x == 0) {
+    double* p = partials + ((size_t)b * tiles + tile) * 4;
+    p[0] = d2; p[1] = e2; p[2] = n2; p[3] = t2;
+  }
+}
+
+// Deterministic reduction of one image's tile partials (fixed order) in a 256-block.
+__device__ __forceinline__ void reduce_partials(const double* __restrict__ partials, int b, int tiles,
+                                                double (&out)[4], double* red) {
+  double a[4] = {0, 0, 0, 0};
+  for (int k = threadIdx.x; k < tiles; k += 256) {
+    const double* p = partials + ((size_t)b * tiles + k) * 4;
+    a[0] += p[0]; a[1] += p[1]; a[2] += p[2]; a[3] += p[3];
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) out[q] = block_sum(a[q], red);
+}
+
+__device__ __forceinline__ void write_metrics(double* metrics, int b, int it, int cap, const double (&a)[4],
+                                              double n_elem, int has_true) {
+  double* m = metrics + ((size_t)b * cap + it) * 2;
+  m[0] = sqrt(a[1]) / sqrt(a[2]);                                   // iteration.py:187
+  m[1] = has_true ? 10.0 * log10(1.0 / (a[3] / n_elem)) : __builtin_nan("");   // utils_eval.py:4-7
+}
+
+// =====================================================================================
+// K3 (A/B): y <- v - g2 * P_{B(xobs, eps)}(v / g2) = (1 - f)(v - g2 xobs), f = min(1, eps/|v/g2 - xobs|)
+// grid (chunks, B); each block re-reduces its image's partials (fixed order).
+// =====================================================================================
+__global__ __launch_bounds__(256) void k3_l2_dual(float* __restrict__ y, const float* __restrict__ xobs,
+                                                   const double* __restrict__ partials, int tiles, size_t n,
+                                                   double gamma2, double eps, double* __restrict__ metrics,
+                                                   int it, int cap, int record, int has_true) {
+  __shared__ double red[4];
+  const int b = blockIdx.y;
+  double a[4];
+  reduce_partials(partials, b, tiles, a, red);
+  const double nrm = sqrt(a[0]);
+  const double f = nrm > eps ? eps / nrm : 1.0;
+  const double omf = 1.0 - f;
+  if (record && blockIdx.x == 0 && threadIdx.x == 0) write_metrics(metrics, b, it, cap, a, (double)n, has_true);
+  float* yb = y + (size_t)b * n;
+  const float* ob = xobs + (size_t)b * n;
+  const size_t chunk = 2048;
+  const size_t beg = (size_t)blockIdx.x * chunk;
+  for (size_t k = beg + threadIdx.x; k < beg + chunk && k < n; k += 256)
+    yb[k] = (float)(omf * ((double)yb[k] - gamma2 * (double)ob[k]));
+}
+
+__global__ __launch_bounds__(256) void k3_metrics(const double* __restrict__ partials, int tiles, size_t n,
+                                                   double* __restrict__ metrics, int it, int cap, int has_true) {
+  __shared__ double red[4];
+  double a[4];
+  reduce_partials(partials, blockIdx.x, tiles, a, red);
+  if (threadIdx.x == 0) write_metrics(metrics, blockIdx.x, it, cap, a, (double)n, has_true);
+}
+
+// =====================================================================================
+// l1-ball threshold (operators.py:94-100).  The reference sorts |v| and takes
+// theta = max(0, max_k (S_k - eta)/k); equivalently theta is the root of
+// f(t) = sum max(|v|-t, 0) - eta.  One 1024-thread workgroup per image runs a 3-level
+// radix select on the float bit patterns of |v| (11 + 11 + 9 bits): each level builds
+// an LDS histogram (count, sum) of the candidates, finds the highest bin whose lower
+// edge still has f >= 0, and descends into it.  A final exact pass gives
+// K = #{|v| > t*}, S = sum of those (fp64, fixed order), theta = (S - eta) / K.
+// =====================================================================================
+constexpr int kSelThreads = 512;
+
+__device__ __forceinline__ double block_sum1024(double v, double* scratch) {
+  return block_sum<double, kSelThreads>(v, scratch);
+}
+
+// One radix level: histogram of candidates whose bits above this level equal `prefix`,
+// then the highest bin j with f(lo_j) >= 0.  Updates prefix / (Khi, Shi).
+template <int SH, int NBITS>
+__device__ __forceinline__ void select_level(const unsigned* __restrict__ vb, size_t n, double eta,
+                                             unsigned& prefix, double& Khi, double& Shi, unsigned* cnt,
+                                             float* sm, int* s_j, double* s_KS) {
+  constexpr int nb = 1 << NBITS;
+  constexpr unsigned hi_mask = (SH + NBITS >= 31) ? 0u : (0x7fffffffu & ~((1u << (SH + NBITS)) - 1u));
+  for (int j = threadIdx.x; j < nb; j += kSelThreads) { cnt[j] = 0; sm[j] = 0.f; }
+  __syncthreads();
+  for (size_t i = threadIdx.x; i < n; i += kSelThreads) {
+    const unsigned u = vb[i] & 0x7fffffffu;
+    if ((u & hi_mask) == prefix) {
+      const unsigned j = (u >> SH) & (unsigned)(nb - 1);
+      atomicAdd(&cnt[j], 1u);
+      atomicAdd(&sm[j], __uint_as_float(u));
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) {                      // wave 0: suffix scan over the bins from the top
+    constexpr int per = nb / 64;
+    const int lane = threadIdx.x;
+    double kc = 0, sc = 0;
+    for (int q = 0; q < per; ++q) { kc += cnt[lane * per + q]; sc += sm[lane * per + q]; }
+    double ks = kc, ss = sc;                   // inclusive suffix over lanes lane..63
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const double tk = __shfl_down(ks, off, 64), ts = __shfl_down(ss, off, 64);
+      if (lane + off < 64) { ks += tk; ss += ts; }
+    }
+    double K = Khi + ks - kc, S = Shi + ss - sc;   // strictly above this lane's bins
+    int found = -1;
+    double fK = 0, fS = 0;
+    for (int q = per - 1; q >= 0; --q) {
+      const int j = lane * per + q;
+      const double K2 = K + cnt[j], S2 = S + sm[j];
+      const double lo = (double)__uint_as_float(prefix | ((unsigned)j << SH));
+      if (S2 - K2 * lo - eta >= 0.0) { found = j; fK = K; fS = S; break; }
+      K = K2; S = S2;
+    }
+    int best = found;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) best = max(best, __shfl_xor(best, off, 64));
+    if (best >= 0 && found == best) { *s_j = best; s_KS[0] = fK; s_KS[1] = fS; }
+    if (best < 0 && lane == 0) {               // approximate sums missed: take bin 0
+      *s_j = 0;
+      s_KS[0] = K; s_KS[1] = S;                // lane 0's K/S after its loop = all bins >= 1 ... plus bin 0
+    }
+  }
+  __syncthreads();
+  if (*s_j == 0 && threadIdx.x == 0) {         // "above bin 0" = Khi + all bins >= 1, exactly
+    double K = Khi, S = Shi;
+    for (int j = nb - 1; j >= 1; --j) { K += cnt[j]; S += sm[j]; }
+    s_KS[0] = K; s_KS[1] = S;
+  }
+  __syncthreads();
+  prefix |= (unsigned)(*s_j) << SH;
+  Khi = s_KS[0];
+  Shi = s_KS[1];
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(kSelThreads) void l1_select_kernel(const float* __restrict__ v, float* __restrict__ theta,
+                                                                 size_t n, double eta) {
+  __shared__ unsigned cnt[2048];
+  __shared__ float sm[2048];
+  __shared__ double red[8];
+  __shared__ int s_j;
+  __shared__ double s_KS[2];
+  const int b = blockIdx.x;
+  const unsigned* vb = reinterpret_cast<const unsigned*>(v + (size_t)b * n);
+  if (!(eta > 0.0)) {                         // eta == 0: projection onto {0}
+    if (threadIdx.x == 0) theta[b] = __builtin_inff();
+    return;
+  }
+  double tot = 0;
+  for (size_t i = threadIdx.x; i < n; i += kSelThreads) tot += (double)__uint_as_float(vb[i] & 0x7fffffffu);
+  tot = block_sum1024(tot, red);
+  if (tot <= eta) {                            // already inside the ball: theta = 0
+    if (threadIdx.x == 0) theta[b] = 0.f;
+    return;
+  }
+  unsigned prefix = 0;
+  double Khi = 0, Shi = 0;                     // candidates strictly above the current range
+  select_level<20, 11>(vb, n, eta, prefix, Khi, Shi, cnt, sm, &s_j, s_KS);
+  select_level<9, 11>(vb, n, eta, prefix, Khi, Shi, cnt, sm, &s_j, s_KS);
+  select_level<0, 9>(vb, n, eta, prefix, Khi, Shi, cnt, sm, &s_j, s_KS);
+  // exact pass: elements strictly greater than the selected float value `prefix`
+  double K = 0, S = 0;
+  for (size_t i = threadIdx.x; i < n; i += kSelThreads) {
+    const unsigned u = vb[i] & 0x7fffffffu;
+    if (u > prefix) { K += 1.0; S += (double)__uint_as_float(u); }
+  }
+  K = block_sum1024(K, red);
+  S = block_sum1024(S, red);
+  if (threadIdx.x == 0) {
+    const double th = K > 0 ? (S - eta) / K : (double)__uint_as_float(prefix);
+    theta[b] = (float)(th > 0 ? th : 0.0);
+  }
+}
+
+// =====================================================================================
+// Standalone operators (pnp_op_*): stencil, l2 projection, shrink, GKL, PSNR, packing.
+// =====================================================================================
+template <int KIND, int ADJ>
+__global__ __launch_bounds__(256) void op_phi_kernel(const float* __restrict__ x, float* __restrict__ out,
+                                                      OpDesc op, int H, int W, int tiles_x) {
+  __shared__ float lds[kLdsW * kLdsW];
+  const int tile = blockIdx.x, bc = blockIdx.y;
+  const int ty = tile / tiles_x;
+  const int i0 = ty * kST, j0 = (tile - ty * tiles_x) * kST;
+  const int tx = threadIdx.x & 31, tg = threadIdx.x >> 5;
+  const size_t plane = (size_t)H * W;
+  const float* xp = x + (size_t)bc * plane;
+  float acc[4];
+  if (KIND == OP_BLUR) {
+    const int LW = kST + 2 * op.R;
+    fill_halo(lds, LW, i0, j0, op.R, H, W, [&](size_t k) { return xp[k]; });
+    __syncthreads();
+    stencil4(lds, LW, op.R, ADJ ? op.taps_adj : op.taps_fwd, op.ntaps, acc);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = i0 + 4 * tg + r, j = j0 + tx;
+    if (i >= H || j >= W) continue;
+    const size_t k = (size_t)i * W + j;
+    float v;
+    if (KIND == OP_BLUR) v = acc[r];
+    else if (KIND == OP_MASK) v = xp[k] * (float)op.mask[k];
+    else v = xp[k];
+    out[(size_t)bc * plane + k] = v;
+  }
+}
+
+// per image partial sums of (x - x0)^2 (or (xt - x)^2 for psnr): grid (chunks, B)
+__global__ __launch_bounds__(256) void sqdiff_partials(const float* __restrict__ a, const float* __restrict__ c,
+                                                        double* __restrict__ partials, size_t n, int chunks) {
+  __shared__ double red[4];
+  const int b = blockIdx.y;
+  const size_t chunk = 2048, beg = (size_t)blockIdx.x * chunk;
+  double acc = 0;
+  for (size_t k = beg + threadIdx.x; k < beg + chunk && k < n; k += 256) {
+    const double d = (double)a[(size_t)b * n + k] - (double)c[(size_t)b * n + k];
+    acc += d * d;
+  }
+  acc = block_sum(acc, red);
+  if (threadIdx.x == 0) partials[(size_t)b * chunks + blockIdx.x] = acc;
+}
+
+__global__ __launch_bounds__(256) void l2_apply(const float* __restrict__ x, const float* __restrict__ x0,
+                                                 float* __restrict__ out, const double* __restrict__ partials,
+                                                 size_t n, int chunks, double eps) {
+  __shared__ double red[4];
+  const int b = blockIdx.y;
+  double a = 0;
+  for (int k = threadIdx.x; k < chunks; k += 256) a += partials[(size_t)b * chunks + k];
+  a = block_sum(a, red);
+  const double nrm = sqrt(a);
+  const size_t chunk = 2048, beg = (size_t)blockIdx.x * chunk;
+  for (size_t k = beg + threadIdx.x; k < beg + chunk && k < n; k += 256) {
+    const size_t i = (size_t)b * n + k;
+    out[i] = nrm > eps ? (float)((double)x0[i] + eps * ((double)x[i] - (double)x0[i]) / nrm) : x[i];
+  }
+}
+
+__global__ __launch_bounds__(256) void shrink_kernel(const float* __restrict__ v, float* __restrict__ out,
+                                                      const float* __restrict__ theta, size_t n) {
+  const int b = blockIdx.y;
+  const float th = theta[b];
+  const size_t chunk = 2048, beg = (size_t)blockIdx.x * chunk;
+  for (size_t k = beg + threadIdx.x; k < beg + chunk && k < n; k += 256) {
+    const float x = v[(size_t)b * n + k];
+    out[(size_t)b * n + k] = copysignf(fmaxf(fabsf(x) - th, 0.f), x);
+  }
+}
+
+__global__ __launch_bounds__(256) void gkl_kernel(const float* __restrict__ x, const float* __restrict__ x0,
+                                                   float* __restrict__ out, size_t count, double gamma, double alpha) {
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < count; i += (size_t)gridDim.x * 256) {
+    const double t = (double)x[i] - gamma * alpha;
+    out[i] = (float)(0.5 * (t + sqrt(t * t + 4.0 * gamma * (double)x0[i])));
+  }
+}
+
+// Denoiser input packing for pnp_op_denoise: u32 = [clamp](x), u16 = padded NHWC4 fp16.
+__global__ __launch_bounds__(256) void pack_input_kernel(const float* __restrict__ x, float* __restrict__ u32,
+                                                          half_t* __restrict__ u16, int B, int C, int H, int W,
+                                                          int clamp_in) {
+  const size_t plane = (size_t)H * W;
+  const size_t total = (size_t)B * plane;
+  for (size_t p = (size_t)blockIdx.x * 256 + threadIdx.x; p < total; p += (size_t)gridDim.x * 256) {
+    const size_t b = p / plane, k = p - b * plane;
+    const int i = (int)(k / W), j = (int)(k - (size_t)i * W);
+    half4_t h4 = {0, 0, 0, 0};
+    for (int c = 0; c < C; ++c) {
+      const size_t idx = (b * C + c) * plane + k;
+      float u = x[idx];
+      if (clamp_in) u = fminf(fmaxf(u, 0.f), 1.f);
+      u32[idx] = u;
+      h4[c] = (half_t)u;
+    }
+    *reinterpret_cast<half4_t*>(u16 + ((b * (H + 2) + i + 1) * (W + 2) + j + 1) * 4) = h4;
+  }
+}
+
+// =====================================================================================
+// Launchers (host)
+// =====================================================================================
+struct TileGrid {
+  int tiles_x, tiles_y, tiles;
+};
+inline TileGrid tile_grid(int H, int W) {
+  TileGrid g;
+  g.tiles_x = (W + kST - 1) / kST;
+  g.tiles_y = (H + kST - 1) / kST;
+  g.tiles = g.tiles_x * g.tiles_y;
+  return g;
+}
+
+void launch_k1(int kind, const float* x, const float* y, const float* s, float* u32, half_t* u16, float* w,
+               const OpDesc& op, int B, int C, int H, int W, float gamma1, int clamp_in, int method_b,
+               hipStream_t st) {
+  const TileGrid g = tile_grid(H, W);
+  dim3 grid(g.tiles, B);
+#define K1_ARGS x, y, s, u32, u16, w, op, C, H, W, g.tiles_x, gamma1, clamp_in, method_b
+  if (kind == OP_BLUR) hipLaunchKernelGGL(k1_primal_pre<OP_BLUR>, grid, dim3(256), 0, st, K1_ARGS);
+  else if (kind == OP_MASK) hipLaunchKernelGGL(k1_primal_pre<OP_MASK>, grid, dim3(256), 0, st, K1_ARGS);
+  else hipLaunchKernelGGL(k1_primal_pre<OP_ID>, grid, dim3(256), 0, st, K1_ARGS);
+#undef K1_ARGS
+}
+
+template <int KIND>
+static void launch_k2_kind(int method, dim3 grid, hipStream_t st, const float* xn, const float* xo, float* y,
+                           const float* xobs, const float* xtrue, float* s, const float* w, const float* theta,
+                           double* partials, const OpDesc& op, int C, int H, int W, int tiles_x, int tiles,
+                           double gamma2, double gkl_gamma, double gkl_alpha, int record) {
+#define K2_ARGS xn, xo, y, xobs, xtrue, s, w, theta, partials, op, C, H, W, tiles_x, tiles, gamma2, gkl_gamma, \
+                gkl_alpha, record
+  if (method == M_A) hipLaunchKernelGGL((k2_dual<KIND, M_A>), grid, dim3(256), 0, st, K2_ARGS);
+  else if (method == M_B) hipLaunchKernelGGL((k2_dual<KIND, M_B>), grid, dim3(256), 0, st, K2_ARGS);
+  else hipLaunchKernelGGL((k2_dual<KIND, M_C>), grid, dim3(256), 0, st, K2_ARGS);
+#undef K2_ARGS
+}
+
+void launch_k2(int kind, int method, const float* xn, const float* xo, float* y, const float* xobs,
+               const float* xtrue, float* s, const float* w, const float* theta, double* partials,
+               const OpDesc& op, int B, int C, int H, int W, double gamma2, double gkl_gamma, double gkl_alpha,
+               int record, hipStream_t st) {
+  const TileGrid g = tile_grid(H, W);
+  dim3 grid(g.tiles, B);
+  if (kind == OP_BLUR)
+    launch_k2_kind<OP_BLUR>(method, grid, st, xn, xo, y, xobs, xtrue, s, w, theta, partials, op, C, H, W,
+                            g.tiles_x, g.tiles, gamma2, gkl_gamma, gkl_alpha, record);
+  else if (kind == OP_MASK)
+    launch_k2_kind<OP_MASK>(method, grid, st, xn, xo, y, xobs, xtrue, s, w, theta, partials, op, C, H, W,
+                            g.tiles_x, g.tiles, gamma2, gkl_gamma, gkl_alpha, record);
+  else
+    launch_k2_kind<OP_ID>(method, grid, st, xn, xo, y, xobs, xtrue, s, w, theta, partials, op, C, H, W,
+                          g.tiles_x, g.tiles, gamma2, gkl_gamma, gkl_alpha, record);
+}
+
+int partial_tiles(int H, int W) { return tile_grid(H, W).tiles; }
+
+void launch_k3(int method, float* y, const float* xobs, const double* partials, int B, int C, int H, int W,
+               double gamma2, double eps, double* metrics, int it, int cap, int record, int has_true,
+               hipStream_t st) {
+  const TileGrid g = tile_grid(H, W);
+  const size_t n = (size_t)C * H * W;
+  if (method == M_C) {
+    if (record) hipLaunchKernelGGL(k3_metrics, dim3(B), dim3(256), 0, st, partials, g.tiles, n, metrics, it, cap,
+                                   has_true);
+    return;
+  }
+  const int chunks = (int)((n + 2047) / 2048);
+  hipLaunchKernelGGL(k3_l2_dual, dim3(chunks, B), dim3(256), 0, st, y, xobs, partials, g.tiles, n, gamma2, eps,
+                     metrics, it, cap, record, has_true);
+}
+
+void launch_l1_select(const float* v, float* theta, int B, size_t n, double eta, hipStream_t st) {
+  hipLaunchKernelGGL(l1_select_kernel, dim3(B), dim3(kSelThreads), 0, st, v, theta, n, eta);
+}
+
+void launch_op_phi(int kind, int adj, const float* x, float* out, const OpDesc& op, int BC, int H, int W,
+                   hipStream_t st) {
+  const TileGrid g = tile_grid(H, W);
+  dim3 grid(g.tiles, BC);
+  if (kind == OP_BLUR) {
+    if (adj) hipLaunchKernelGGL((op_phi_kernel<OP_BLUR, 1>), grid, dim3(256), 0, st, x, out, op, H, W, g.tiles_x);
+    else hipLaunchKernelGGL((op_phi_kernel<OP_BLUR, 0>), grid, dim3(256), 0, st, x, out, op, H, W, g.tiles_x);
+  } else if (kind == OP_MASK) {
+    hipLaunchKernelGGL((op_phi_kernel<OP_MASK, 0>), grid, dim3(256), 0, st, x, out, op, H, W, g.tiles_x);
+  } else {
+    hipLaunchKernelGGL((op_phi_kernel<OP_ID, 0>), grid, dim3(256), 0, st, x, out, op, H, W, g.tiles_x);
+  }
+}
+
+int chunk_count(size_t n) { return (int)((n + 2047) / 2048); }
+
+void launch_l2_proj(const float* x, const float* x0, float* out, double* partials, int B, size_t n, double eps,
+                    hipStream_t st) {
+  const int chunks = chunk_count(n);
+  hipLaunchKernelGGL(sqdiff_partials, dim3(chunks, B), dim3(256), 0, st, x, x0, partials, n, chunks);
+  hipLaunchKernelGGL(l2_apply, dim3(chunks, B), dim3(256), 0, st, x, x0, out, partials, n, chunks, eps);
+}
+
+void launch_sqdiff(const float* a, const float* c, double* partials, int B, size_t n, hipStream_t st) {
+  const int chunks = chunk_count(n);
+  hipLaunchKernelGGL(sqdiff_partials, dim3(chunks, B), dim3(256), 0, st, a, c, partials, n, chunks);
+}
+
+void launch_shrink(const float* v, float* out, const float* theta, int B, size_t n, hipStream_t st) {
+  hipLaunchKernelGGL(shrink_kernel, dim3(chunk_count(n), B), dim3(256), 0, st, v, out, theta, n);
+}
+
+void launch_gkl(const float* x, const float* x0, float* out, size_t count, double gamma, double alpha,
+                hipStream_t st) {
+  size_t blocks = (count + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  if (blocks == 0) blocks = 1;
+  hipLaunchKernelGGL(gkl_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, x0, out, count, gamma, alpha);
+}
+
+void launch_pack_input(const float* x, float* u32, half_t* u16, int B, int C, int H, int W, int clamp_in,
+                       hipStream_t st) {
+  size_t blocks = ((size_t)B * H * W + 255) / 256;
+  if (blocks > 16384) blocks = 16384;
+  hipLaunchKernelGGL(pack_input_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, u32, u16, B, C, H, W,
+                     clamp_in);
+}
+
+}  // namespace pnp

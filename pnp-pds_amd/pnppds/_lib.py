@@ -1,0 +1,262 @@
+"""ctypes binding of libpnppds.so (include/pnppds.h).
+
+There is no CPU fallback: if the library is missing or no gfx950 device is present,
+every compute call raises.  The library is built in-tree by ``make -C pnp-pds_amd``
+(``__graft_entry__.build()``).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libpnppds.so")
+
+PNP_OK = 0
+ERRORS = {-1: "PNP_E_ARG", -2: "PNP_E_UNSUPPORTED", -3: "PNP_E_HIP", -4: "PNP_E_OOM", -5: "PNP_E_STATE"}
+
+METHOD_A, METHOD_B, METHOD_C, METHOD_ADMM_B2 = 0, 1, 2, 3
+OP_ID, OP_BLUR, OP_RANDOM_SAMPLING = 0, 1, 2
+
+
+class PnpError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"{ERRORS.get(code, code)}: {msg}")
+        self.code = code
+
+
+class pnp_params(C.Structure):
+    _fields_ = [("gamma1", C.c_double), ("gamma2", C.c_double), ("alpha_s", C.c_double),
+                ("alpha_n", C.c_double), ("my_lambda", C.c_double), ("m1", C.c_int32), ("m2", C.c_int32),
+                ("gamma_in_admm_step1", C.c_double), ("gaussian_nl", C.c_double), ("sp_nl", C.c_double),
+                ("poisson_alpha", C.c_double), ("r", C.c_double), ("record_metrics", C.c_int32)]
+
+
+_lib = None
+_lock = threading.Lock()
+
+_P = C.c_void_p
+_F = C.POINTER(C.c_float)
+_D = C.POINTER(C.c_double)
+_SIGS = {
+    "pnp_abi_version": ([], C.c_int),
+    "pnp_device_count": ([C.POINTER(C.c_int)], C.c_int),
+    "pnp_create": ([C.c_int, C.POINTER(_P)], C.c_int),
+    "pnp_destroy": ([_P], C.c_int),
+    "pnp_last_error": ([_P], C.c_char_p),
+    "pnp_synchronize": ([_P], C.c_int),
+    "pnp_set_denoiser": ([_P, C.c_int, C.c_int, C.c_int, _F, C.c_size_t, C.c_int, C.c_int, C.c_int], C.c_int),
+    "pnp_set_precision": ([_P, C.c_int], C.c_int),
+    "pnp_set_operator": ([_P, C.c_int, _D, C.c_int, C.c_int, C.POINTER(C.c_uint8), C.c_int, C.c_int], C.c_int),
+    "pnp_run": ([_P, C.c_int, C.POINTER(pnp_params), C.c_int, C.c_int, C.c_int, C.c_int, _F, _F, _F, C.c_int,
+                 _F, _F, _D, _D, _D], C.c_int),
+    "pnp_solver_setup": ([_P, C.c_int, C.POINTER(pnp_params), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int],
+                         C.c_int),
+    "pnp_solver_load": ([_P, _F, _F, _F], C.c_int),
+    "pnp_solver_load_device": ([_P, _P, _P, _P], C.c_int),
+    "pnp_solver_iterate": ([_P, C.c_int], C.c_int),
+    "pnp_solver_fetch": ([_P, _F, _F, _D, _D], C.c_int),
+    "pnp_solver_iterations_done": ([_P, C.POINTER(C.c_int)], C.c_int),
+    "pnp_solver_state": ([_P, C.POINTER(_P), C.POINTER(_P), C.POINTER(_P)], C.c_int),
+    "pnp_profile_enable": ([_P, C.c_int], C.c_int),
+    "pnp_profile_read": ([_P, C.c_int, C.POINTER(C.c_char_p), _D, C.POINTER(C.c_int), C.POINTER(C.c_int)],
+                         C.c_int),
+    "pnp_op_phi": ([_P, _P, _P, C.c_int, C.c_int, C.c_int, C.c_int, _P], C.c_int),
+    "pnp_op_adj_phi": ([_P, _P, _P, C.c_int, C.c_int, C.c_int, C.c_int, _P], C.c_int),
+    "pnp_op_proj_l2_ball": ([_P, _P, _P, _P, C.c_int, C.c_int64, C.c_double, C.c_double, C.c_double, C.c_double,
+                             _P], C.c_int),
+    "pnp_op_proj_l1_ball": ([_P, _P, _P, C.c_int, C.c_int64, C.c_double, C.c_double, C.c_double, _P], C.c_int),
+    "pnp_op_prox_gkl": ([_P, _P, _P, _P, C.c_int64, C.c_double, C.c_double, _P], C.c_int),
+    "pnp_op_denoise": ([_P, _P, _P, C.c_int, C.c_int, C.c_int, C.c_int, _P], C.c_int),
+    "pnp_op_psnr": ([_P, _P, _P, C.c_int, C.c_int64, _D, _P], C.c_int),
+}
+
+
+def load_library(path: str = LIB_PATH):
+    """Load libpnppds.so (raises if absent — there is no fallback path)."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(path):
+                raise RuntimeError(f"libpnppds.so not found at {path}; run `make -C pnp-pds_amd` "
+                                   "(or __graft_entry__.build())")
+            lib = C.CDLL(path)
+            for name, (args, res) in _SIGS.items():
+                fn = getattr(lib, name)
+                fn.argtypes = args
+                fn.restype = res
+            if lib.pnp_abi_version() != 1:
+                raise RuntimeError("libpnppds ABI mismatch")
+            _lib = lib
+    return _lib
+
+
+def _fptr(a):
+    return a.ctypes.data_as(_F) if a is not None else None
+
+
+def _dptr(a):
+    return a.ctypes.data_as(_D) if a is not None else None
+
+
+def device_count() -> int:
+    lib = load_library()
+    n = C.c_int(0)
+    rc = lib.pnp_device_count(C.byref(n))
+    if rc != PNP_OK:
+        return 0
+    return n.value
+
+
+def as_f32(a):
+    return np.ascontiguousarray(a, dtype=np.float32)
+
+
+class Context:
+    """One device context (one GPU).  Not thread-safe; one per host thread / rank."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load_library()
+        self.device = device
+        h = _P()
+        rc = self.lib.pnp_create(device, C.byref(h))
+        if rc != PNP_OK:
+            raise PnpError(rc, self.lib.pnp_last_error(None).decode())
+        self.h = h
+        self._denoiser_key = None
+        self._operator_key = None
+
+    # -- plumbing --
+    def _check(self, rc):
+        if rc != PNP_OK:
+            raise PnpError(rc, self.lib.pnp_last_error(self.h).decode())
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.pnp_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def synchronize(self):
+        self._check(self.lib.pnp_synchronize(self.h))
+
+    # -- configuration --
+    def set_denoiser(self, weights, key=None):
+        """weights: pnppds.weights.DenoiserWeights."""
+        if key is not None and key == self._denoiser_key:
+            return
+        flat = as_f32(weights.flat())
+        self._check(self.lib.pnp_set_denoiser(self.h, weights.channels, weights.depth, weights.width,
+                                              _fptr(flat), flat.size, weights.act, weights.residual,
+                                              weights.clamp_io))
+        self._denoiser_key = key
+
+    def set_operator(self, kind: int, h=None, mask=None, key=None):
+        if key is not None and key == self._operator_key:
+            return
+        hh = np.ascontiguousarray(h, np.float64) if h is not None else None
+        mm = np.ascontiguousarray(mask, np.uint8) if mask is not None else None
+        self._check(self.lib.pnp_set_operator(
+            self.h, kind, hh.ctypes.data_as(_D) if hh is not None else None,
+            hh.shape[0] if hh is not None else 0, hh.shape[1] if hh is not None else 0,
+            mm.ctypes.data_as(C.POINTER(C.c_uint8)) if mm is not None else None,
+            mm.shape[0] if mm is not None else 0, mm.shape[1] if mm is not None else 0))
+        self._operator_key = key
+
+    # -- whole solver --
+    def run(self, method, params: pnp_params, x0, xobs, xtrue, max_iter, want_s=True):
+        x0, xobs = as_f32(x0), as_f32(xobs)
+        xtrue = as_f32(xtrue) if xtrue is not None else None
+        B, Cc, H, W = x0.shape
+        x_out = np.empty_like(x0)
+        s_out = np.empty_like(x0) if want_s else None
+        c_out = np.empty((B, max_iter), np.float64)
+        p_out = np.empty((B, max_iter), np.float64)
+        t = C.c_double(0)
+        self._check(self.lib.pnp_run(self.h, method, C.byref(params), B, Cc, H, W, _fptr(x0), _fptr(xobs),
+                                     _fptr(xtrue), max_iter, _fptr(x_out), _fptr(s_out), _dptr(c_out),
+                                     _dptr(p_out), C.byref(t)))
+        return x_out, s_out, c_out, p_out, t.value
+
+    def solver_setup(self, method, params, B, Cc, H, W, cap):
+        self._check(self.lib.pnp_solver_setup(self.h, method, C.byref(params), B, Cc, H, W, cap))
+        self._shape = (B, Cc, H, W)
+        self._cap = cap
+
+    def solver_load(self, x0, xobs, xtrue=None):
+        x0, xobs = as_f32(x0), as_f32(xobs)
+        xtrue = as_f32(xtrue) if xtrue is not None else None
+        self._check(self.lib.pnp_solver_load(self.h, _fptr(x0), _fptr(xobs), _fptr(xtrue)))
+
+    def solver_load_device(self, d_x0: int, d_xobs: int, d_xtrue: int | None):
+        self._check(self.lib.pnp_solver_load_device(self.h, _P(d_x0), _P(d_xobs),
+                                                    _P(d_xtrue) if d_xtrue else None))
+
+    def solver_iterate(self, n):
+        self._check(self.lib.pnp_solver_iterate(self.h, n))
+
+    def solver_fetch(self):
+        B, Cc, H, W = self._shape
+        x = np.empty((B, Cc, H, W), np.float32)
+        s = np.empty((B, Cc, H, W), np.float32)
+        c = np.empty((B, max(self._cap, 0)), np.float64)
+        p = np.empty((B, max(self._cap, 0)), np.float64)
+        self._check(self.lib.pnp_solver_fetch(self.h, _fptr(x), _fptr(s), _dptr(c), _dptr(p)))
+        return x, s, c, p
+
+    def profile_enable(self, on=True):
+        self._check(self.lib.pnp_profile_enable(self.h, 1 if on else 0))
+
+    def profile_read(self):
+        cap = 64
+        names = (C.c_char_p * cap)()
+        avg = (C.c_double * cap)()
+        calls = (C.c_int * cap)()
+        n = C.c_int(0)
+        self._check(self.lib.pnp_profile_read(self.h, cap, names, avg, calls, C.byref(n)))
+        return {names[i].decode(): (avg[i], calls[i]) for i in range(n.value)}
+
+    # -- single operators on device pointers (ints from e.g. torch.Tensor.data_ptr()) --
+    def op_phi(self, x, y, B, Cc, H, W, adj=False, stream=None):
+        fn = self.lib.pnp_op_adj_phi if adj else self.lib.pnp_op_phi
+        self._check(fn(self.h, _P(x), _P(y), B, Cc, H, W, _P(stream) if stream else None))
+
+    def op_proj_l2_ball(self, x, x0, out, B, n, alpha_n, gaussian_nl, sp_nl, r=1.0, stream=None):
+        self._check(self.lib.pnp_op_proj_l2_ball(self.h, _P(x), _P(x0), _P(out), B, n, alpha_n, gaussian_nl,
+                                                 sp_nl, r, _P(stream) if stream else None))
+
+    def op_proj_l1_ball(self, x, out, B, n, alpha_s, sp_nl, r=1.0, stream=None):
+        self._check(self.lib.pnp_op_proj_l1_ball(self.h, _P(x), _P(out), B, n, alpha_s, sp_nl, r,
+                                                 _P(stream) if stream else None))
+
+    def op_prox_gkl(self, x, x0, out, count, gamma, alpha, stream=None):
+        self._check(self.lib.pnp_op_prox_gkl(self.h, _P(x), _P(x0), _P(out), count, gamma, alpha,
+                                             _P(stream) if stream else None))
+
+    def op_denoise(self, x, out, B, Cc, H, W, stream=None):
+        self._check(self.lib.pnp_op_denoise(self.h, _P(x), _P(out), B, Cc, H, W, _P(stream) if stream else None))
+
+    def op_psnr(self, xt, x, B, n, stream=None):
+        out = np.empty(B, np.float64)
+        self._check(self.lib.pnp_op_psnr(self.h, _P(xt), _P(x), B, n, _dptr(out), _P(stream) if stream else None))
+        return out
+
+
+_contexts: dict = {}
+
+
+def get_context(device: int = 0) -> Context:
+    """Process-wide cached context per device."""
+    ctx = _contexts.get(device)
+    if ctx is None:
+        ctx = Context(device)
+        _contexts[device] = ctx
+    return ctx

@@ -1,0 +1,106 @@
+"""test_iter — device-resident mirror of iteration.test_iter (iteration.py:10-196).
+
+Same positional signature and return tuple as the reference:
+    x_n, s_n + 0.5, c[max_iter], psnr[max_iter], ssim[max_iter], average_time
+The whole loop (primal prox step through the MFMA denoiser, dual ascent with Φ/Φᵀ,
+over-relaxation, l2-ball / l1-ball / GKL proxes, c_n and PSNR) runs on the MI355X via
+``pnp_run``; nothing is computed on the host.
+
+Differences from the reference, by design:
+  * method names: README's 'ours-A/B/C' are accepted as aliases of 'A/B/C-Proposed'
+    (the reference only recognises the latter, iteration.py:48-63, and crashes on the
+    README names at :183-185); unknown methods raise ValueError.
+  * ``phi``/``adj_phi`` must come from pnppds.operators.get_observation_operators (opaque
+    Python closures cannot run on the device; there is no host fallback).
+  * state is fp32 on the device (the reference mixes fp32 x and fp64 y); denoiser
+    operands are fp16 with fp32 accumulation.  Tolerances: DESIGN.md §Parity.
+  * ``ssim`` is not computed on the device yet (utils_eval.eval_ssim needs skimage,
+    which is absent here, so it is also unpinned); it is returned as NaN.
+  * ``average_time`` is wall-clock seconds per iteration (the reference reports
+    process_time, iteration.py:43,193-194).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import _lib
+from ._device import get_ctx
+from .denoiser import Denoiser
+from .operators import ObservationOperator
+from .weights import DenoiserWeights
+
+METHODS = {
+    "A-Proposed": _lib.METHOD_A, "ours-A": _lib.METHOD_A,
+    "B-Proposed": _lib.METHOD_B, "ours-B": _lib.METHOD_B,
+    "C-Proposed": _lib.METHOD_C, "ours-C": _lib.METHOD_C,
+}
+
+
+def make_params(gamma1, gamma2, alpha_s, alpha_n, myLambda, m1, m2, gammaInADMMStep1, gaussian_nl, sp_nl,
+                poisson_alpha, r, record_metrics=True) -> _lib.pnp_params:
+    return _lib.pnp_params(float(gamma1), float(gamma2), float(alpha_s), float(alpha_n), float(myLambda),
+                           int(m1), int(m2), float(gammaInADMMStep1), float(gaussian_nl), float(sp_nl),
+                           float(poisson_alpha), float(r), 1 if record_metrics else 0)
+
+
+def resolve_method(method: str) -> int:
+    if method not in METHODS:
+        raise ValueError(f"Unknown method: {method!r} (device path supports {sorted(METHODS)})")
+    return METHODS[method]
+
+
+def _resolve_denoiser(path_prox, ch) -> Denoiser:
+    if isinstance(path_prox, Denoiser):
+        return path_prox
+    if isinstance(path_prox, DenoiserWeights):
+        return Denoiser(path_prox.name, ch, weights=path_prox)
+    return Denoiser(path_prox, ch)
+
+
+def _check_ops(phi, adj_phi):
+    if not isinstance(phi, ObservationOperator) or not isinstance(adj_phi, ObservationOperator):
+        raise TypeError("phi/adj_phi must come from pnppds.operators.get_observation_operators "
+                        "(the device solver needs the operator's description, not a closure)")
+    if phi.kind != adj_phi.kind or adj_phi.adjoint is phi.adjoint:
+        raise ValueError("adj_phi must be the adjoint of phi")
+
+
+def test_iter_batch(x_0, x_obsrv, x_true, phi, adj_phi, gamma1, gamma2, alpha_s, alpha_n, myLambda, m1, m2,
+                    gammaInADMMStep1, gaussian_nl, sp_nl, poisson_alpha, path_prox, max_iter,
+                    method="A-Proposed", ch=3, r=1, record_metrics=True, ctx=None):
+    """Batched test_iter over B independent images: arrays are [B, C, H, W].
+    Returns (x[B,C,H,W] f32, s+0.5 [B,C,H,W] f32, c[B,max_iter], psnr[B,max_iter], ssim, avg_time)."""
+    m = resolve_method(method)
+    _check_ops(phi, adj_phi)
+    x0 = np.asarray(x_0)
+    if x0.ndim != 4:
+        raise ValueError("test_iter_batch expects [B, C, H, W] arrays")
+    B, Cc, H, W = x0.shape
+    if Cc != ch:
+        raise ValueError(f"ch={ch} but images have {Cc} channels")
+    ctx = ctx or get_ctx()
+    den = _resolve_denoiser(path_prox, ch)
+    den.configure(ctx)
+    phi.configure(ctx, H, W)
+    prm = make_params(gamma1, gamma2, alpha_s, alpha_n, myLambda, m1, m2, gammaInADMMStep1, gaussian_nl, sp_nl,
+                      poisson_alpha, r, record_metrics)
+    xt = None if x_true is None else np.broadcast_to(np.asarray(x_true, np.float32), x0.shape)
+    xo = np.broadcast_to(np.asarray(x_obsrv, np.float32), x0.shape)
+    x, s, c, psnr, t = ctx.run(m, prm, x0, xo, xt, int(max_iter))
+    ssim = np.full((B, int(max_iter)), np.nan)
+    return x, s, c, psnr, ssim, t
+
+
+def test_iter(x_0, x_obsrv, x_true, phi, adj_phi, gamma1, gamma2, alpha_s, alpha_n, myLambda, m1, m2,
+              gammaInADMMStep1, gaussian_nl, sp_nl, poisson_alpha, path_prox, max_iter, method="A-Proposed",
+              ch=3, r=1):
+    """iteration.py:10 signature; x_0 etc. are (C,H,W) (RGB) or (H,W) (gray)."""
+    x0 = np.asarray(x_0)
+    shp = x0.shape
+    to4 = (lambda a: np.asarray(a).reshape((1, 1) + shp)) if x0.ndim == 2 else \
+        (lambda a: np.asarray(a).reshape((1,) + shp))
+    x, s, c, psnr, ssim, t = test_iter_batch(to4(x0), to4(x_obsrv), None if x_true is None else to4(x_true),
+                                             phi, adj_phi, gamma1, gamma2, alpha_s, alpha_n, myLambda, m1, m2,
+                                             gammaInADMMStep1, gaussian_nl, sp_nl, poisson_alpha, path_prox,
+                                             max_iter, method, ch, r)
+    return x.reshape(shp), s.reshape(shp).astype(np.float64), c[0], psnr[0], ssim[0], t

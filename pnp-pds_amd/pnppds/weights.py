@@ -355,7 +355,10 @@ def resolve_weights(file_name: str, channels: int | None = None) -> DenoiserWeig
     conversion if the .pth itself is present and no npz exists."""
     if file_name.endswith(".npz") and os.path.exists(file_name):
         return DenoiserWeights.load_npz(file_name)
-    stem = os.path.splitext(os.path.basename(file_name))[0]
+    stem = os.path.basename(file_name)
+    for ext in (".pth", ".npz", ".pt"):
+        if stem.endswith(ext):
+            stem = stem[: -len(ext)]
     npz = os.path.join(WEIGHTS_DIR, stem + ".npz")
     if os.path.exists(npz):
         w = DenoiserWeights.load_npz(npz)

@@ -1,0 +1,79 @@
+"""C-ABI: the library builds, loads and exports every symbol include/pnppds.h declares.
+CPU-only (no compute calls)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import REPO
+
+HEADER = os.path.join(REPO, "include", "pnppds.h")
+LIB = os.path.join(REPO, "pnp-pds_amd", "lib", "libpnppds.so")
+
+
+def declared_symbols():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(pnp_\w+)\s*\(", src, flags=re.M)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not os.path.exists(LIB):
+        subprocess.run(["make", "-C", os.path.join(REPO, "pnp-pds_amd"), "-j8"], check=True,
+                       capture_output=True)
+    return ctypes.CDLL(LIB)
+
+
+def test_header_declares_entry_points():
+    syms = declared_symbols()
+    for s in ("pnp_create", "pnp_run", "pnp_set_denoiser", "pnp_set_operator", "pnp_op_denoise",
+              "pnp_op_proj_l1_ball", "pnp_op_proj_l2_ball", "pnp_op_prox_gkl", "pnp_solver_iterate"):
+        assert s in syms
+    assert len(syms) >= 25
+
+
+def test_library_exports_every_declared_symbol(lib):
+    missing = [s for s in declared_symbols() if not hasattr(lib, s)]
+    assert not missing, missing
+
+
+def test_exports_are_plain_c(lib):
+    out = subprocess.run(["nm", "-D", "--defined-only", LIB], capture_output=True, text=True, check=True).stdout
+    exported = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
+    for s in declared_symbols():
+        assert s in exported, s           # unmangled extern "C"
+
+
+def test_abi_version_and_errors_without_gpu(lib):
+    assert lib.pnp_abi_version() == 1
+    lib.pnp_last_error.restype = ctypes.c_char_p
+    h = ctypes.c_void_p()
+    rc = lib.pnp_create(0, ctypes.byref(h))
+    if rc != 0:      # no GPU here: must fail loudly with a message, never fall back
+        assert rc in (-2, -3)
+        assert lib.pnp_last_error(None)
+        assert not h.value
+
+
+def test_null_context_is_rejected(lib):
+    assert lib.pnp_solver_iterate(None, 1) == -1
+    assert lib.pnp_synchronize(None) == -1
+
+
+def test_params_struct_layout():
+    from pnppds import _lib
+    # 5 doubles, 2 int32, 5 doubles, 1 int32 (+4 padding) as in pnppds.h
+    assert ctypes.sizeof(_lib.pnp_params) == 8 * 5 + 4 * 2 + 8 * 5 + 8
+    assert _lib.pnp_params.m1.offset == 40 and _lib.pnp_params.gamma_in_admm_step1.offset == 48
+
+
+def test_product_does_not_import_oracle():
+    """The shipped package never references the test oracle."""
+    pkg = os.path.join(REPO, "pnp-pds_amd")
+    for root, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith((".py", ".hip", ".h")):
+                txt = open(os.path.join(root, f)).read()
+                assert "pnp_oracle" not in txt and "import oracle" not in txt, f

@@ -1,0 +1,93 @@
+"""GPU parity of the whole on-device PnP-PDS loop vs trajectories of the reference's test_iter."""
+import numpy as np
+import pytest
+
+from conftest import load_golden
+from oracle import pnp_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+CASES = ["A_blur", "A_id", "A_rs", "A_gray", "B_blur", "C_rs", "C_blur"]
+
+
+def run_case(g):
+    from pnppds import operators as ops
+    from pnppds.iteration import test_iter
+    g1, g2, as_, an, lam, m1, m2, gadmm, sig, sp, palpha, iters, ch, r = g["params"]
+    phi, adj = ops.get_observation_operators(str(g["deg_op"]), "blur_1", r)
+    return test_iter(g["x_0"], g["x_obs"], g["x_true"], phi, adj, g1, g2, as_, an, lam, int(m1), int(m2), gadmm,
+                     sig, sp, palpha, str(g["arch"]) + ".pth", int(iters), str(g["method"]), int(ch), r)
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_trajectory_matches_reference(case):
+    g = load_golden(f"iter_{case}.npz")
+    x, s, c, psnr, ssim, t = run_case(g)
+    assert x.shape == g["x_out"].shape and x.dtype == np.float32
+    # PSNR within the north-star tolerance (0.01 dB) at every iteration
+    np.testing.assert_allclose(psnr, g["psnr"], atol=0.01)
+    np.testing.assert_allclose(x, g["x_out"], atol=5e-3)
+    np.testing.assert_allclose(c, g["c"], rtol=0.05, atol=2e-4)
+    np.testing.assert_allclose(s, g["s_out"], atol=5e-3 if case.startswith("B") else 1e-7)
+    assert t > 0
+
+
+def test_long_run_psnr_within_001db():
+    """3x256x256, ours-A + blur, 120 iterations: every PSNR within 0.01 dB of the reference."""
+    from pnppds import operators as ops
+    from pnppds.iteration import test_iter
+    g = load_golden("long_A_blur_256.npz")
+    phi, adj = ops.get_observation_operators("blur", "blur_1", 0.8)
+    x, s, c, psnr, ssim, t = test_iter(g["x_obs"], g["x_obs"], g["x_true"], phi, adj, 0.99, 0.99, 1.0, 0.95, 1.0,
+                                       15, 15, 0.1, 0.01, 0.0, 300, "DnCNN_nobn_nch_3_nlev_0.01.pth", 120,
+                                       "ours-A", 3, 0.8)
+    d = np.abs(psnr - g["psnr"])
+    assert d.max() < 0.01, (d.max(), int(d.argmax()))
+    np.testing.assert_allclose(x, g["x_out"].astype(np.float32), atol=2e-3)
+
+
+def test_batch_equals_single_images():
+    """Images are independent: a batch gives bit-identical results to one-image runs
+    (the property the multi-GPU sharding relies on)."""
+    from pnppds import operators as ops
+    from pnppds.iteration import test_iter_batch
+    g = load_golden("iter_B_blur.npz")
+    g1, g2, as_, an, lam, m1, m2, gadmm, sig, sp, palpha, iters, ch, r = g["params"]
+    rng = np.random.default_rng(0)
+    xt = np.stack([g["x_true"], np.clip(g["x_true"] + 0.05 * rng.standard_normal(g["x_true"].shape), 0, 1),
+                   g["x_true"][:, ::-1, :]]).astype(np.float32)
+    phi, adj = ops.get_observation_operators("blur", "blur_1", r)
+    xo = np.stack([O.blur(a, ops.load_blur_kernel("blur_1")) + 0.01 * rng.standard_normal(a.shape) for a in xt])
+    args = (g1, g2, as_, an, lam, int(m1), int(m2), gadmm, sig, sp, palpha, "DnCNN_nobn_nch_3_nlev_0.01", 4,
+            "B-Proposed", 3, r)
+    xb, sb, cb, pb, _, _ = test_iter_batch(xo, xo, xt, phi, adj, *args)
+    for i in range(3):
+        x1, s1, c1, p1, _, _ = test_iter_batch(xo[i:i + 1], xo[i:i + 1], xt[i:i + 1], phi, adj, *args)
+        np.testing.assert_array_equal(x1[0], xb[i])
+        np.testing.assert_array_equal(s1[0], sb[i])
+        np.testing.assert_array_equal(p1[0], pb[i])
+
+
+def test_unknown_method_and_closure_rejected():
+    from pnppds import operators as ops
+    from pnppds.iteration import test_iter
+    x = np.zeros((3, 16, 16))
+    phi, adj = ops.get_observation_operators("Id", "blur_1", 0.8)
+    with pytest.raises(ValueError):
+        test_iter(x, x, x, phi, adj, 1, 1, 1, 1, 1, 1, 1, 0.1, 0.01, 0, 300, "DnCNN_nobn_nch_3_nlev_0.01", 1,
+                  "A-PDS-TV", 3, 1)
+    with pytest.raises(TypeError):
+        test_iter(x, x, x, lambda v: v, lambda v: v, 1, 1, 1, 1, 1, 1, 1, 0.1, 0.01, 0, 300,
+                  "DnCNN_nobn_nch_3_nlev_0.01", 1, "A-Proposed", 3, 1)
+
+
+def test_numpy_api_mirrors_reference(golden_ops):
+    """pnppds.operators functions (numpy in / numpy out, device inside) vs golden."""
+    from pnppds import operators as ops
+    g = golden_ops
+    phi, adj = ops.get_observation_operators("blur", "blur_1", 0.8)
+    np.testing.assert_allclose(phi(g["x_rgb64"]), g["phi_blur_rgb64"], atol=2e-6)
+    np.testing.assert_allclose(adj(g["x_gray64"]), g["adj_blur_gray64"], atol=2e-6)
+    v, x0 = g["prox_v"], g["prox_x0"]
+    np.testing.assert_allclose(ops.proj_l2_ball(x0 + v, 0.95, 0.01, 0.1, x0, 0.8), g["l2_0.01_0.95"], atol=2e-7)
+    np.testing.assert_allclose(ops.proj_l1_ball(v, 0.95, 0.1, 0.8), g["l1_0.1"], atol=1e-6)
