@@ -78,7 +78,7 @@ def cpu_baseline(x_true, x_obs, h, budget_s, max_iter):
     import torch
     from oracle import pnp_oracle as O
     from pnppds.weights import resolve_weights
-    torch.set_num_threads(os.cpu_count() or 1)
+    torch.set_num_threads(int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1))
     den = O.OracleDenoiser(resolve_weights(ARCH, 3))
     phi, adj = O.observation_operators("blur", h)
     xo = x_obs.astype(np.float64)

@@ -27,29 +27,66 @@ __device__ __forceinline__ void decode_tile(int t, const ConvShape& s, int& b, i
   tx0 = (r - ty * s.tiles_x) * kTileW;
 }
 
-// Stage the 10 x 34 x 64-channel halo tile (padded coords [ty0, ty0+10) x [tx0, tx0+34))
-// into the swizzled LDS image.  2720 16-byte chunks, 11 per thread; consecutive threads
-// read consecutive 16 B of a pixel row (coalesced), write 8 lanes per 128-B pixel.
+// The 10 x 34 x 64-channel halo tile (padded coords [ty0, ty0+10) x [tx0, tx0+34)) is
+// 2720 16-byte chunks: 11 per thread.  Consecutive threads read consecutive 16 B of a
+// pixel row (coalesced); 8 lanes write one 128-B pixel of the swizzled LDS image.
+constexpr int kHaloChunks = kHaloPix * 8;
+constexpr int kHaloPerThread = (kHaloChunks + 255) / 256;
+
+// Issue the global loads of a halo tile into registers (no wait: T14 issue-early).
+// Every lane loads unconditionally (surplus lanes re-read the last pixel): a guarded load
+// makes hipcc merge the destination through a branch and wait vmcnt right after issue.
+__device__ __forceinline__ void halo_load(uint4 (&v)[kHaloPerThread], const half_t* __restrict__ in,
+                                          const ConvShape& s, int b, int ty0, int tx0) {
+  const half_t* base = in + (((size_t)b * s.Hp + ty0) * s.Wp + tx0) * kWidth;
+#pragma unroll
+  for (int k = 0; k < kHaloPerThread; ++k) {
+    const int q = threadIdx.x + 256 * k;
+    const int p = min(q >> 3, kHaloPix - 1), c = q & 7;
+    const int pr = p / kHaloW, pc = p - pr * kHaloW;
+    v[k] = *reinterpret_cast<const uint4*>(base + ((size_t)pr * s.Wp + pc) * kWidth + c * 8);
+  }
+}
+
+// Write a loaded halo tile into an LDS image (write-late).
+__device__ __forceinline__ void halo_store(unsigned char* hl, const uint4 (&v)[kHaloPerThread]) {
+#pragma unroll
+  for (int k = 0; k < kHaloPerThread; ++k) {
+    const int q = threadIdx.x + 256 * k;
+    if (q < kHaloChunks) *reinterpret_cast<uint4*>(hl + halo_chunk_offset(q >> 3, q & 7)) = v[k];
+  }
+}
+
 __device__ __forceinline__ void stage_halo64(unsigned char* hl, const half_t* __restrict__ in,
                                              const ConvShape& s, int b, int ty0, int tx0) {
+  uint4 v[kHaloPerThread];
+  halo_load(v, in, s, b, ty0, tx0);
+  halo_store(hl, v);
+}
+
+// LDS-DMA (global_load_lds_dwordx4) staging of a halo tile: no register destination, so
+// the loads stay in flight across the MFMA loop.  One wave-instruction writes 1 KiB of
+// LDS = 8 pixels: slot g (g = 4j + wave, 43 slots) covers pixels 8g .. 8g+7.  The LDS
+// destination is lane-linear, so the XOR swizzle is applied to the per-lane SOURCE
+// address (lane l loads logical chunk (l&7) ^ swz(p) of pixel p into slot l&7).  Slots
+// past pixel 339 re-read pixel 339 into the 4-pixel pad (never read back).
+constexpr int kDmaSlots = (kHaloPix + 7) / 8;                 // 43
+constexpr int kHaloDmaBytes = kDmaSlots * 1024;               // 44032
+__device__ __forceinline__ void halo_dma(unsigned char* hl, const half_t* __restrict__ in, const ConvShape& s,
+                                         int b, int ty0, int tx0) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const half_t* base = in + (((size_t)b * s.Hp + ty0) * s.Wp + tx0) * kWidth;
-  constexpr int kChunks = kHaloPix * 8;
-  uint4 v[(kChunks + 255) / 256];
 #pragma unroll
-  for (int k = 0; k < (kChunks + 255) / 256; ++k) {
-    const int q = threadIdx.x + 256 * k;
-    if (q < kChunks) {
-      const int p = q >> 3, c = q & 7;
-      const int pr = p / kHaloW, pc = p - pr * kHaloW;
-      v[k] = *reinterpret_cast<const uint4*>(base + ((size_t)pr * s.Wp + pc) * kWidth + c * 8);
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < (kChunks + 255) / 256; ++k) {
-    const int q = threadIdx.x + 256 * k;
-    if (q < kChunks) {
-      const int p = q >> 3, c = q & 7;
-      *reinterpret_cast<uint4*>(hl + halo_chunk_offset(p, c)) = v[k];
+  for (int j = 0; j < (kDmaSlots + 3) / 4; ++j) {
+    const int g = 4 * j + wave;
+    if (g < kDmaSlots) {
+      const int p = 8 * g + (lane >> 3);
+      const int c = (lane & 7) ^ ((p >> 1) & 7);
+      const int pl = min(p, kHaloPix - 1);
+      const int pr = pl / kHaloW, pc = pl - pr * kHaloW;
+      const half_t* src = base + ((size_t)pr * s.Wp + pc) * kWidth + c * 8;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)(hl + g * 1024), 16, 0, 0);
     }
   }
 }
@@ -76,9 +113,14 @@ __device__ __forceinline__ void store_act64(half_t* __restrict__ out, const Conv
 }
 
 // ------------------------------------------------------------------------------------
-// Body layer 64 -> 64 (basic_models.py:16-17,29-33).  LDS: 72 KiB weights + 42.5 KiB
-// halo tile = 114.5 KiB -> one workgroup (4 waves) per CU, persistent over tiles.
+// Body layer 64 -> 64 (basic_models.py:16-17,29-33).  LDS: 72 KiB weights + two 42.5 KiB
+// halo buffers = 157 KiB -> one workgroup (4 waves) per CU, persistent over tiles.
+// Software pipeline per tile: issue the global loads of tile t+1 into registers, run
+// tile t's 144 MFMAs/wave from LDS buffer `cur`, store tile t, then write tile t+1 into
+// buffer `cur^1`; one barrier per tile.
 // ------------------------------------------------------------------------------------
+constexpr int kHaloBytes = kHaloPix * 128;
+
 __global__ __launch_bounds__(256, 1) void conv_body_kernel(const half_t* __restrict__ in,
                                                             half_t* __restrict__ out,
                                                             const uint4* __restrict__ wpk,
@@ -86,7 +128,6 @@ __global__ __launch_bounds__(256, 1) void conv_body_kernel(const half_t* __restr
                                                             ConvShape s, int act) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned char* wl = smem;
-  unsigned char* hl = smem + kBodyWBytes;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int h = lane >> 5, col = lane & 31;
 
@@ -97,35 +138,54 @@ __global__ __launch_bounds__(256, 1) void conv_body_kernel(const half_t* __restr
 #pragma unroll
     for (int r = 0; r < 16; ++r) bias_r[m][r] = bias[32 * m + 16 * h + r];
 
-  for (int t = blockIdx.x; t < s.tiles; t += gridDim.x) {
+  int t = blockIdx.x;
+  int cur = 0;
+  if (t < s.tiles) {
     int b, ty0, tx0;
     decode_tile(t, s, b, ty0, tx0);
-    __syncthreads();                      // previous tile's reads of hl are done
-    stage_halo64(hl, in, s, b, ty0, tx0);
-    __syncthreads();
+    halo_dma(smem + kBodyWBytes, in, s, b, ty0, tx0);
+  }
+  __syncthreads();                            // drains the DMA (vmcnt(0)) + barrier
+  for (; t < s.tiles; t += gridDim.x) {
+    int b, ty0, tx0;
+    decode_tile(t, s, b, ty0, tx0);
+    const int tn = t + gridDim.x;
+    if (tn < s.tiles) {                       // next tile -> the other buffer, in flight
+      int bn, tyn, txn;
+      decode_tile(tn, s, bn, tyn, txn);
+      halo_dma(smem + kBodyWBytes + (cur ^ 1) * kHaloDmaBytes, in, s, bn, tyn, txn);
+    }
+    const unsigned char* hl = smem + kBodyWBytes + cur * kHaloDmaBytes;
+    const int pw = 2 * wave * kHaloW + col;   // this lane's pixel at tap (0,0), N-tile 0
+    auto ldA = [&](int ks, int m) {
+      return *reinterpret_cast<const half8_t*>(wl + ((ks * 2 + m) * 64 + lane) * 16);
+    };
+    auto ldB = [&](int ks, int n) {
+      const int tap = ks >> 2, sub = ks & 3;
+      const int p = pw + (n + tap / 3) * kHaloW + tap % 3;
+      return *reinterpret_cast<const half8_t*>(hl + halo_chunk_offset(p, 2 * sub + h));
+    };
 
+    // K loop with the fragments of step ks+1 read from LDS while step ks's MFMAs run.
     floatx16 acc00 = {}, acc01 = {}, acc10 = {}, acc11 = {};
+    half8_t a0 = ldA(0, 0), a1 = ldA(0, 1), b0 = ldB(0, 0), b1 = ldB(0, 1);
 #pragma unroll
-    for (int tap = 0; tap < 9; ++tap) {
-      const int ky = tap / 3, kx = tap % 3;
-      const int p0 = (2 * wave + ky) * kHaloW + col + kx;
-      const int p1 = p0 + kHaloW;
-#pragma unroll
-      for (int sub = 0; sub < 4; ++sub) {
-        const int ks = tap * 4 + sub;
-        const half8_t a0 = *reinterpret_cast<const half8_t*>(wl + ((ks * 2 + 0) * 64 + lane) * 16);
-        const half8_t a1 = *reinterpret_cast<const half8_t*>(wl + ((ks * 2 + 1) * 64 + lane) * 16);
-        const int chunk = 2 * sub + h;
-        const half8_t b0 = *reinterpret_cast<const half8_t*>(hl + halo_chunk_offset(p0, chunk));
-        const half8_t b1 = *reinterpret_cast<const half8_t*>(hl + halo_chunk_offset(p1, chunk));
-        acc00 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b0, acc00, 0, 0, 0);
-        acc10 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b0, acc10, 0, 0, 0);
-        acc01 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b1, acc01, 0, 0, 0);
-        acc11 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b1, acc11, 0, 0, 0);
+    for (int ks = 0; ks < kBodyKSteps; ++ks) {
+      half8_t na0, na1, nb0, nb1;
+      if (ks + 1 < kBodyKSteps) {
+        na0 = ldA(ks + 1, 0); na1 = ldA(ks + 1, 1);
+        nb0 = ldB(ks + 1, 0); nb1 = ldB(ks + 1, 1);
       }
+      acc00 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b0, acc00, 0, 0, 0);
+      acc10 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b0, acc10, 0, 0, 0);
+      acc01 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b1, acc01, 0, 0, 0);
+      acc11 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b1, acc11, 0, 0, 0);
+      if (ks + 1 < kBodyKSteps) { a0 = na0; a1 = na1; b0 = nb0; b1 = nb1; }
     }
     store_act64(out, s, b, ty0 + 2 * wave, tx0 + col, h, acc00, acc10, bias_r, act);
     store_act64(out, s, b, ty0 + 2 * wave + 1, tx0 + col, h, acc01, acc11, bias_r, act);
+    __syncthreads();                          // next tile landed (vmcnt(0)); buffer cur free
+    cur ^= 1;
   }
 }
 
@@ -200,7 +260,6 @@ __global__ __launch_bounds__(256) void conv_tail_kernel(const half_t* __restrict
                                                          int clamp_out) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned char* wl = smem;
-  unsigned char* hl = smem + kTailWBytes;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int q4 = lane >> 4, c16 = lane & 15;
   for (int i = tid; i < kTailWBytes / 16; i += 256) reinterpret_cast<uint4*>(wl)[i] = wpk[i];
@@ -209,23 +268,35 @@ __global__ __launch_bounds__(256) void conv_tail_kernel(const half_t* __restrict
   for (int c = 0; c < kMaxC; ++c) bias_r[c] = c < C ? bias[c] : 0.f;
   const size_t plane = (size_t)s.H * s.W;
 
+  unsigned char* hl = smem + kTailWBytes;
   for (int t = blockIdx.x; t < s.tiles; t += gridDim.x) {
     int b, ty0, tx0;
     decode_tile(t, s, b, ty0, tx0);
-    __syncthreads();
+    __syncthreads();                      // previous tile's reads of hl are done
     stage_halo64(hl, in, s, b, ty0, tx0);
     __syncthreads();
+    auto ldB = [&](int ks, int n) {
+      const int tap = ks >> 1;
+      const int p = (2 * wave + (n >> 1) + tap / 3) * kHaloW + 16 * (n & 1) + c16 + tap % 3;
+      return *reinterpret_cast<const half8_t*>(hl + halo_chunk_offset(p, 4 * (ks & 1) + q4));
+    };
     floatx4 acc[4] = {};
+    half8_t a = *reinterpret_cast<const half8_t*>(wl + lane * 16);
+    half8_t bf[4] = {ldB(0, 0), ldB(0, 1), ldB(0, 2), ldB(0, 3)};
 #pragma unroll
-    for (int ks = 0; ks < kTailKSteps; ++ks) {
-      const int tap = ks >> 1, ky = tap / 3, kx = tap % 3;
-      const half8_t a = *reinterpret_cast<const half8_t*>(wl + (ks * 64 + lane) * 16);
-      const int chunk = 4 * (ks & 1) + q4;
+    for (int ks = 0; ks < kTailKSteps; ++ks) {          // step ks+1 read while ks computes
+      half8_t na, nb[4];
+      if (ks + 1 < kTailKSteps) {
+        na = *reinterpret_cast<const half8_t*>(wl + ((ks + 1) * 64 + lane) * 16);
 #pragma unroll
-      for (int n = 0; n < 4; ++n) {
-        const int p = (2 * wave + (n >> 1) + ky) * kHaloW + 16 * (n & 1) + c16 + kx;
-        const half8_t bf = *reinterpret_cast<const half8_t*>(hl + halo_chunk_offset(p, chunk));
-        acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, bf, acc[n], 0, 0, 0);
+        for (int n = 0; n < 4; ++n) nb[n] = ldB(ks + 1, n);
+      }
+#pragma unroll
+      for (int n = 0; n < 4; ++n) acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, bf[n], acc[n], 0, 0, 0);
+      if (ks + 1 < kTailKSteps) {
+        a = na;
+#pragma unroll
+        for (int n = 0; n < 4; ++n) bf[n] = nb[n];
       }
     }
     // C/D map of 16x16: col = lane & 15 (pixel), row = 4*(lane>>4) + r (output channel).
@@ -318,8 +389,8 @@ ConvShape make_conv_shape(int B, int H, int W) {
   return s;
 }
 
-constexpr int kBodyLds = kBodyWBytes + kHaloPix * 128;
-constexpr int kTailLds = kTailWBytes + kHaloPix * 128;
+constexpr int kBodyLds = kBodyWBytes + 2 * kHaloDmaBytes;   // 161792 B of the 160 KiB
+constexpr int kTailLds = kTailWBytes + kHaloBytes;        // 61952 B: two workgroups per CU
 
 hipError_t conv_kernels_init() {
   hipError_t e = hipFuncSetAttribute((const void*)conv_body_kernel,
