@@ -58,8 +58,17 @@ def synthetic_batch(B, C, H, W, seed):
     return out
 
 
-def conv_flops_per_launch(B, H, W):
-    return 2.0 * 64 * 64 * 9 * B * H * W
+def images_per_launch(B, H, W, chunk):
+    """Mirror of capi.hip denoise_chunk(): images per conv launch."""
+    if chunk > 0:
+        return min(chunk, B)
+    per_img = 2.0 * (H + 2) * (W + 2) * 64 * 2
+    return max(1, min(int(8e9 // per_img), B))
+
+
+def conv_flops_per_launch(m, H, W):
+    """Algorithmic FLOPs of one 64->64 3x3 conv launch over m images."""
+    return 2.0 * 64 * 64 * 9 * m * H * W
 
 
 def prox_bytes(B, C, H, W):
@@ -106,6 +115,10 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU-baseline work")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile", type=int, default=1, help="HIP-event per-kernel timing in the timed region")
+    ap.add_argument("--chunk", type=int, default=0, help="images per denoiser pass (0 = auto)")
+    ap.add_argument("--chunk-sweep", type=str, default="", help="e.g. 4,8,16,256: time each (stderr)")
+    ap.add_argument("--variant", type=int, default=3, help="conv_body kernel variant (0..3)")
+    ap.add_argument("--variant-sweep", type=str, default="", help="e.g. 0,1: interleaved A/B (stderr)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -142,11 +155,40 @@ def main():
 
     cap = Wm + K
     prm = make_params(GAMMA1, GAMMA2, 1.0, ALPHA_N, 1.0, 15, 15, 0.1, SIGMA, 0.0, 300, 0.8, True)
+    ctx.set_denoise_chunk(args.chunk)
     ctx.solver_setup(_lib.METHOD_A, prm, B, C, H, W, cap)
     ctx.solver_load_device(d_obs.data_ptr(), d_obs.data_ptr(), d_true.data_ptr())   # x_0 = x_obs (main.py:62)
     ctx.solver_iterate(Wm)
     ctx.synchronize()
     torch.cuda.synchronize()
+    for ch in [int(v) for v in args.chunk_sweep.split(",") if v]:
+        ctx.set_denoise_chunk(ch)
+        ctx.solver_iterate(1)
+        ctx.synchronize()
+        ts = time.perf_counter()
+        ctx.solver_iterate(3)
+        ctx.synchronize()
+        log(f"[sweep] chunk={ch}: {(time.perf_counter() - ts) / 3 * 1e3:.2f} ms/iter")
+    vs = [int(v) for v in args.variant_sweep.split(",") if v]
+    if vs:
+        res = {v: [] for v in vs}
+        for _ in range(3):                     # interleaved rounds in one process
+            for v in vs:
+                ctx.set_body_variant(v)
+                ctx.solver_iterate(1)
+                ctx.synchronize()
+                ts = time.perf_counter()
+                ctx.solver_iterate(2)
+                ctx.synchronize()
+                res[v].append((time.perf_counter() - ts) / 2 * 1e3)
+        for v in vs:
+            log(f"[variant] {v}: ms/iter median {sorted(res[v])[1]:.2f} min {min(res[v]):.2f}")
+    ctx.set_body_variant(args.variant)
+    if args.chunk_sweep or vs:                 # restart the trajectory after the sweep
+        ctx.set_denoise_chunk(args.chunk)
+        ctx.solver_load_device(d_obs.data_ptr(), d_obs.data_ptr(), d_true.data_ptr())
+        ctx.solver_iterate(Wm)
+        ctx.synchronize()
 
     # ---- timed region ------------------------------------------------------------------------
     if args.profile:
@@ -185,7 +227,7 @@ def main():
             kt = {k: round(v[0], 4) for k, v in prof.items()}
             line["kernel_ms"] = kt
             body_ms = prof["conv_body"][0]
-            fl = conv_flops_per_launch(B, H, W)
+            fl = conv_flops_per_launch(images_per_launch(B, H, W, args.chunk), H, W)
             ach = fl / (body_ms * 1e-3) / 1e12
             line["roofline"] = {"kernel": "conv_body (64->64 3x3 implicit GEMM, fp16 MFMA)", "bound": "mfma",
                                 "achieved": round(ach, 1), "peak": FP16_PEAK_TFLOPS, "unit": "TFLOP/s",

@@ -101,6 +101,16 @@ int pnp_set_denoiser(pnp_ctx* ctx, int channels, int depth, int width, const flo
                      size_t n_params, int activation, int residual_sign, int clamp_io);
 int pnp_set_precision(pnp_ctx* ctx, int precision);
 
+/* Performance knobs (no effect on results).
+ * PNP_TUNE_DENOISE_CHUNK: images per denoiser pass (0 = auto: the activation ping-pong
+ * pair of a pass is sized to stay resident in the 256 MB Infinity Cache).             */
+enum pnp_tuning_key {
+  PNP_TUNE_DENOISE_CHUNK = 1,
+  PNP_TUNE_BODY_VARIANT = 2   /* 64->64 conv kernel: 0 = 4 waves/WG, 1 = 8 waves/WG,
+                                 2 = warp-specialised, 3 = weights in registers (default) */
+};
+int pnp_set_tuning(pnp_ctx* ctx, int key, int value);
+
 /* Observation operator (operators.py:60-79).  BLUR: h is kh x kw float64 row-major
  * (blur_models/blur_1.mat: 19x19); RANDOM_SAMPLING: keep_mask is H x W uint8 (1 keeps
  * the pixel; the reference drops RandomState(1234).permutation(H*W)[:round(H*W*(1-r))]).

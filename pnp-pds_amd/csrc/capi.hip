@@ -47,6 +47,10 @@ struct pnp_ctx {
 
   // denoiser
   int den_C = 0, den_depth = 0, den_act = 0, den_residual = 1, den_clamp = 1;
+  int den_chunk = 0;   // images per denoiser pass; 0 = auto
+  int body_variant = 3;   // conv_body kernel: 0 = 4 waves x 2 rows, 1 = 8 waves x 1 row,
+                          // 2 = warp-specialised, 3 = weights in registers + 3-deep halo ring
+  int ablate = 0;         // profiling only (env PNPPDS_ABLATE); results are wrong when set
   bool den_ready = false;
   DevBuf head_w, head_b, body_w, body_b, tail_w, tail_b;
 
@@ -65,6 +69,7 @@ struct pnp_ctx {
 
   // scratch for single ops
   DevBuf scr_u32, scr_u16, scr_act[2], scr_part, scr_theta;
+  DevBuf trash;   // sink of masked-out conv epilogue stores
 
   // profiling
   bool prof = false;
@@ -202,33 +207,6 @@ size_t act_bytes(int B, int H, int W, int ch) {
   return ((size_t)B * (H + 2) * (W + 2) + (size_t)10 * (W + 2) + 64) * ch * sizeof(half_t);
 }
 
-void run_denoiser(pnp_ctx* ctx, const half_t* u16, const float* u32, float* xout, DevBuf (&act)[2], int B, int H,
-                  int W, hipStream_t st) {
-  if (!ctx->den_ready) fail(ctx, PNP_E_STATE, "denoiser not set (pnp_set_denoiser)");
-  const ConvShape s = make_conv_shape(B, H, W);
-  {
-    ProfScope ps(ctx, "conv_head", st);
-    launch_conv_head(u16, P<half_t>(act[0]), ctx->head_w.p, P<float>(ctx->head_b), s, ctx->den_act, ctx->num_cus,
-                     st);
-    check_launch(ctx, "conv_head");
-  }
-  int cur = 0;
-  const size_t wstride = kBodyWBytes;
-  for (int l = 0; l < ctx->den_depth - 2; ++l) {
-    ProfScope ps(ctx, "conv_body", st);
-    launch_conv_body(P<half_t>(act[cur]), P<half_t>(act[cur ^ 1]), (const char*)ctx->body_w.p + l * wstride,
-                     P<float>(ctx->body_b) + l * kWidth, s, ctx->den_act, ctx->num_cus, st);
-    check_launch(ctx, "conv_body");
-    cur ^= 1;
-  }
-  {
-    ProfScope ps(ctx, "conv_tail", st);
-    launch_conv_tail(P<half_t>(act[cur]), u32, xout, ctx->tail_w.p, P<float>(ctx->tail_b), s, ctx->den_C,
-                     ctx->den_residual, ctx->den_clamp, ctx->num_cus, st);
-    check_launch(ctx, "conv_tail");
-  }
-}
-
 // Padded activation images: the one-pixel border must be zero for the geometry in use.
 // Kernels never write the border, so a buffer is zeroed once per (B, H, W) it serves;
 // reusing it for another geometry (whose border lands on stale interior data) re-zeroes.
@@ -244,6 +222,55 @@ void ensure_padded(pnp_ctx* ctx, DevBuf& b, int B, int H, int W, int ch, hipStre
 
 void ensure_act(pnp_ctx* ctx, DevBuf (&act)[2], int B, int H, int W, hipStream_t st) {
   for (int i = 0; i < 2; ++i) ensure_padded(ctx, act[i], B, H, W, kWidth, st);
+}
+
+// Images per denoiser pass.  Auto: the whole batch, unless its two fp16 activation
+// images (2 x B x (H+2)(W+2) x 128 B) would exceed 8 GB.  (Passes sized to stay in the
+// 256 MB Infinity Cache measured no faster at 256x256: conv_body is not HBM-bound.)
+int denoise_chunk(pnp_ctx* ctx, int B, int H, int W) {
+  if (ctx->den_chunk > 0) return std::min(ctx->den_chunk, B);
+  const double per_img = 2.0 * (H + 2) * (W + 2) * kWidth * sizeof(half_t);
+  const int m = (int)std::floor(8e9 / per_img);
+  return std::max(1, std::min(m, B));
+}
+
+// Denoiser forward over B images: u16 (padded NHWC4) + u32 (NCHW, residual input) -> xout.
+void run_denoiser(pnp_ctx* ctx, const half_t* u16, const float* u32, float* xout, DevBuf (&act)[2], int B, int H,
+                  int W, hipStream_t st) {
+  if (!ctx->den_ready) fail(ctx, PNP_E_STATE, "denoiser not set (pnp_set_denoiser)");
+  const int m = denoise_chunk(ctx, B, H, W);
+  ensure_act(ctx, act, m, H, W, st);
+  const int C = ctx->den_C;
+  for (int b0 = 0; b0 < B; b0 += m) {
+    const int mb = std::min(m, B - b0);
+    ConvShape s = make_conv_shape(mb, H, W);
+    s.ablate = ctx->ablate;
+    ensure(ctx, ctx->trash, 4096);
+    s.trash = P<half_t>(ctx->trash);
+    const half_t* in4 = u16 + (size_t)b0 * (H + 2) * (W + 2) * 4;
+    const float* xin = u32 + (size_t)b0 * C * H * W;
+    float* xo = xout + (size_t)b0 * C * H * W;
+    {
+      ProfScope ps(ctx, "conv_head", st);
+      launch_conv_head(in4, P<half_t>(act[0]), ctx->head_w.p, P<float>(ctx->head_b), s, ctx->den_act,
+                       ctx->num_cus, st);
+      check_launch(ctx, "conv_head");
+    }
+    int cur = 0;
+    for (int l = 0; l < ctx->den_depth - 2; ++l) {
+      ProfScope ps(ctx, "conv_body", st);
+      launch_conv_body(P<half_t>(act[cur]), P<half_t>(act[cur ^ 1]), (const char*)ctx->body_w.p + l * kBodyWBytes,
+                       P<float>(ctx->body_b) + l * kWidth, s, ctx->den_act, ctx->num_cus, ctx->body_variant, st);
+      check_launch(ctx, "conv_body");
+      cur ^= 1;
+    }
+    {
+      ProfScope ps(ctx, "conv_tail", st);
+      launch_conv_tail(P<half_t>(act[cur]), xin, xo, ctx->tail_w.p, P<float>(ctx->tail_b), s, C, ctx->den_residual,
+                       ctx->den_clamp, ctx->num_cus, st);
+      check_launch(ctx, "conv_tail");
+    }
+  }
 }
 
 // -------- one solver iteration -------------------------------------------------------
@@ -319,7 +346,6 @@ void solver_setup(pnp_ctx* ctx, int method, const pnp_params* params, int B, int
   ensure(ctx, ctx->u32, fb);
   if (method == PNP_METHOD_B) ensure(ctx, ctx->w, fb);
   ensure_padded(ctx, ctx->u16, B, H, W, 4, ctx->stream);
-  ensure_act(ctx, ctx->act, B, H, W, ctx->stream);
   ensure(ctx, ctx->partials, (size_t)B * partial_tiles(H, W) * 4 * sizeof(double));
   ensure(ctx, ctx->metrics, (size_t)B * std::max(ctx->cap, 1) * 2 * sizeof(double));
   ensure(ctx, ctx->theta, (size_t)B * sizeof(float));
@@ -399,6 +425,7 @@ int pnp_create(int device, pnp_ctx** out) {
         fail(ctx, PNP_E_UNSUPPORTED, "device %d is %s; this library is built for gfx950 only", device,
              prop.gcnArchName);
       ctx->num_cus = prop.multiProcessorCount;
+      if (const char* ab = std::getenv("PNPPDS_ABLATE")) ctx->ablate = std::atoi(ab);   // profiling only
       HIPCHK(ctx, hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
       HIPCHK(ctx, conv_kernels_init());
     } catch (const PnpError&) {
@@ -418,7 +445,7 @@ int pnp_destroy(pnp_ctx* ctx) {
                     &ctx->taps_fwd, &ctx->taps_adj, &ctx->mask, &ctx->x[0], &ctx->x[1], &ctx->y, &ctx->s,
                     &ctx->w, &ctx->xobs, &ctx->xtrue, &ctx->u32, &ctx->u16, &ctx->act[0], &ctx->act[1],
                     &ctx->partials, &ctx->metrics, &ctx->theta, &ctx->scr_u32, &ctx->scr_u16,
-                    &ctx->scr_act[0], &ctx->scr_act[1], &ctx->scr_part, &ctx->scr_theta};
+                    &ctx->scr_act[0], &ctx->scr_act[1], &ctx->scr_part, &ctx->scr_theta, &ctx->trash};
   for (DevBuf* b : bufs) release(*b);
   for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -431,6 +458,23 @@ const char* pnp_last_error(const pnp_ctx* ctx) { return ctx ? ctx->err.c_str() :
 int pnp_synchronize(pnp_ctx* ctx) {
   if (!ctx) return PNP_E_ARG;
   return guarded(ctx, [&] { HIPCHK(ctx, hipStreamSynchronize(ctx->stream)); });
+}
+
+int pnp_set_tuning(pnp_ctx* ctx, int key, int value) {
+  if (!ctx) return PNP_E_ARG;
+  return guarded(ctx, [&] {
+    if (key == PNP_TUNE_DENOISE_CHUNK) {
+      if (value < 0) fail(ctx, PNP_E_ARG, "chunk must be >= 0");
+      ctx->den_chunk = value;
+      return;
+    }
+    if (key == PNP_TUNE_BODY_VARIANT) {
+      if (value < 0 || value > 3) fail(ctx, PNP_E_ARG, "body variant must be 0..3");
+      ctx->body_variant = value;
+      return;
+    }
+    fail(ctx, PNP_E_UNSUPPORTED, "tuning key %d", key);
+  });
 }
 
 int pnp_set_precision(pnp_ctx* ctx, int precision) {
@@ -738,7 +782,6 @@ int pnp_op_denoise(pnp_ctx* ctx, const float* x, float* out, int B, int C, int H
     hipStream_t st = pick_stream(ctx, stream);
     ensure(ctx, ctx->scr_u32, (size_t)B * C * H * W * sizeof(float));
     ensure_padded(ctx, ctx->scr_u16, B, H, W, 4, st);
-    ensure_act(ctx, ctx->scr_act, B, H, W, st);
     launch_pack_input(x, P<float>(ctx->scr_u32), P<half_t>(ctx->scr_u16), B, C, H, W, ctx->den_clamp, st);
     check_launch(ctx, "pack_input");
     run_denoiser(ctx, P<half_t>(ctx->scr_u16), P<float>(ctx->scr_u32), out, ctx->scr_act, B, H, W, st);

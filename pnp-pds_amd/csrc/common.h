@@ -41,11 +41,19 @@ __host__ __device__ inline int mfma32_row_to_channel(int i) {
   return 16 * ((i >> 2) & 1) + (i & 3) + 4 * (i >> 3);
 }
 
-// LDS image of a halo tile (hidden activations): pixel p occupies 128 B; its eight
-// 16-B channel chunks are XOR-swizzled by ((p >> 1) & 7) so that the 16-lane groups of
-// a ds_read_b128 over 16 consecutive pixels hit 16 distinct bank slots.
+// LDS image of a halo tile (hidden activations): pixel (row pr, column pc) of the
+// 10 x 34 halo occupies 128 B at p = pr*34 + pc; its eight 16-B channel chunks are
+// XOR-swizzled by ((pc >> 1) & 7) so that the 16-lane groups of a ds_read_b128 over 16
+// consecutive pixels of a row hit 16 distinct bank slots (34 is even, so p & 1 == pc & 1).
+// The swizzle depends on the column only: a wave's tap offsets differ by whole rows, so
+// the per-lane part of every fragment address is one of (3 columns x chunk) values and
+// the row steps fold into immediate offsets.
+__device__ __forceinline__ int halo_off(int pr, int pc, int chunk) {
+  return (pr * kHaloW + pc) * 128 + 16 * (chunk ^ ((pc >> 1) & 7));
+}
 __device__ __forceinline__ int halo_chunk_offset(int p, int chunk) {
-  return p * 128 + 16 * (chunk ^ ((p >> 1) & 7));
+  const int pr = p / kHaloW;
+  return halo_off(pr, p - pr * kHaloW, chunk);
 }
 
 __device__ __forceinline__ float act_fn(float v, int act) {

@@ -10,6 +10,8 @@ struct ConvShape {
   int B, H, W;       // image size (unpadded)
   int Hp, Wp;        // padded (H+2, W+2)
   int tiles_x, tiles_y, tiles;
+  int ablate;        // profiling only (env PNPPDS_ABLATE): bit0 skip prefetch DMA, bit1 skip stores
+  half_t* trash;     // >= 1 KiB scratch: destination of masked-out epilogue stores
 };
 ConvShape make_conv_shape(int B, int H, int W);
 hipError_t conv_kernels_init();
@@ -18,8 +20,9 @@ void pack_head_weights(const float* W, int C, uint16_t* out);
 void pack_tail_weights(const float* W, int C, uint16_t* out);
 void launch_conv_head(const half_t* in4, half_t* out, const void* w, const float* bias, const ConvShape& s,
                       int act, int num_cus, hipStream_t st);
+// variant 0: 4 waves x (2 rows x 64 ch); variant 1: 8 waves x (1 row x 64 ch)
 void launch_conv_body(const half_t* in, half_t* out, const void* w, const float* bias, const ConvShape& s,
-                      int act, int num_cus, hipStream_t st);
+                      int act, int num_cus, int variant, hipStream_t st);
 void launch_conv_tail(const half_t* in, const float* xin, float* xout, const void* w, const float* bias,
                       const ConvShape& s, int C, int residual_sign, int clamp_out, int num_cus, hipStream_t st);
 

@@ -20,6 +20,8 @@ ERRORS = {-1: "PNP_E_ARG", -2: "PNP_E_UNSUPPORTED", -3: "PNP_E_HIP", -4: "PNP_E_
 
 METHOD_A, METHOD_B, METHOD_C, METHOD_ADMM_B2 = 0, 1, 2, 3
 OP_ID, OP_BLUR, OP_RANDOM_SAMPLING = 0, 1, 2
+TUNE_DENOISE_CHUNK = 1
+TUNE_BODY_VARIANT = 2
 
 
 class PnpError(RuntimeError):
@@ -50,6 +52,7 @@ _SIGS = {
     "pnp_synchronize": ([_P], C.c_int),
     "pnp_set_denoiser": ([_P, C.c_int, C.c_int, C.c_int, _F, C.c_size_t, C.c_int, C.c_int, C.c_int], C.c_int),
     "pnp_set_precision": ([_P, C.c_int], C.c_int),
+    "pnp_set_tuning": ([_P, C.c_int, C.c_int], C.c_int),
     "pnp_set_operator": ([_P, C.c_int, _D, C.c_int, C.c_int, C.POINTER(C.c_uint8), C.c_int, C.c_int], C.c_int),
     "pnp_run": ([_P, C.c_int, C.POINTER(pnp_params), C.c_int, C.c_int, C.c_int, C.c_int, _F, _F, _F, C.c_int,
                  _F, _F, _D, _D, _D], C.c_int),
@@ -158,6 +161,14 @@ class Context:
                                               _fptr(flat), flat.size, weights.act, weights.residual,
                                               weights.clamp_io))
         self._denoiser_key = key
+
+    def set_denoise_chunk(self, images: int):
+        """Images per denoiser pass (0 = auto).  Performance only."""
+        self._check(self.lib.pnp_set_tuning(self.h, TUNE_DENOISE_CHUNK, int(images)))
+
+    def set_body_variant(self, variant: int):
+        """64->64 conv kernel variant (0: 4 waves/WG, 1: 8 waves/WG).  Performance only."""
+        self._check(self.lib.pnp_set_tuning(self.h, TUNE_BODY_VARIANT, int(variant)))
 
     def set_operator(self, kind: int, h=None, mask=None, key=None):
         if key is not None and key == self._operator_key:

@@ -56,6 +56,21 @@ def test_denoiser_ragged_batched(gpu_ctx, B, C, H, W):
     np.testing.assert_array_equal(one[0], out[B - 1])
 
 
+@pytest.mark.parametrize("B,C,H,W", [(3, 3, 50, 70), (2, 3, 256, 256)])
+def test_body_variants_bit_identical(gpu_ctx, B, C, H, W):
+    """All conv_body kernel variants run the same MFMA K-sequence per output: same bits."""
+    rng = np.random.default_rng(11)
+    w = DenoiserWeights.load_npz(os.path.join(WEIGHTS_DIR, "DnCNN_nobn_nch_3_nlev_0.01.npz"))
+    x = rng.uniform(0, 1, (B, C, H, W)).astype(np.float32)
+    outs = []
+    for v in (0, 1, 2, 3):
+        gpu_ctx.set_body_variant(v)
+        outs.append(run_denoise(gpu_ctx, w, x))
+    gpu_ctx.set_body_variant(3)
+    for v in (1, 2, 3):
+        np.testing.assert_array_equal(outs[0], outs[v])
+
+
 def test_denoiser_full_size_rgb(gpu_ctx):
     """256x256 RGB, real weights, batch 2 — the metric's image shape."""
     w = DenoiserWeights.load_npz(os.path.join(WEIGHTS_DIR, "DnCNN_nobn_nch_3_nlev_0.01.npz"))

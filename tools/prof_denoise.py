@@ -1,0 +1,42 @@
+"""Profiling driver: the denoiser alone (pnp_op_denoise) on a batch of RGB images.
+
+    rocprofv3 --kernel-trace --stats -- python3 tools/prof_denoise.py [--batch 64] [--reps 3]
+    rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES ... -- python3 tools/prof_denoise.py
+"""
+import argparse
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "pnp-pds_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--size", type=int, default=256)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--chunk", type=int, default=0)
+    ap.add_argument("--variant", type=int, default=3)
+    a = ap.parse_args()
+    import torch
+    from pnppds import _lib
+    from pnppds.weights import resolve_weights
+    ctx = _lib.Context(0)
+    ctx.set_denoiser(resolve_weights("DnCNN_nobn_nch_3_nlev_0.01", 3))
+    ctx.set_denoise_chunk(a.chunk)
+    ctx.set_body_variant(a.variant)
+    B, C, H, W = a.batch, 3, a.size, a.size
+    x = torch.rand((B, C, H, W), device="cuda:0")
+    y = torch.empty_like(x)
+    for _ in range(a.reps):
+        ctx.op_denoise(x.data_ptr(), y.data_ptr(), B, C, H, W)
+    ctx.synchronize()
+    torch.cuda.synchronize()
+    print("done", float(y.mean()))
+
+
+if __name__ == "__main__":
+    main()
