@@ -49,7 +49,9 @@ struct pnp_ctx {
   int den_C = 0, den_depth = 0, den_act = 0, den_residual = 1, den_clamp = 1;
   int den_chunk = 0;   // images per denoiser pass; 0 = auto
   int body_variant = 3;   // conv_body kernel: 0 = 4 waves x 2 rows, 1 = 8 waves x 1 row,
-                          // 2 = warp-specialised, 3 = weights in registers + 3-deep halo ring
+                          // 2 = warp-specialised, 3 = weights in registers + 3-deep halo ring,
+                          // 4 = one wave per SIMD holding the whole layer's weights,
+                          // 5 / 6 = variant 3 on a channel-plane halo, 2- / 3-deep fragment ring
   int ablate = 0;         // profiling only (env PNPPDS_ABLATE); results are wrong when set
   bool den_ready = false;
   DevBuf head_w, head_b, body_w, body_b, tail_w, tail_b;
@@ -469,7 +471,7 @@ int pnp_set_tuning(pnp_ctx* ctx, int key, int value) {
       return;
     }
     if (key == PNP_TUNE_BODY_VARIANT) {
-      if (value < 0 || value > 3) fail(ctx, PNP_E_ARG, "body variant must be 0..3");
+      if (value < 0 || value > 6) fail(ctx, PNP_E_ARG, "body variant must be 0..6");
       ctx->body_variant = value;
       return;
     }

@@ -14,6 +14,8 @@
 // rows 2w, 2w+1 (two 32-pixel N-tiles) x all 64 output channels (two 32-row M-tiles)
 // = 4 accumulators of 32x32.  Per K-step: 2 weight + 2 activation ds_read_b128 and
 // 4 MFMAs.
+#include <type_traits>
+
 #include "kernels.h"
 
 namespace pnp {
@@ -631,34 +633,74 @@ __device__ __forceinline__ int dma_count(int wave) {           // slots issued b
 // Halo DMA through a buffer descriptor: the tile base lives in SGPRs and the per-lane
 // byte offsets of this wave's slots are tile-invariant (computed once per launch), so an
 // issue costs one VGPR per slot instead of a 64-bit address.
-constexpr int kV3Slots = (kDmaSlots + 7) / 8;                 // 6 per wave (waves >= 3: 5)
-__device__ __forceinline__ void v3_dma_offsets(unsigned (&off)[kV3Slots], const ConvShape& s, int wave) {
-  const int lane = threadIdx.x & 63;
+template <int NW>
+struct RingDma {                                               // one wave's share of a halo DMA
+  static constexpr int kSlots = (kDmaSlots + NW - 1) / NW;     // NW=8: 6 (waves >= 3: 5); NW=4: 11 (wave 3: 10)
+  unsigned off[kSlots];
+  __device__ __forceinline__ void init(const ConvShape& s, int wave) {
+    const int lane = threadIdx.x & 63;
 #pragma unroll
-  for (int j = 0; j < kV3Slots; ++j) {
-    const int p = 8 * (8 * j + wave) + (lane >> 3);
-    const int pl = min(p, kHaloPix - 1);
-    const int pr = pl / kHaloW, pc = pl - pr * kHaloW;
-    const int c = (lane & 7) ^ ((pc >> 1) & 7);
-    off[j] = (unsigned)(((pr * s.Wp + pc) * kWidth + c * 8) * 2);
+    for (int j = 0; j < kSlots; ++j) {
+      const int p = 8 * (NW * j + wave) + (lane >> 3);
+      const int pl = min(p, kHaloPix - 1);
+      const int pr = pl / kHaloW, pc = pl - pr * kHaloW;
+      const int c = (lane & 7) ^ ((pc >> 1) & 7);
+      off[j] = (unsigned)(((pr * s.Wp + pc) * kWidth + c * 8) * 2);
+    }
   }
-}
-__device__ __forceinline__ void v3_dma(unsigned char* hl, const half_t* __restrict__ in, const ConvShape& s,
-                                       int t, const unsigned (&off)[kV3Slots], int wave) {
-  int b, ty0, tx0;
-  decode_tile(t, s, b, ty0, tx0);
-  const half_t* base = in + (((size_t)b * s.Hp + ty0) * s.Wp + tx0) * kWidth;
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, 0x7fffffff, 0x00020000);
-  const int lane = threadIdx.x & 63;
+  __device__ __forceinline__ void issue(unsigned char* hl, const half_t* __restrict__ in, const ConvShape& s, int t,
+                                        int wave) const {
+    int b, ty0, tx0;
+    decode_tile(t, s, b, ty0, tx0);
+    const half_t* base = in + (((size_t)b * s.Hp + ty0) * s.Wp + tx0) * kWidth;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, 0x7fffffff, 0x00020000);
+    const int lane = threadIdx.x & 63;
 #pragma unroll
-  for (int j = 0; j < kV3Slots; ++j) {
-    const int g = 8 * j + wave;
-    if (g < kDmaSlots - 1 || (g == kDmaSlots - 1 && lane < 32))   // slot 42: pixels 336..339
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(hl + g * 1024), 16,
-                                               off[j], 0, 0, 0);
+    for (int j = 0; j < kSlots; ++j) {
+      const int g = NW * j + wave;
+      if (g < kDmaSlots - 1 || (g == kDmaSlots - 1 && lane < 32))   // slot 42: pixels 336..339
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(hl + g * 1024), 16,
+                                                 off[j], 0, 0, 0);
+    }
   }
-}
+};
 
+// Channel-plane halo image (variant 3 PLANES): chunk c (channels 8c..8c+7) of halo pixel p
+// at c*5440 + 16p.  A 16-lane ds_read_b128 group over consecutive pixels is then 256
+// contiguous bytes (conflict-free without a swizzle) and every fragment address is one
+// per-lane base plus an immediate.  Wave w DMAs plane w: 6 instructions of 64 pixels
+// (the last one 20), each lane one 16-B chunk; the 8 waves read the 8 chunks of the same
+// 128-B pixel lines together, so the lines are fetched from L2 once.
+constexpr int kPlaneBytes = kHaloPix * 16;                     // 5440
+struct PlaneDma {
+  unsigned off[6];
+  __device__ __forceinline__ void init(const ConvShape& s, int wave) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      const int pl = min(64 * j + lane, kHaloPix - 1);
+      const int pr = pl / kHaloW, pc = pl - pr * kHaloW;
+      off[j] = (unsigned)(((pr * s.Wp + pc) * kWidth + wave * 8) * 2);
+    }
+  }
+  __device__ __forceinline__ void issue(unsigned char* hl, const half_t* __restrict__ in, const ConvShape& s, int t,
+                                        int wave) const {
+    int b, ty0, tx0;
+    decode_tile(t, s, b, ty0, tx0);
+    const half_t* base = in + (((size_t)b * s.Hp + ty0) * s.Wp + tx0) * kWidth;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, 0x7fffffff, 0x00020000);
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int j = 0; j < 6; ++j)
+      if (j < 5 || lane < kHaloPix - 320)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rs, (__attribute__((address_space(3))) void*)(hl + wave * kPlaneBytes + 1024 * j), 16, off[j], 0, 0, 0);
+  }
+};
+
+template <bool PLANES, int NFRAG>
 __global__ __launch_bounds__(512, 2) void conv_body_v3_kernel(const half_t* __restrict__ in,
                                                                half_t* __restrict__ out,
                                                                const uint4* __restrict__ wpk,
@@ -680,12 +722,12 @@ __global__ __launch_bounds__(512, 2) void conv_body_v3_kernel(const half_t* __re
                                                ((ks * 2 + m) * 64 + lane) * 16);
 
   auto buf = [&](int i) { return smem + i * kV3Halo; };
-  unsigned doff[kV3Slots];
-  v3_dma_offsets(doff, s, wave);
+  typename std::conditional<PLANES, PlaneDma, RingDma<8>>::type dma;
+  dma.init(s, wave);
   auto issue_dma = [&](int tt, int bi) {      // clamped: always the same instruction count
-    v3_dma(buf(bi), in, s, tt < s.tiles ? tt : s.tiles - 1, doff, wave);
+    dma.issue(buf(bi), in, s, tt < s.tiles ? tt : s.tiles - 1, wave);
   };
-  const int ndma = dma_count<8>(wave);
+  const int ndma = PLANES ? 6 : dma_count<8>(wave);
 
   int t = blockIdx.x;
   if (t < s.tiles) {
@@ -700,7 +742,7 @@ __global__ __launch_bounds__(512, 2) void conv_body_v3_kernel(const half_t* __re
   rs[0] = rs[1] = __builtin_amdgcn_make_buffer_rsrc(out, (short)0, 0, 0x00020000);   // first tile: dropped
   auto stage_read = [&](int j) {
     const int pix = 16 * j + (lane >> 2), c = lane & 3;
-    return *reinterpret_cast<const v4i_t*>(stg + pix * 64 + 16 * (c ^ ((pix >> 2) & 3)));
+    return *reinterpret_cast<const v4i_t*>(stg + pix * 64 + 16 * (c ^ ((pix >> 1) & 3)));
   };
   auto stage_store = [&](int j, const v4i_t& v) {
     const int pix = 16 * j + (lane >> 2), c = lane & 3;
@@ -713,25 +755,34 @@ __global__ __launch_bounds__(512, 2) void conv_body_v3_kernel(const half_t* __re
     const int nxt2 = cur >= 1 ? cur - 1 : 2;  // (cur + 2) % 3
     issue_dma(t + 2 * gridDim.x, nxt2);
     const unsigned char* hl = buf(cur);
+    // PLANES: one per-lane base, every tap / chunk offset an instruction immediate
+    const unsigned char* pb = hl + h * kPlaneBytes + (2 * rp * kHaloW + col) * 16;
     auto ldB = [&](int ks, int n) {
       const int tap = ks >> 2, sub = ks & 3;
+      if (PLANES)
+        return *reinterpret_cast<const half8_t*>(pb + 2 * sub * kPlaneBytes +
+                                                 ((n + tap / 3) * kHaloW + tap % 3) * 16);
       return *reinterpret_cast<const half8_t*>(
           hl + halo_off(2 * rp + n + tap / 3, col + tap % 3, 2 * sub + h));
     };
     floatx16 acc0 = {}, acc1 = {};
-    half8_t fb[2][2];
+    half8_t fb[NFRAG][2];
     v4i_t sv;
-    fb[0][0] = ldB(0, 0);
-    fb[0][1] = ldB(0, 1);
+#pragma unroll
+    for (int k = 0; k < NFRAG - 1; ++k) { fb[k][0] = ldB(k, 0); fb[k][1] = ldB(k, 1); }
 #pragma unroll
     for (int ks = 0; ks < kBodyKSteps; ++ks) {
-      const int r = ks & 1;
+      const int r = ks % NFRAG;
       if ((ks & 7) == 2) {                    // previous tile's stores, one per 8 K-steps
         __builtin_amdgcn_sched_barrier(0);
         sv = stage_read(ks >> 3);
         __builtin_amdgcn_sched_barrier(0);
       }
-      if (ks + 1 < kBodyKSteps) { fb[r ^ 1][0] = ldB(ks + 1, 0); fb[r ^ 1][1] = ldB(ks + 1, 1); }
+      if (ks + NFRAG - 1 < kBodyKSteps) {
+        const int kn = ks + NFRAG - 1;
+        fb[kn % NFRAG][0] = ldB(kn, 0);
+        fb[kn % NFRAG][1] = ldB(kn, 1);
+      }
       acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(wA[ks], fb[r][0], acc0, 0, 0, 0);
       acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(wA[ks], fb[r][1], acc1, 0, 0, 0);
       if ((ks & 7) == 4) {
@@ -739,10 +790,11 @@ __global__ __launch_bounds__(512, 2) void conv_body_v3_kernel(const half_t* __re
         stage_store(ks >> 3, sv);
         __builtin_amdgcn_sched_barrier(0);
       }
+      if (NFRAG > 2) __builtin_amdgcn_sched_barrier(0);   // keep the reads NFRAG-1 steps ahead
     }
     {                                         // bias + activation -> fp16 -> staging (wave-private)
       const float* bl = bias_l + 32 * m + 16 * h;
-      const int sw = (col >> 2) & 3;
+      const int sw = (col >> 1) & 3;    // ds_write_b128 banks repeat every 128 B: 8 lanes distinct
 #pragma unroll
       for (int n = 0; n < 2; ++n) {
         const int pix = n * 32 + col;
@@ -772,6 +824,139 @@ __global__ __launch_bounds__(512, 2) void conv_body_v3_kernel(const half_t* __re
   }
 #pragma unroll
   for (int j = 0; j < 4; ++j) stage_store(j, stage_read(j));
+}
+
+// ------------------------------------------------------------------------------------
+// Body layer, variant 4: one wave per SIMD holding the WHOLE layer's weights.
+// 4 waves; wave w computes all 64 output channels of tile rows 2w, 2w+1.  Its 72
+// A-fragments (288 registers) stay resident for the launch, so every activation fragment
+// read from LDS feeds 2 MFMAs (half the LDS reads of variant 3 per MFMA), and the fragment
+// ring runs two K-steps (8 MFMAs) ahead with counted lgkmcnt waits.  Staging is
+// wave-private (8 KiB: 64 whole 128-B pixels) and its 8 full-line stores per wave are
+// issued during the next tile's K-loop.  Same LDS map as variant 3 (3-deep halo ring).
+// ------------------------------------------------------------------------------------
+constexpr int kV4Stage = 3 * kV3Halo;
+constexpr int kV4Bias = kV4Stage + 4 * 8192;
+constexpr int kV4Lds = kV4Bias + 256;                           // 163584 B
+
+__global__ __launch_bounds__(256, 1) void conv_body_v4_kernel(const half_t* __restrict__ in,
+                                                               half_t* __restrict__ out,
+                                                               const uint4* __restrict__ wpk,
+                                                               const float* __restrict__ bias,
+                                                               ConvShape s, int act) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float* bias_l = reinterpret_cast<float*>(smem + kV4Bias);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h = lane >> 5, col = lane & 31;
+  unsigned char* stg = smem + kV4Stage + wave * 8192;
+  if (tid < kWidth) bias_l[tid] = bias[tid];
+
+  half8_t wA[kBodyKSteps][2];                 // the layer's weights, resident for the launch
+#pragma unroll
+  for (int ks = 0; ks < kBodyKSteps; ++ks)
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+      wA[ks][m] = *reinterpret_cast<const half8_t*>(reinterpret_cast<const unsigned char*>(wpk) +
+                                                    ((ks * 2 + m) * 64 + lane) * 16);
+
+  auto buf = [&](int i) { return smem + i * kV3Halo; };
+  RingDma<4> dma;
+  dma.init(s, wave);
+  auto issue_dma = [&](int tt, int bi) {      // clamped: always the same instruction count
+    dma.issue(buf(bi), in, s, tt < s.tiles ? tt : s.tiles - 1, wave);
+  };
+  const bool full = dma_count<4>(wave) == 11; // waves 0-2 issue 11 slots, wave 3 issues 10
+
+  int t = blockIdx.x;
+  if (t < s.tiles) {
+    issue_dma(t, 0);
+    issue_dma(t + gridDim.x, 1);
+    if (full) asm volatile("s_waitcnt vmcnt(11)" ::: "memory");     // tile t landed
+    else asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+  }
+  __syncthreads();
+  __amdgpu_buffer_rsrc_t rs[2];
+  rs[0] = rs[1] = __builtin_amdgcn_make_buffer_rsrc(out, (short)0, 0, 0x00020000);   // first tile: dropped
+  auto stage_read = [&](int j) {              // 8 whole pixels per instruction
+    const int pix = 8 * j + (lane >> 3), c = lane & 7;
+    return *reinterpret_cast<const v4i_t*>(stg + pix * 128 + 16 * (c ^ (pix & 7)));
+  };
+  auto stage_store = [&](int j, const v4i_t& v) {
+    const int pix = 8 * j + (lane >> 3), c = lane & 7;
+    __builtin_amdgcn_raw_buffer_store_b128(v, rs[j >> 2], (pix & 31) * 128 + 16 * c, 0, 0);
+  };
+  int cur = 0;
+  for (; t < s.tiles; t += gridDim.x) {
+    int b, ty0, tx0;
+    decode_tile(t, s, b, ty0, tx0);
+    const int nxt2 = cur >= 1 ? cur - 1 : 2;  // (cur + 2) % 3
+    issue_dma(t + 2 * gridDim.x, nxt2);
+    const unsigned char* hl = buf(cur);
+    auto ldB = [&](int ks, int n) {
+      const int tap = ks >> 2, sub = ks & 3;
+      return *reinterpret_cast<const half8_t*>(
+          hl + halo_off(2 * wave + n + tap / 3, col + tap % 3, 2 * sub + h));
+    };
+    floatx16 acc[2][2] = {};
+    half8_t fb[3][2];
+    v4i_t sv;
+    fb[0][0] = ldB(0, 0); fb[0][1] = ldB(0, 1);
+    fb[1][0] = ldB(1, 0); fb[1][1] = ldB(1, 1);
+#pragma unroll
+    for (int ks = 0; ks < kBodyKSteps; ++ks) {
+      const int r = ks % 3;
+      if ((ks & 3) == 1 && ks < 32) {         // previous tile's stores: 8, one per 4 K-steps
+        __builtin_amdgcn_sched_barrier(0);
+        sv = stage_read(ks >> 2);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (ks + 2 < kBodyKSteps) { fb[(ks + 2) % 3][0] = ldB(ks + 2, 0); fb[(ks + 2) % 3][1] = ldB(ks + 2, 1); }
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+          acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wA[ks][m], fb[r][n], acc[m][n], 0, 0, 0);
+      if ((ks & 3) == 3 && ks < 32) {
+        __builtin_amdgcn_sched_barrier(0);
+        stage_store(ks >> 2, sv);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    {                                         // bias + activation -> fp16 -> staging (wave-private)
+#pragma unroll
+      for (int n = 0; n < 2; ++n) {
+        const int pix = n * 32 + col;
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+          const float* bl = bias_l + 32 * m + 16 * h;
+          half8_t lo, hi;
+#pragma unroll
+          for (int r = 0; r < 8; ++r) {
+            lo[r] = (half_t)act_fn(acc[m][n][r] + bl[r], act);
+            hi[r] = (half_t)act_fn(acc[m][n][r + 8] + bl[r + 8], act);
+          }
+          const int q = 4 * m + 2 * h;
+          *reinterpret_cast<half8_t*>(stg + pix * 128 + 16 * (q ^ (pix & 7))) = lo;
+          *reinterpret_cast<half8_t*>(stg + pix * 128 + 16 * ((q + 1) ^ (pix & 7))) = hi;
+        }
+      }
+      const int ncols = min(kTileW, s.W - tx0);
+#pragma unroll
+      for (int n = 0; n < 2; ++n) {
+        const int y = ty0 + 2 * wave + n;
+        half_t* row = out + (((size_t)b * s.Hp + y + 1) * s.Wp + tx0 + 1) * kWidth;
+        rs[n] = __builtin_amdgcn_make_buffer_rsrc(row, (short)0, y < s.H ? ncols * 128 : 0, 0x00020000);
+      }
+    }
+    // tile t+1 landed: only the DMA of t+2 and this tile's 8 stores are younger
+    if (full) asm volatile("s_waitcnt vmcnt(19) lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(18) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    cur = cur == 2 ? 0 : cur + 1;
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) stage_store(j, stage_read(j));
 }
 
 // ------------------------------------------------------------------------------------
@@ -1000,7 +1185,12 @@ hipError_t conv_kernels_init() {
   if (e != hipSuccess) return e;
   e = hipFuncSetAttribute((const void*)conv_body_ws_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, kBodyLds);
   if (e != hipSuccess) return e;
-  e = hipFuncSetAttribute((const void*)conv_body_v3_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, kV3Lds);
+  for (const void* k : {(const void*)conv_body_v3_kernel<false, 2>, (const void*)conv_body_v3_kernel<true, 2>,
+                        (const void*)conv_body_v3_kernel<true, 3>}) {
+    e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kV3Lds);
+    if (e != hipSuccess) return e;
+  }
+  e = hipFuncSetAttribute((const void*)conv_body_v4_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, kV4Lds);
   if (e != hipSuccess) return e;
   return hipFuncSetAttribute((const void*)conv_tail_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                              kTailLds);
@@ -1015,8 +1205,17 @@ void launch_conv_head(const half_t* in4, half_t* out, const void* w, const float
 void launch_conv_body(const half_t* in, half_t* out, const void* w, const float* bias, const ConvShape& s,
                       int act, int num_cus, int variant, hipStream_t st) {
   const int grid = s.tiles < num_cus ? s.tiles : num_cus;
-  if (variant == 3)
-    hipLaunchKernelGGL(conv_body_v3_kernel, dim3(grid), dim3(512), kV3Lds, st, in, out, (const uint4*)w, bias,
+  if (variant == 4)
+    hipLaunchKernelGGL(conv_body_v4_kernel, dim3(grid), dim3(256), kV4Lds, st, in, out, (const uint4*)w, bias,
+                       s, act);
+  else if (variant == 5)
+    hipLaunchKernelGGL((conv_body_v3_kernel<true, 2>), dim3(grid), dim3(512), kV3Lds, st, in, out, (const uint4*)w,
+                       bias, s, act);
+  else if (variant == 6)
+    hipLaunchKernelGGL((conv_body_v3_kernel<true, 3>), dim3(grid), dim3(512), kV3Lds, st, in, out, (const uint4*)w,
+                       bias, s, act);
+  else if (variant == 3)
+    hipLaunchKernelGGL((conv_body_v3_kernel<false, 2>), dim3(grid), dim3(512), kV3Lds, st, in, out, (const uint4*)w, bias,
                        s, act);
   else if (variant == 2)
     hipLaunchKernelGGL(conv_body_ws_kernel, dim3(grid), dim3(512), kBodyLds, st, in, out, (const uint4*)w, bias,
