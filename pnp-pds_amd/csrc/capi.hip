@@ -68,6 +68,7 @@ struct pnp_ctx {
   pnp_params prm{};
   int cur = 0;
   DevBuf x[2], y, s, w, xobs, xtrue, u32, u16, act[2], partials, metrics, theta;
+  DevBuf z, p, t;   // comparisonB-2 only
 
   // scratch for single ops
   DevBuf scr_u32, scr_u16, scr_act[2], scr_part, scr_theta;
@@ -324,10 +325,75 @@ void solver_iteration(pnp_ctx* ctx) {
   ctx->it += 1;
 }
 
+// comparisonB-2 (iteration.py:127-132): ADMM with the denoiser as the x-step prox.
+//   x = 1; m1 x { x <- D(x - Phi^T(Phi x + s - z + y) / g1) }        (admm.py:30-36)
+//   s = 1; m2 x { s <- P_l1(s - (Phi x + s - z + y) / g1) }          (admm.py:38-44, r = 1)
+//   z = P_l2(Phi x + s + y; x_obs)  (r = 1);  y <- y + Phi x + s - z
+void solver_iteration_admm(pnp_ctx* ctx) {
+  hipStream_t st = ctx->stream;
+  const pnp_params& p = ctx->prm;
+  const int B = ctx->B, C = ctx->C, H = ctx->H, W = ctx->W;
+  const size_t n = (size_t)C * H * W, N = (size_t)B * n;
+  const OpDesc od = op_desc(ctx);
+  float* xo = P<float>(ctx->x[ctx->cur]);
+  float* xn = P<float>(ctx->x[ctx->cur ^ 1]);
+  float *y = P<float>(ctx->y), *sv = P<float>(ctx->s), *z = P<float>(ctx->z), *w = P<float>(ctx->w);
+  float *pp = P<float>(ctx->p), *t = P<float>(ctx->t);
+  const double g = 1.0 / p.gamma1;
+  {
+    ProfScope ps(ctx, "admm_x_init", st);
+    launch_lincomb(w, 0.0, sv, 1.0, y, 1.0, z, -1.0, nullptr, 0.0, N, st);     // s - z + y (fixed in the x-step)
+    launch_lincomb(xn, 1.0, nullptr, 0.0, nullptr, 0.0, nullptr, 0.0, nullptr, 0.0, N, st);   // admm.py:32
+    check_launch(ctx, "admm_x_init");
+  }
+  for (int i = 0; i < p.m1; ++i) {
+    {
+      ProfScope ps(ctx, "admm_x_grad", st);
+      launch_op_phi(od.kind, 0, xn, t, od, B * C, H, W, st, w);               // Phi x + s - z + y
+      launch_k1(od.kind, xn, t, nullptr, P<float>(ctx->u32), P<half_t>(ctx->u16), nullptr, od, B, C, H, W,
+                (float)g, ctx->den_clamp, 0, st);                              // x - Phi^T(.) / g1 -> denoiser input
+      check_launch(ctx, "admm_x_grad");
+    }
+    run_denoiser(ctx, P<half_t>(ctx->u16), P<float>(ctx->u32), xn, ctx->act, B, H, W, st);   // admm.py:35
+  }
+  {
+    ProfScope ps(ctx, "admm_s_step", st);
+    launch_op_phi(od.kind, 0, xn, pp, od, B * C, H, W, st);                   // Phi x (fixed from here on)
+    launch_lincomb(sv, 1.0, nullptr, 0.0, nullptr, 0.0, nullptr, 0.0, nullptr, 0.0, N, st);   // admm.py:40
+    const double eta = p.alpha_s * (double)n * p.sp_nl * 0.5;               // operators.py:96, r = 1
+    for (int i = 0; i < p.m2; ++i) {
+      launch_lincomb(w, 0.0, sv, 1.0 - g, pp, -g, y, -g, z, g, N, st);       // s - (Phi x + s - z + y) / g1
+      launch_l1_select(w, P<float>(ctx->theta), B, n, eta, st);
+      launch_shrink(w, sv, P<float>(ctx->theta), B, n, st);
+    }
+    check_launch(ctx, "admm_s_step");
+  }
+  {
+    ProfScope ps(ctx, "admm_zy", st);
+    const double eps = std::sqrt((double)n * (1.0 - p.sp_nl)) * p.alpha_n * p.gaussian_nl;   // r = 1
+    launch_lincomb(t, 0.0, pp, 1.0, sv, 1.0, y, 1.0, nullptr, 0.0, N, st);
+    launch_l2_proj(t, P<float>(ctx->xobs), z, P<double>(ctx->partials), B, n, eps, st);
+    launch_lincomb(y, 0.0, y, 1.0, pp, 1.0, sv, 1.0, z, -1.0, N, st);      // iteration.py:132
+    if (p.record_metrics && ctx->it < ctx->cap)
+      launch_metrics(xn, xo, ctx->has_true ? P<float>(ctx->xtrue) : nullptr, P<double>(ctx->partials),
+                     P<double>(ctx->metrics), B, n, ctx->it, ctx->cap, st);
+    check_launch(ctx, "admm_zy");
+  }
+  ctx->cur ^= 1;
+  ctx->it += 1;
+}
+
+void solver_step(pnp_ctx* ctx) {
+  if (ctx->method == PNP_METHOD_ADMM_B2) solver_iteration_admm(ctx);
+  else solver_iteration(ctx);
+}
+
 void solver_setup(pnp_ctx* ctx, int method, const pnp_params* params, int B, int C, int H, int W, int cap) {
   if (!params) fail(ctx, PNP_E_ARG, "params is NULL");
-  if (method < PNP_METHOD_A || method > PNP_METHOD_C)
+  if (method < PNP_METHOD_A || method > PNP_METHOD_ADMM_B2)
     fail(ctx, PNP_E_UNSUPPORTED, "method %d not supported on device", method);
+  if (method == PNP_METHOD_ADMM_B2 && (params->m1 < 0 || params->m2 < 0 || params->gamma1 == 0.0))
+    fail(ctx, PNP_E_ARG, "comparisonB-2 needs m1, m2 >= 0 and gamma1 != 0");
   if (B < 1 || C < 1 || C > kMaxC || H < 1 || W < 1) fail(ctx, PNP_E_ARG, "bad shape B=%d C=%d H=%d W=%d", B, C, H, W);
   if (!ctx->den_ready) fail(ctx, PNP_E_STATE, "denoiser not set");
   if (ctx->den_C != C) fail(ctx, PNP_E_ARG, "denoiser has %d channels, images have %d", ctx->den_C, C);
@@ -346,9 +412,15 @@ void solver_setup(pnp_ctx* ctx, int method, const pnp_params* params, int B, int
   ensure(ctx, ctx->xobs, fb);
   ensure(ctx, ctx->xtrue, fb);
   ensure(ctx, ctx->u32, fb);
-  if (method == PNP_METHOD_B) ensure(ctx, ctx->w, fb);
+  if (method == PNP_METHOD_B || method == PNP_METHOD_ADMM_B2) ensure(ctx, ctx->w, fb);
+  if (method == PNP_METHOD_ADMM_B2) {
+    ensure(ctx, ctx->z, fb);
+    ensure(ctx, ctx->p, fb);
+    ensure(ctx, ctx->t, fb);
+  }
   ensure_padded(ctx, ctx->u16, B, H, W, 4, ctx->stream);
-  ensure(ctx, ctx->partials, (size_t)B * partial_tiles(H, W) * 4 * sizeof(double));
+  ensure(ctx, ctx->partials,
+         (size_t)B * std::max(partial_tiles(H, W), chunk_count((size_t)C * H * W)) * 4 * sizeof(double));
   ensure(ctx, ctx->metrics, (size_t)B * std::max(ctx->cap, 1) * 2 * sizeof(double));
   ensure(ctx, ctx->theta, (size_t)B * sizeof(float));
   ctx->loaded = false;
@@ -359,6 +431,7 @@ void solver_reset_state(pnp_ctx* ctx) {
   const size_t fb = (size_t)ctx->B * ctx->C * ctx->H * ctx->W * sizeof(float);
   HIPCHK(ctx, hipMemsetAsync(ctx->y.p, 0, fb, ctx->stream));          // iteration.py:24
   HIPCHK(ctx, hipMemsetAsync(ctx->s.p, 0, fb, ctx->stream));          // iteration.py:27
+  if (ctx->method == PNP_METHOD_ADMM_B2) HIPCHK(ctx, hipMemsetAsync(ctx->z.p, 0, fb, ctx->stream));
   if (ctx->cap) {
     std::vector<double> nanbuf((size_t)ctx->B * ctx->cap * 2, std::nan(""));
     HIPCHK(ctx, hipMemcpyAsync(ctx->metrics.p, nanbuf.data(), nanbuf.size() * sizeof(double), hipMemcpyHostToDevice,
@@ -629,7 +702,7 @@ int pnp_solver_iterate(pnp_ctx* ctx, int n_iter) {
       ctx->prof_log.clear();
       ctx->ev_used = 0;
     }
-    for (int i = 0; i < n_iter; ++i) solver_iteration(ctx);
+    for (int i = 0; i < n_iter; ++i) solver_step(ctx);
   });
 }
 
@@ -670,7 +743,7 @@ int pnp_run(pnp_ctx* ctx, int method, const pnp_params* params, int B, int C, in
     solver_reset_state(ctx);
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     const auto t0 = std::chrono::steady_clock::now();
-    for (int i = 0; i < max_iter; ++i) solver_iteration(ctx);
+    for (int i = 0; i < max_iter; ++i) solver_step(ctx);
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     if (avg_time_s) *avg_time_s = max_iter ? dt / max_iter : 0.0;

@@ -52,14 +52,21 @@ void launch_k3(int method, float* y, const float* xobs, const double* partials, 
 int partial_tiles(int H, int W);
 int chunk_count(size_t n);
 void launch_l1_select(const float* v, float* theta, int B, size_t n, double eta, hipStream_t st);
+// out = Phi(x) (or Phi^T x) [+ add]
 void launch_op_phi(int kind, int adj, const float* x, float* out, const OpDesc& op, int BC, int H, int W,
-                   hipStream_t st);
+                   hipStream_t st, const float* add = nullptr);
 void launch_l2_proj(const float* x, const float* x0, float* out, double* partials, int B, size_t n, double eps,
                     hipStream_t st);
 void launch_sqdiff(const float* a, const float* c, double* partials, int B, size_t n, hipStream_t st);
 void launch_shrink(const float* v, float* out, const float* theta, int B, size_t n, hipStream_t st);
 void launch_gkl(const float* x, const float* x0, float* out, size_t count, double gamma, double alpha,
                 hipStream_t st);
+// comparisonB-2: out = k + ca*a + cb*b + cc*c + cd*d (null inputs skipped), fp64 arithmetic
+void launch_lincomb(float* out, double k, const float* a, double ca, const float* b, double cb, const float* c,
+                    double cc, const float* d, double cd, size_t count, hipStream_t st);
+// c_n / PSNR of xn against xo / xt into metrics[b][it] (partials: B * chunk_count(n) * 4 doubles)
+void launch_metrics(const float* xn, const float* xo, const float* xt, double* partials, double* metrics, int B,
+                    size_t n, int it, int cap, hipStream_t st);
 void launch_pack_input(const float* x, float* u32, half_t* u16, int B, int C, int H, int W, int clamp_in,
                        hipStream_t st);
 

@@ -383,7 +383,8 @@ __global__ __launch_bounds__(kSelThreads) void l1_select_kernel(const float* __r
 // =====================================================================================
 template <int KIND, int ADJ>
 __global__ __launch_bounds__(256) void op_phi_kernel(const float* __restrict__ x, float* __restrict__ out,
-                                                      OpDesc op, int H, int W, int tiles_x) {
+                                                      const float* __restrict__ add, OpDesc op, int H, int W,
+                                                      int tiles_x) {
   __shared__ float lds[kLdsW * kLdsW];
   const int tile = blockIdx.x, bc = blockIdx.y;
   const int ty = tile / tiles_x;
@@ -407,6 +408,7 @@ __global__ __launch_bounds__(256) void op_phi_kernel(const float* __restrict__ x
     if (KIND == OP_BLUR) v = acc[r];
     else if (KIND == OP_MASK) v = xp[k] * (float)op.mask[k];
     else v = xp[k];
+    if (add) v += add[(size_t)bc * plane + k];
     out[(size_t)bc * plane + k] = v;
   }
 }
@@ -479,6 +481,53 @@ __global__ __launch_bounds__(256) void pack_input_kernel(const float* __restrict
       h4[c] = (half_t)u;
     }
     *reinterpret_cast<half4_t*>(u16 + ((b * (H + 2) + i + 1) * (W + 2) + j + 1) * 4) = h4;
+  }
+}
+
+// =====================================================================================
+// comparisonB-2 (ADMM with denoiser, iteration.py:127-132, admm.py:30-44): elementwise
+// linear combinations and the per-image c_n / PSNR partial sums.
+// =====================================================================================
+struct LinComb {
+  double k, c[4];
+  const float* in[4];
+};
+// out = k + sum_q c[q] * in[q]   (null inputs skipped), evaluated in fp64
+__global__ __launch_bounds__(256) void lincomb_kernel(float* __restrict__ out, LinComb lc, size_t count) {
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < count; i += (size_t)gridDim.x * 256) {
+    double v = lc.k;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (lc.in[q]) v += lc.c[q] * (double)lc.in[q][i];
+    out[i] = (float)v;
+  }
+}
+
+// partials [B][chunks][4] = {0, sum (xn - xo)^2, sum xo^2, sum (xt - xn)^2}, grid (chunks, B)
+__global__ __launch_bounds__(256) void metric_partials_kernel(const float* __restrict__ xn,
+                                                               const float* __restrict__ xo,
+                                                               const float* __restrict__ xt,
+                                                               double* __restrict__ partials, size_t n, int chunks) {
+  __shared__ double red[4];
+  const int b = blockIdx.y;
+  const size_t beg = (size_t)blockIdx.x * 2048;
+  double e2 = 0, n2 = 0, t2 = 0;
+  for (size_t k = beg + threadIdx.x; k < beg + 2048 && k < n; k += 256) {
+    const size_t i = (size_t)b * n + k;
+    const double a = xn[i], o = xo[i];
+    e2 += (a - o) * (a - o);
+    n2 += o * o;
+    if (xt) {
+      const double q = (double)xt[i] - a;
+      t2 += q * q;
+    }
+  }
+  e2 = block_sum(e2, red);
+  n2 = block_sum(n2, red);
+  t2 = block_sum(t2, red);
+  if (threadIdx.x == 0) {
+    double* p = partials + ((size_t)b * chunks + blockIdx.x) * 4;
+    p[0] = 0; p[1] = e2; p[2] = n2; p[3] = t2;
   }
 }
 
@@ -560,17 +609,19 @@ void launch_l1_select(const float* v, float* theta, int B, size_t n, double eta,
 }
 
 void launch_op_phi(int kind, int adj, const float* x, float* out, const OpDesc& op, int BC, int H, int W,
-                   hipStream_t st) {
+                   hipStream_t st, const float* add) {
   const TileGrid g = tile_grid(H, W);
   dim3 grid(g.tiles, BC);
+#define PHI_ARGS x, out, add, op, H, W, g.tiles_x
   if (kind == OP_BLUR) {
-    if (adj) hipLaunchKernelGGL((op_phi_kernel<OP_BLUR, 1>), grid, dim3(256), 0, st, x, out, op, H, W, g.tiles_x);
-    else hipLaunchKernelGGL((op_phi_kernel<OP_BLUR, 0>), grid, dim3(256), 0, st, x, out, op, H, W, g.tiles_x);
+    if (adj) hipLaunchKernelGGL((op_phi_kernel<OP_BLUR, 1>), grid, dim3(256), 0, st, PHI_ARGS);
+    else hipLaunchKernelGGL((op_phi_kernel<OP_BLUR, 0>), grid, dim3(256), 0, st, PHI_ARGS);
   } else if (kind == OP_MASK) {
-    hipLaunchKernelGGL((op_phi_kernel<OP_MASK, 0>), grid, dim3(256), 0, st, x, out, op, H, W, g.tiles_x);
+    hipLaunchKernelGGL((op_phi_kernel<OP_MASK, 0>), grid, dim3(256), 0, st, PHI_ARGS);
   } else {
-    hipLaunchKernelGGL((op_phi_kernel<OP_ID, 0>), grid, dim3(256), 0, st, x, out, op, H, W, g.tiles_x);
+    hipLaunchKernelGGL((op_phi_kernel<OP_ID, 0>), grid, dim3(256), 0, st, PHI_ARGS);
   }
+#undef PHI_ARGS
 }
 
 int chunk_count(size_t n) { return (int)((n + 2047) / 2048); }
@@ -605,6 +656,29 @@ void launch_pack_input(const float* x, float* u32, half_t* u16, int B, int C, in
   if (blocks > 16384) blocks = 16384;
   hipLaunchKernelGGL(pack_input_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, u32, u16, B, C, H, W,
                      clamp_in);
+}
+
+}  // namespace pnp
+
+namespace pnp {
+
+void launch_lincomb(float* out, double k, const float* a, double ca, const float* b, double cb, const float* c,
+                    double cc, const float* d, double cd, size_t count, hipStream_t st) {
+  LinComb lc;
+  lc.k = k;
+  lc.c[0] = ca; lc.c[1] = cb; lc.c[2] = cc; lc.c[3] = cd;
+  lc.in[0] = a; lc.in[1] = b; lc.in[2] = c; lc.in[3] = d;
+  size_t blocks = (count + 255) / 256;
+  if (blocks > 16384) blocks = 16384;
+  if (blocks == 0) blocks = 1;
+  hipLaunchKernelGGL(lincomb_kernel, dim3((unsigned)blocks), dim3(256), 0, st, out, lc, count);
+}
+
+void launch_metrics(const float* xn, const float* xo, const float* xt, double* partials, double* metrics, int B,
+                    size_t n, int it, int cap, hipStream_t st) {
+  const int chunks = chunk_count(n);
+  hipLaunchKernelGGL(metric_partials_kernel, dim3(chunks, B), dim3(256), 0, st, xn, xo, xt, partials, n, chunks);
+  hipLaunchKernelGGL(k3_metrics, dim3(B), dim3(256), 0, st, partials, chunks, n, metrics, it, cap, xt ? 1 : 0);
 }
 
 }  // namespace pnp

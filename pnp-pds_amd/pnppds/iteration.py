@@ -33,6 +33,7 @@ METHODS = {
     "A-Proposed": _lib.METHOD_A, "ours-A": _lib.METHOD_A,
     "B-Proposed": _lib.METHOD_B, "ours-B": _lib.METHOD_B,
     "C-Proposed": _lib.METHOD_C, "ours-C": _lib.METHOD_C,
+    "comparisonB-2": _lib.METHOD_ADMM_B2,
 }
 
 
