@@ -132,6 +132,7 @@ def main():
     from pnppds import _lib
     from pnppds.iteration import make_params
     from pnppds.operators import load_blur_kernel
+    from pnppds.shard import max_over_ranks
     from pnppds.weights import resolve_weights
 
     B, C, H, W = args.batch, 3, args.size, args.size
@@ -203,9 +204,7 @@ def main():
     t_el = time.perf_counter() - t_start
     if world > 1:
         dist.barrier()
-        tt = torch.tensor([t_el], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        t_el = float(tt.item())
+        t_el = max_over_ranks(t_el, device=f"cuda:{local}")   # job time = slowest rank
     prof = ctx.profile_read() if args.profile else {}
     x_out, s_out, c_hist, psnr_hist = ctx.solver_fetch()
 
