@@ -9,8 +9,10 @@ synthetic RGB 256x256 images per GPU, inputs resident in HBM.  Images are indepe
 ranks process disjoint shards with no data-path collective (weak scaling: 256 images per
 GPU).  ``value`` = image-iterations/s over the whole job (sum over ranks / max rank time).
 
-Also reported: ``roofline`` of the dominant kernel (conv_body, MFMA-bound: algorithmic
-FLOPs / HIP-event duration vs the fp16 dense MFMA peak), HBM fractions of the fused
+Also reported: ``roofline`` of the dominant kernel (conv_body: 288 FLOP/B, below the
+2500/8 = 312 FLOP/B ridge, so HBM-bound: algorithmic bytes / HIP-event duration vs 8 TB/s,
+with the MFMA fraction alongside and ``traffic`` = PMC-measured bytes per launch from this
+round's committed profile), HBM fractions of the fused
 prox/operator kernels, PSNR delta vs the CPU oracle on image 0, and ``cpu_baseline``: the
 oracle restatement of the reference's test_iter timed on this host (rank 0, N=1 only).
 """
@@ -69,6 +71,27 @@ def images_per_launch(B, H, W, chunk):
 def conv_flops_per_launch(m, H, W):
     """Algorithmic FLOPs of one 64->64 3x3 conv launch over m images."""
     return 2.0 * 64 * 64 * 9 * m * H * W
+
+
+def conv_bytes_per_launch(m, H, W):
+    """Algorithmic HBM bytes of one 64->64 conv launch over m images: read and write the
+    fp16 64-channel activations once (the zero border, halo re-reads and weights are not
+    algorithmic)."""
+    return 2 * m * H * W * 64 * 2
+
+
+TRAFFIC_JSON = "profiles/r01/bench/traffic.json"
+
+
+def measured_traffic(kernel, B):
+    """HBM bytes per launch from this round's committed PMC passes of this bench command
+    (tools/profile_bench.sh + tools/traffic_from_pmc.py), or None."""
+    try:
+        with open(os.path.join(REPO, TRAFFIC_JSON)) as f:
+            t = json.load(f)
+        return t["kernels"][kernel]["bytes"] if B == 256 else None
+    except (OSError, KeyError, ValueError):
+        return None
 
 
 def prox_bytes(B, C, H, W):
@@ -226,12 +249,18 @@ def main():
             kt = {k: round(v[0], 4) for k, v in prof.items()}
             line["kernel_ms"] = kt
             body_ms = prof["conv_body"][0]
-            fl = conv_flops_per_launch(images_per_launch(B, H, W, args.chunk), H, W)
-            ach = fl / (body_ms * 1e-3) / 1e12
-            line["roofline"] = {"kernel": "conv_body (64->64 3x3 implicit GEMM, fp16 MFMA)", "bound": "mfma",
-                                "achieved": round(ach, 1), "peak": FP16_PEAK_TFLOPS, "unit": "TFLOP/s",
-                                "frac": round(ach / FP16_PEAK_TFLOPS, 4), "traffic": None,
-                                "flops_per_launch": fl}
+            m = images_per_launch(B, H, W, args.chunk)
+            fl = conv_flops_per_launch(m, H, W)
+            by = conv_bytes_per_launch(m, H, W)
+            gbs = by / (body_ms * 1e-3) / 1e9
+            tfl = fl / (body_ms * 1e-3) / 1e12
+            # arithmetic intensity 288 FLOP/B < ridge 2500/8 = 312.5: the HBM roof binds
+            line["roofline"] = {"kernel": "conv_body (64->64 3x3 implicit GEMM, fp16 MFMA)", "bound": "hbm",
+                                "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": measured_traffic("conv_body", B),
+                                "bytes_per_launch": by, "flops_per_launch": fl,
+                                "mfma_tflops": round(tfl, 1), "mfma_frac": round(tfl / FP16_PEAK_TFLOPS, 4),
+                                "traffic_source": TRAFFIC_JSON}
             pb = prox_bytes(B, C, H, W)
             line["prox_hbm"] = {k: {"GB/s": round(pb[k] / (prof[k][0] * 1e-3) / 1e9, 1),
                                     "frac": round(pb[k] / (prof[k][0] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}

@@ -1,0 +1,60 @@
+"""Per-launch HBM traffic of the bench's kernels from rocprofv3 PMC passes (profiling only).
+
+    python tools/traffic_from_pmc.py profiles/r01/bench/pmc_fetch.csv profiles/r01/bench/pmc_write.csv \
+        --out profiles/r01/bench/traffic.json
+
+FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  On gfx950 FETCH_SIZE reports half the
+bytes of wide (16 B/lane) coalesced streaming reads (MI355X_MICROARCH.md, HBM section), the
+access pattern of the conv kernels' LDS-DMA halo loads, so it is doubled for them; the
+prox/operator kernels load 4 B per lane, for which FETCH_SIZE already matches their byte
+count (k2_dual: 1107 MB raw vs 1007 MB algorithmic + halo), so they are taken as reported.
+WRITE_SIZE is exact for 16-B-per-lane stores.  bench.py puts the conv_body entry in its
+roofline ``traffic`` field.
+"""
+import argparse
+import collections
+import csv
+import json
+import re
+
+WIDE_READ = ("conv_body", "conv_head", "conv_tail")
+
+
+def short(name):
+    n = re.sub(r"\(.*", "", name)
+    for k in ("conv_body", "conv_head", "conv_tail", "k1_primal_pre", "k2_dual", "k3_l2_dual", "l1_select"):
+        if k in n:
+            return k
+    return None
+
+
+def per_dispatch(path, counter):
+    vals = collections.defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        k = short(r["Kernel_Name"])
+        if k and r["Counter_Name"] == counter:
+            vals[k].append(float(r["Counter_Value"]) * 1024.0)
+    return {k: sum(v) / len(v) for k, v in vals.items()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("fetch_csv")
+    ap.add_argument("write_csv")
+    ap.add_argument("--out", required=True)
+    a = ap.parse_args()
+    rd = per_dispatch(a.fetch_csv, "FETCH_SIZE")
+    wr = per_dispatch(a.write_csv, "WRITE_SIZE")
+    out = {"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes ({a.fetch_csv}, {a.write_csv})",
+           "kernels": {}}
+    for k in sorted(set(rd) | set(wr)):
+        r = rd.get(k, 0.0) * (2.0 if k in WIDE_READ else 1.0)
+        out["kernels"][k] = {"read_bytes": round(r), "write_bytes": round(wr.get(k, 0.0)),
+                             "bytes": round(r + wr.get(k, 0.0)),
+                             "fetch_correction": 2.0 if k in WIDE_READ else 1.0}
+    json.dump(out, open(a.out, "w"), indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
