@@ -633,7 +633,10 @@ __device__ __forceinline__ int dma_count(int wave) {           // slots issued b
 // Halo DMA through a buffer descriptor: the tile base lives in SGPRs and the per-lane
 // byte offsets of this wave's slots are tile-invariant (computed once per launch), so an
 // issue costs one VGPR per slot instead of a 64-bit address.
-template <int NW>
+// UNIFORM: every wave issues kSlots (the extra slots re-read pixel 339 into padding past
+// the halo), so the issue has no control flow and the compiler's own vmcnt accounting for
+// loads issued before it stays exact; the buffer must then hold NW * kSlots KiB.
+template <int NW, bool UNIFORM = false>
 struct RingDma {                                               // one wave's share of a halo DMA
   static constexpr int kSlots = (kDmaSlots + NW - 1) / NW;     // NW=8: 6 (waves >= 3: 5); NW=4: 11 (wave 3: 10)
   unsigned off[kSlots];
@@ -659,7 +662,7 @@ struct RingDma {                                               // one wave's sha
 #pragma unroll
     for (int j = 0; j < kSlots; ++j) {
       const int g = NW * j + wave;
-      if (g < kDmaSlots - 1 || (g == kDmaSlots - 1 && lane < 32))   // slot 42: pixels 336..339
+      if (UNIFORM || g < kDmaSlots - 1 || (g == kDmaSlots - 1 && lane < 32))   // slot 42: pixels 336..339
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(hl + g * 1024), 16,
                                                  off[j], 0, 0, 0);
     }
@@ -1019,89 +1022,123 @@ __global__ __launch_bounds__(256) void conv_head_kernel(const half_t* __restrict
 // ------------------------------------------------------------------------------------
 // Tail layer 64 -> C (basic_models.py:18,35-36) + residual + clamp (denoiser.py:42),
 // writing the new primal iterate x+ in fp32 NCHW.  v_mfma_f32_16x16x32_f16 with the C
-// output channels as the (padded-to-16) A rows; each wave covers 4 N-tiles of 16 px.
+// output channels as the (padded-to-16) A rows, kept in registers for the launch (72
+// VGPRs); each wave covers 4 N-tiles of 16 px (2 tile rows).  The kernel is HBM-bound
+// (8.4 MB of fp16 activations in, 2 x 0.8 MB fp32 per RGB 256^2 image), so it runs the
+// variant-3 memory pipeline: 3-deep LDS-DMA halo ring (two tiles in flight per CU), the
+// residual input x loaded by range-checked buffer loads at tile start (older than the
+// DMA, so the compiler's vmcnt for them does not wait on it), outputs moved to a
+// row-major lane layout with ds_bpermute (no LDS memory access, so no wait on the pending
+// LDS-DMA) so every load/store is one 64-lane row-contiguous fp32 instruction per channel,
+// and a counted vmcnt at the tile boundary that waits for the next tile's DMA only.
 // ------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void conv_tail_kernel(const half_t* __restrict__ in,
-                                                         const float* __restrict__ xin,
-                                                         float* __restrict__ xout,
-                                                         const uint4* __restrict__ wpk,
-                                                         const float* __restrict__ bias,
-                                                         ConvShape s, int C, int residual_sign,
-                                                         int clamp_out) {
+constexpr int kTailHalo = 44 * 1024;                           // 11 uniform DMA slots per wave
+constexpr int kTailLds = 3 * kTailHalo;                         // 135168 B
+
+__global__ __launch_bounds__(256, 1) void conv_tail_kernel(const half_t* __restrict__ in,
+                                                            const float* __restrict__ xin,
+                                                            float* __restrict__ xout,
+                                                            const uint4* __restrict__ wpk,
+                                                            const float* __restrict__ bias,
+                                                            ConvShape s, int C, int residual_sign,
+                                                            int clamp_out) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  unsigned char* wl = smem;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int q4 = lane >> 4, c16 = lane & 15;
-  for (int i = tid; i < kTailWBytes / 16; i += 256) reinterpret_cast<uint4*>(wl)[i] = wpk[i];
+  half8_t wA[kTailKSteps];
+#pragma unroll
+  for (int ks = 0; ks < kTailKSteps; ++ks)
+    wA[ks] = *reinterpret_cast<const half8_t*>(reinterpret_cast<const unsigned char*>(wpk) + (ks * 64 + lane) * 16);
   float bias_r[kMaxC];
 #pragma unroll
   for (int c = 0; c < kMaxC; ++c) bias_r[c] = c < C ? bias[c] : 0.f;
-  const size_t plane = (size_t)s.H * s.W;
+  const unsigned plane = (unsigned)(s.H * s.W);
+
+  auto buf = [&](int i) { return smem + i * kTailHalo; };
+  RingDma<4, true> dma;
+  dma.init(s, wave);
+  auto issue_dma = [&](int tt, int bi) {      // clamped: always the same instruction count
+    dma.issue(buf(bi), in, s, tt < s.tiles ? tt : s.tiles - 1, wave);
+  };
 
   int t = blockIdx.x;
-  int cur = 0;
   if (t < s.tiles) {
-    int b, ty0, tx0;
-    decode_tile(t, s, b, ty0, tx0);
-    halo_dma(smem + kTailWBytes, in, s, b, ty0, tx0);
+    issue_dma(t, 0);
+    issue_dma(t + gridDim.x, 1);
+    asm volatile("s_waitcnt vmcnt(11)" ::: "memory");                 // tile t landed
   }
   __syncthreads();
+  int cur = 0;
   for (; t < s.tiles; t += gridDim.x) {
     int b, ty0, tx0;
     decode_tile(t, s, b, ty0, tx0);
-    const int tn = t + gridDim.x;
-    if (tn < s.tiles) {                       // next tile -> other buffer, in flight
-      int bn, tyn, txn;
-      decode_tile(tn, s, bn, tyn, txn);
-      halo_dma(smem + kTailWBytes + (cur ^ 1) * kHaloDmaBytes, in, s, bn, tyn, txn);
+    // store layout: lane -> pixel (tile row 2*wave + lane/32, column lane%32)
+    const int y = ty0 + 2 * wave + (lane >> 5), x = tx0 + (lane & 31);
+    const unsigned off = (y < s.H && x < s.W) ? (unsigned)(y * s.W + x) * 4u : 0x80000000u;   // OOR: dropped
+    __amdgpu_buffer_rsrc_t rs[kMaxC];
+    float xi[kMaxC];
+#pragma unroll
+    for (int c = 0; c < kMaxC; ++c) {         // always kMaxC loads (c >= C: zero-size descriptor)
+      rs[c] = __builtin_amdgcn_make_buffer_rsrc((void*)(xin + ((size_t)b * C + (c < C ? c : 0)) * plane), (short)0,
+                                                c < C ? (int)(plane * 4u) : 0, 0x00020000);
+      xi[c] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs[c], off, 0, 0));
     }
-    const unsigned char* hl = smem + kTailWBytes + cur * kHaloDmaBytes;
+    __builtin_amdgcn_sched_barrier(0);       // residual loads stay older than the DMA
+    const int nxt2 = cur >= 1 ? cur - 1 : 2;
+    issue_dma(t + 2 * gridDim.x, nxt2);
+    const unsigned char* hl = buf(cur);
     auto ldB = [&](int ks, int n) {
       const int tap = ks >> 1;
       return *reinterpret_cast<const half8_t*>(
           hl + halo_off(2 * wave + (n >> 1) + tap / 3, 16 * (n & 1) + c16 + tap % 3, 4 * (ks & 1) + q4));
     };
     floatx4 acc[4] = {};
-    half8_t a = *reinterpret_cast<const half8_t*>(wl + lane * 16);
-    half8_t bf[4] = {ldB(0, 0), ldB(0, 1), ldB(0, 2), ldB(0, 3)};
+    half8_t fb[2][4];
+#pragma unroll
+    for (int n = 0; n < 4; ++n) fb[0][n] = ldB(0, n);
 #pragma unroll
     for (int ks = 0; ks < kTailKSteps; ++ks) {          // step ks+1 read while ks computes
-      half8_t na, nb[4];
+      const int r = ks & 1;
       if (ks + 1 < kTailKSteps) {
-        na = *reinterpret_cast<const half8_t*>(wl + ((ks + 1) * 64 + lane) * 16);
 #pragma unroll
-        for (int n = 0; n < 4; ++n) nb[n] = ldB(ks + 1, n);
+        for (int n = 0; n < 4; ++n) fb[r ^ 1][n] = ldB(ks + 1, n);
       }
 #pragma unroll
-      for (int n = 0; n < 4; ++n) acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, bf[n], acc[n], 0, 0, 0);
-      if (ks + 1 < kTailKSteps) {
-        a = na;
-#pragma unroll
-        for (int n = 0; n < 4; ++n) bf[n] = nb[n];
-      }
+      for (int n = 0; n < 4; ++n) acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wA[ks], fb[r][n], acc[n], 0, 0, 0);
     }
-    // C/D map of 16x16: col = lane & 15 (pixel), row = 4*(lane>>4) + r (output channel).
-    if (q4 == 0) {
+    // C/D map of 16x16: col = lane & 15 (pixel of N-tile n), row = 4*(lane>>4) + r (channel):
+    // lanes 0..15 hold channels 0..3 of N-tile n.  Store-layout lane l wants N-tile l>>4,
+    // pixel l&15: four cross-lane permutes per channel, then a per-lane select.
+    float net[kMaxC];
+    const int src = (lane & 15) << 2;
+#pragma unroll
+    for (int c = 0; c < kMaxC; ++c) {
+      float pv[4];
 #pragma unroll
       for (int n = 0; n < 4; ++n) {
-        const int y = ty0 + 2 * wave + (n >> 1), x = tx0 + 16 * (n & 1) + c16;
-        if (y < s.H && x < s.W) {
-#pragma unroll
-          for (int c = 0; c < kMaxC; ++c) {
-            if (c < C) {
-              const size_t idx = ((size_t)b * C + c) * plane + (size_t)y * s.W + x;
-              const float net = acc[n][c] + bias_r[c];
-              const float xi = xin[idx];
-              float o = residual_sign > 0 ? net + xi : xi - net;
-              if (clamp_out) o = fminf(fmaxf(o, 0.f), 1.f);
-              xout[idx] = o;
-            }
-          }
-        }
+        const float e = acc[n][c];   // a copy: bit_cast of an ext-vector element lvalue reads element 0 here
+        pv[n] = __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(src, __builtin_bit_cast(int, e)));
       }
+      const int nn = lane >> 4;
+      net[c] = nn == 0 ? pv[0] : nn == 1 ? pv[1] : nn == 2 ? pv[2] : pv[3];
     }
-    __syncthreads();                          // next tile landed; buffer cur free
-    cur ^= 1;
+
+#pragma unroll
+    for (int c = 0; c < kMaxC; ++c) {
+      const float nc = net[c] + bias_r[c];
+      float o = residual_sign > 0 ? nc + xi[c] : xi[c] - nc;
+      if (clamp_out) o = fminf(fmaxf(o, 0.f), 1.f);
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, o),
+                                            __builtin_amdgcn_make_buffer_rsrc(
+                                                (void*)(xout + ((size_t)b * C + (c < C ? c : 0)) * plane), (short)0,
+                                                c < C ? (int)(plane * 4u) : 0, 0x00020000),
+                                            off, 0, 0);
+    }
+    // tile t+1 landed: younger than its DMA are this tile's 4 loads, DMA of t+2 and 4 stores
+    asm volatile("s_waitcnt vmcnt(19) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    cur = cur == 2 ? 0 : cur + 1;
   }
 }
 
@@ -1175,7 +1212,6 @@ ConvShape make_conv_shape(int B, int H, int W) {
 }
 
 constexpr int kBodyLds = kBodyWBytes + 2 * kHaloDmaBytes + 256;   // 162048 B of the 160 KiB (+ bias)
-constexpr int kTailLds = kTailWBytes + 2 * kHaloDmaBytes;   // 106496 B: one workgroup per CU
 
 hipError_t conv_kernels_init() {
   hipError_t e = hipFuncSetAttribute((const void*)conv_body_kernel,
