@@ -59,8 +59,8 @@ struct pnp_ctx {
   // operator
   int op_kind = PNP_OP_ID;
   int op_H = 0, op_W = 0;
-  int op_ntaps = 0, op_R = 0;
-  DevBuf taps_fwd, taps_adj, mask;
+  int op_ntaps = 0, op_R = 0, op_taps_id = 0;
+  DevBuf taps_fwd, taps_adj, mask, dense_fwd, dense_adj;
 
   // solver
   int method = -1, B = 0, C = 0, H = 0, W = 0, cap = 0, it = 0;
@@ -194,6 +194,10 @@ OpDesc op_desc(pnp_ctx* ctx) {
   d.ntaps = ctx->op_ntaps;
   d.R = ctx->op_R;
   d.mask = P<const uint8_t>(ctx->mask);
+  d.dense_fwd = ctx->op_kind == PNP_OP_BLUR ? P<const float>(ctx->dense_fwd) : nullptr;
+  d.dense_adj = ctx->op_kind == PNP_OP_BLUR ? P<const float>(ctx->dense_adj) : nullptr;
+  d.Rd = ctx->op_kind == PNP_OP_BLUR ? dense_radius(ctx->op_R) : 0;
+  d.taps_id = ctx->op_kind == PNP_OP_BLUR ? ctx->op_taps_id : TAPS_DENSE;
   return d;
 }
 
@@ -317,7 +321,7 @@ void solver_iteration(pnp_ctx* ctx) {
   }
   {
     ProfScope ps(ctx, "k3_dual", st);
-    launch_k3(ctx->method, P<float>(ctx->y), P<float>(ctx->xobs), P<double>(ctx->partials), B, C, H, W, p.gamma2,
+    launch_k3(ctx->method, P<float>(ctx->y), P<float>(ctx->xobs), P<double>(ctx->partials), od, B, C, H, W, p.gamma2,
               l2_eps(ctx, n), P<double>(ctx->metrics), ctx->it, ctx->cap, record, ctx->has_true, st);
     check_launch(ctx, "k3");
   }
@@ -420,7 +424,7 @@ void solver_setup(pnp_ctx* ctx, int method, const pnp_params* params, int B, int
   }
   ensure_padded(ctx, ctx->u16, B, H, W, 4, ctx->stream);
   ensure(ctx, ctx->partials,
-         (size_t)B * std::max(partial_tiles(H, W), chunk_count((size_t)C * H * W)) * 4 * sizeof(double));
+         (size_t)B * std::max(partial_tiles(H, W) * C, chunk_count((size_t)C * H * W)) * 4 * sizeof(double));
   ensure(ctx, ctx->metrics, (size_t)B * std::max(ctx->cap, 1) * 2 * sizeof(double));
   ensure(ctx, ctx->theta, (size_t)B * sizeof(float));
   ctx->loaded = false;
@@ -520,7 +524,8 @@ int pnp_destroy(pnp_ctx* ctx) {
                     &ctx->taps_fwd, &ctx->taps_adj, &ctx->mask, &ctx->x[0], &ctx->x[1], &ctx->y, &ctx->s,
                     &ctx->w, &ctx->xobs, &ctx->xtrue, &ctx->u32, &ctx->u16, &ctx->act[0], &ctx->act[1],
                     &ctx->partials, &ctx->metrics, &ctx->theta, &ctx->scr_u32, &ctx->scr_u16,
-                    &ctx->scr_act[0], &ctx->scr_act[1], &ctx->scr_part, &ctx->scr_theta, &ctx->trash};
+                    &ctx->scr_act[0], &ctx->scr_act[1], &ctx->scr_part, &ctx->scr_theta, &ctx->trash,
+                    &ctx->z, &ctx->p, &ctx->t, &ctx->dense_fwd, &ctx->dense_adj};
   for (DevBuf* b : bufs) release(*b);
   for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -641,6 +646,30 @@ int pnp_set_operator(pnp_ctx* ctx, int kind, const double* h, int kh, int kw, co
       ensure(ctx, ctx->taps_adj, adj.size() * sizeof(int4));
       HIPCHK(ctx, hipMemcpy(ctx->taps_fwd.p, fwd.data(), fwd.size() * sizeof(int4), hipMemcpyHostToDevice));
       HIPCHK(ctx, hipMemcpy(ctx->taps_adj.p, adj.data(), adj.size() * sizeof(int4), hipMemcpyHostToDevice));
+      if (const int Rd = dense_radius(R)) {   // dense (2Rd+1)^2 tables for the register-blocked stencils
+        const int D = 2 * Rd + 1;
+        std::vector<float> df((size_t)D * D, 0.f), da((size_t)D * D, 0.f);
+        for (size_t i = 0; i < fwd.size(); ++i) {
+          float v;
+          std::memcpy(&v, &fwd[i].z, 4);
+          df[(size_t)(fwd[i].y + Rd) * D + fwd[i].x + Rd] += v;   // column-major: [ox + Rd][oy + Rd]
+          da[(size_t)(adj[i].y + Rd) * D + adj[i].x + Rd] += v;
+        }
+        std::vector<uint32_t> mf(D, 0u), mad(D, 0u);   // non-zero pattern, column-major like the tables
+        for (int cx = 0; cx < D; ++cx)
+          for (int cy = 0; cy < D; ++cy) {
+            if (df[(size_t)cx * D + cy] != 0.f) mf[cx] |= 1u << cy;
+            if (da[(size_t)cx * D + cy] != 0.f) mad[cx] |= 1u << cy;
+          }
+        ctx->op_taps_id = match_taps(Rd, mf.data(), mad.data());
+        std::vector<float> pf((size_t)(Rd + 1) * D * 4), pa((size_t)(Rd + 1) * D * 4);
+        pack_tap_pairs(Rd, df.data(), pf.data());
+        pack_tap_pairs(Rd, da.data(), pa.data());
+        ensure(ctx, ctx->dense_fwd, pf.size() * sizeof(float));
+        ensure(ctx, ctx->dense_adj, pa.size() * sizeof(float));
+        HIPCHK(ctx, hipMemcpy(ctx->dense_fwd.p, pf.data(), pf.size() * sizeof(float), hipMemcpyHostToDevice));
+        HIPCHK(ctx, hipMemcpy(ctx->dense_adj.p, pa.data(), pa.size() * sizeof(float), hipMemcpyHostToDevice));
+      }
       ctx->op_ntaps = (int)fwd.size();
       ctx->op_R = R;
       ctx->op_kind = kind;

@@ -37,7 +37,17 @@ struct OpDesc {
   int ntaps;
   int R;                  // max |offset| (halo radius), <= 16
   const uint8_t* mask;    // H*W keep-mask (random_sampling)
+  const float* dense_fwd; // packed tap pairs for the register-blocked stencils (ops.hip rb_stencil):
+  const float* dense_adj; //   [p = 0..Rd][oy + Rd][2][2], see pack_tap_pairs
+  int Rd;                 // radius of the dense tables: smallest of {2, 4, 8} >= R, 0 if R > 8
+  int taps_id;            // compile-time tap pattern (TAPS_*) the stencils are specialised on, 0 = dense
 };
+inline int dense_radius(int R) { return R <= 2 ? 2 : R <= 4 ? 4 : R <= 8 ? 8 : 0; }
+enum { TAPS_DENSE = 0, TAPS_BLUR_1 = 1, TAPS_SQUARE_MINI = 2 };
+// Which generated pattern (taps_gen.h) matches these column-major masks of Phi's dense table.
+int match_taps(int Rd, const uint32_t* fwd_cols, const uint32_t* adj_cols);
+// Column-major dense table W[ox + Rd][oy + Rd] -> the (Rd+1) x (2Rd+1) x 2 float2 pairs rb_stencil reads.
+void pack_tap_pairs(int Rd, const float* W, float* out);
 
 void launch_k1(int kind, const float* x, const float* y, const float* s, float* u32, half_t* u16, float* w,
                const OpDesc& op, int B, int C, int H, int W, float gamma1, int clamp_in, int method_b,
@@ -46,10 +56,12 @@ void launch_k2(int kind, int method, const float* xn, const float* xo, float* y,
                const float* xtrue, float* s, const float* w, const float* theta, double* partials,
                const OpDesc& op, int B, int C, int H, int W, double gamma2, double gkl_gamma, double gkl_alpha,
                int record, hipStream_t st);
-void launch_k3(int method, float* y, const float* xobs, const double* partials, int B, int C, int H, int W,
+void launch_k3(int method, float* y, const float* xobs, const double* partials, const OpDesc& op, int B, int C,
+               int H, int W,
                double gamma2, double eps, double* metrics, int it, int cap, int record, int has_true,
                hipStream_t st);
 int partial_tiles(int H, int W);
+int k2_partials(const OpDesc& op, int C, int H, int W);   // partial-sum entries per image written by launch_k2
 int chunk_count(size_t n);
 void launch_l1_select(const float* v, float* theta, int B, size_t n, double eta, hipStream_t st);
 // out = Phi(x) (or Phi^T x) [+ add]

@@ -17,6 +17,9 @@
 // kernel's non-zero taps with wrap-around halo loads; Phi^T is the correlation
 // (operators.py:24-38).  'random_sampling' is a pointwise keep-mask (operators.py:40-58).
 #include "kernels.h"
+#include "taps_gen.h"
+
+#include <utility>
 
 namespace pnp {
 
@@ -485,6 +488,242 @@ __global__ __launch_bounds__(256) void pack_input_kernel(const float* __restrict
 }
 
 // =====================================================================================
+// Register-blocked blur passes (operators.py:7-38 inside iteration.py:50/51).  The stencil
+// over a 19x19 (R = 9) or 5x5 (R = 2) kernel runs on a 64 x 128 block tile staged in LDS
+// with its periodic halo; thread (tx, ty) owns columns 2tx, 2tx+1 and rows 16ty .. +15.
+// For each of the 2R+2 LDS columns it touches, the thread loads the (16 + 2R)-row column
+// segment once into registers and applies every non-zero tap of the two kernel columns
+// that use it to its 16 x 2 accumulators: 0.2 LDS reads per FMA instead of 1 in stencil4.
+// Taps come from a dense (2R+1)^2 column-major table ([ox + R][oy + R]), one batch of
+// scalar loads per kernel column, zeros skipped by a uniform branch.
+// Per-tile partial sums are written per 32 x 32 cell (the k3 reduction grid).
+// =====================================================================================
+constexpr int kRbW = 64, kRbH = 128, kRbRows = 16;
+
+// Periodic ('wrap') halo fill of the (128+2R) x (64+2R) tile.  The loads of a batch of
+// kRbFill elements per thread are issued before any LDS store (all addresses clamped in
+// range, so the loads are unconditional and stay in flight together).
+constexpr int kRbFill = 8;
+template <int R, class F>
+__device__ __forceinline__ void rb_fill(float* lds, int i0, int j0, int H, int W, F val) {
+  constexpr int LW = kRbW + 2 * R, LH = kRbH + 2 * R, N = LW * LH;
+  for (int q0 = threadIdx.x; q0 < N; q0 += 256 * kRbFill) {
+    float v[kRbFill];
+#pragma unroll
+    for (int k = 0; k < kRbFill; ++k) {
+      const int q = min(q0 + 256 * k, N - 1);
+      const int ly = q / LW, lx = q - ly * LW;
+      int gi = i0 - R + ly, gj = j0 - R + lx;        // R <= H, W: one wrap covers the rows read
+      gi += gi < 0 ? H : 0;
+      gi -= gi >= H ? H : 0;
+      gj += gj < 0 ? W : 0;
+      gj -= gj >= W ? W : 0;
+      gi = gi < 0 ? 0 : (gi >= H ? H - 1 : gi);      // beyond: rows/cols only zero taps touch
+      gj = gj < 0 ? 0 : (gj >= W ? W - 1 : gj);
+      v[k] = val((size_t)gi * W + gj);
+    }
+#pragma unroll
+    for (int k = 0; k < kRbFill; ++k)
+      if (q0 + 256 * k < N) lds[q0 + 256 * k] = v[k];
+  }
+}
+
+typedef float f2_t __attribute__((ext_vector_type(2)));
+
+// Thread (tx, ty) accumulates rows 16ty..+15 of output columns 2tx, 2tx+1 as float2
+// pairs (v_pk_fma_f32).  LDS columns are read in pairs (A = 2tx+2p, B = A+1) by one
+// ds_read_b64 per row: 32 lanes x 8 B contiguous, conflict-free.  Column A feeds output
+// column 0 with kernel column 2p and output column 1 with kernel column 2p-1; column B
+// feeds them with kernel columns 2p+1 and 2p.  Each pair of taps is one packed FMA with
+// the column value broadcast.  The loop is fully unrolled over the compile-time non-zero
+// pattern TAPS (taps_gen.h; DenseTaps<R> for any other kernel): no per-tap branches (a
+// branch per tap made hipcc copy the 32 accumulators at every join) and no loads of
+// LDS columns or weights that only zero taps touch.  Tap values are runtime data.
+template <int R>
+struct DenseTaps {
+  static constexpr int kR = R;
+  static constexpr bool kDense = true;
+  __host__ __device__ static constexpr uint32_t col(int) { return (1u << (2 * R + 1)) - 1u; }
+};
+
+// wp: packed tap pairs [p][dyi][2] (float2): [.][.][0] = (W[2p][dyi], W[2p-1][dyi]) for
+// LDS column A, [.][.][1] = (W[2p+1][dyi], W[2p][dyi]) for column B (W = column-major
+// dense table, out-of-range columns 0), built on the host (pnp_set_operator) so each
+// packed FMA takes its weight pair straight from one s_load_dwordx2.
+template <class T, int P>
+__device__ __forceinline__ void rb_pair(const f2_t* base, const f2_t* __restrict__ wp, f2_t (&acc)[kRbRows]) {
+  constexpr int R = T::kR, LW = kRbW + 2 * R, D = 2 * R + 1;
+  constexpr uint32_t m0 = T::col(2 * P);
+  constexpr uint32_t mm1 = 2 * P >= 1 ? T::col(2 * P - 1) : 0u;
+  constexpr uint32_t m1 = 2 * P + 1 < D ? T::col(2 * P + 1) : 0u;
+  constexpr uint32_t mA = m0 | mm1, mB = m1 | m0;
+  if constexpr ((mA | mB) != 0u) {
+    f2_t cv[kRbRows + 2 * R];
+#pragma unroll
+    for (int k = 0; k < kRbRows + 2 * R; ++k) cv[k] = base[k * (LW / 2) + P];   // unused rows: dead loads
+#pragma unroll
+    for (int dyi = 0; dyi < D; ++dyi) {
+      if ((mA >> dyi) & 1u) {
+        const f2_t w2 = wp[(P * D + dyi) * 2 + 0];
+#pragma unroll
+        for (int r = 0; r < kRbRows; ++r)
+          acc[r] = __builtin_elementwise_fma(w2, f2_t{cv[r + dyi].x, cv[r + dyi].x}, acc[r]);
+      }
+      if ((mB >> dyi) & 1u) {
+        const f2_t w2 = wp[(P * D + dyi) * 2 + 1];
+#pragma unroll
+        for (int r = 0; r < kRbRows; ++r)
+          acc[r] = __builtin_elementwise_fma(w2, f2_t{cv[r + dyi].y, cv[r + dyi].y}, acc[r]);
+      }
+    }
+  }
+}
+
+template <class T, int... Ps>
+__device__ __forceinline__ void rb_pair_dispatch(int p, const f2_t* base, const f2_t* __restrict__ wp,
+                                                 f2_t (&acc)[kRbRows], std::integer_sequence<int, Ps...>) {
+  (void)((p == Ps ? (rb_pair<T, Ps>(base, wp, acc), true) : false) || ...);
+}
+
+// wp: packed tap pairs [p][dyi][2] (float2): [.][.][0] = (W[2p][dyi], W[2p-1][dyi]) for
+// LDS column A, [.][.][1] = (W[2p+1][dyi], W[2p][dyi]) for column B (W = column-major
+// dense table, out-of-range columns 0), built on the host (pnp_set_operator) so each
+// packed FMA takes its weight pair straight from one s_load_dwordx2.  The pair loop
+// stays a runtime loop (one straight-line, compile-time-masked body per pair), so the
+// weights and the column values of only one pair are live at a time.
+template <class T>
+__device__ __forceinline__ void rb_stencil(const float* lds, const f2_t* __restrict__ wp, f2_t (&acc)[kRbRows]) {
+  constexpr int R = T::kR, LW = kRbW + 2 * R;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+#pragma unroll
+  for (int r = 0; r < kRbRows; ++r) acc[r] = f2_t{0.f, 0.f};
+  const f2_t* base = reinterpret_cast<const f2_t*>(lds + ty * kRbRows * LW + 2 * tx);
+#pragma unroll 1
+  for (int p = 0; p <= R; ++p) rb_pair_dispatch<T>(p, base, wp, acc, std::make_integer_sequence<int, R + 1>{});
+}
+
+// One block = one 64 x 128 tile of ONE channel plane (grid (tiles, B*C)), so the halo
+// fill of one block overlaps the stencil of the others.  K1 writes its channel of the
+// NHWC4 fp16 denoiser input with 2-byte stores.
+template <class T>
+__global__ __launch_bounds__(256) void k1_blur_rb(const float* __restrict__ x, const float* __restrict__ y,
+                                                   const float* __restrict__ s, float* __restrict__ u32,
+                                                   half_t* __restrict__ u16, float* __restrict__ w,
+                                                   const f2_t* __restrict__ wd_adj, int C, int H, int W,
+                                                   int tiles_x, float gamma1, int clamp_in, int method_b) {
+  constexpr int R = T::kR;
+  __shared__ float lds[(kRbW + 2 * R) * (kRbH + 2 * R)];
+  const int tile = blockIdx.x, bc = blockIdx.y, b = bc / C, c = bc - b * C;
+  const int i0 = (tile / tiles_x) * kRbH, j0 = (tile % tiles_x) * kRbW;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const size_t plane = (size_t)H * W;
+  const float* yp = y + (size_t)bc * plane;
+  rb_fill<R>(lds, i0, j0, H, W, [&](size_t k) { return yp[k]; });
+  __syncthreads();
+  f2_t g[kRbRows];
+  rb_stencil<T>(lds, wd_adj, g);
+  const int j = j0 + 2 * tx;
+#pragma unroll
+  for (int r = 0; r < kRbRows; ++r) {
+    const int i = i0 + ty * kRbRows + r;
+    if (i >= H) break;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      if (j + q >= W) break;
+      const size_t idx = (size_t)bc * plane + (size_t)i * W + j + q;
+      float u = x[idx] - gamma1 * g[r][q];
+      if (clamp_in) u = fminf(fmaxf(u, 0.f), 1.f);
+      u32[idx] = u;
+      u16[(((size_t)b * (H + 2) + i + 1) * (W + 2) + j + q + 1) * 4 + c] = (half_t)u;
+      if (method_b) w[idx] = s[idx] - gamma1 * y[idx];
+    }
+  }
+}
+
+// partials: [B][cells][C][4] (per 32 x 32 cell and channel), reduced by k3 in that order.
+template <class T, int METHOD>
+__global__ __launch_bounds__(256) void k2_blur_rb(const float* __restrict__ xn, const float* __restrict__ xo,
+                                                   float* __restrict__ y, const float* __restrict__ xobs,
+                                                   const float* __restrict__ xtrue, float* __restrict__ s,
+                                                   const float* __restrict__ w, const float* __restrict__ theta,
+                                                   double* __restrict__ partials, const f2_t* __restrict__ wd_fwd,
+                                                   int C, int H, int W, int tiles_x, int cells_x, int cells,
+                                                   double gamma2, double gkl_gamma, double gkl_alpha, int record) {
+  constexpr int R = T::kR;
+  __shared__ float lds[(kRbW + 2 * R) * (kRbH + 2 * R)];
+  const int tile = blockIdx.x, bc = blockIdx.y, b = bc / C, c = bc - b * C;
+  const int i0 = (tile / tiles_x) * kRbH, j0 = (tile % tiles_x) * kRbW;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const size_t plane = (size_t)H * W;
+  const float* xnp = xn + (size_t)bc * plane;
+  const float* xop = xo + (size_t)bc * plane;
+  rb_fill<R>(lds, i0, j0, H, W, [&](size_t k) { return 2.f * xnp[k] - xop[k]; });
+  __syncthreads();
+  f2_t g[kRbRows];
+  rb_stencil<T>(lds, wd_fwd, g);
+  double d2 = 0, e2 = 0, n2 = 0, t2 = 0;
+  const float th = METHOD == M_B ? theta[b] : 0.f;
+  const int j = j0 + 2 * tx;
+#pragma unroll
+  for (int r = 0; r < kRbRows; ++r) {
+    const int i = i0 + ty * kRbRows + r;
+    if (i >= H) break;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      if (j + q >= W) break;
+      const size_t idx = (size_t)bc * plane + (size_t)i * W + j + q;
+      double gv = g[r][q];
+      if (METHOD == M_B) {
+        const float wv = w[idx];
+        const float sp = copysignf(fmaxf(fabsf(wv) - th, 0.f), wv);   // operators.py:98
+        gv += 2.0 * (double)sp - (double)s[idx];
+        s[idx] = sp;
+      }
+      const double v = (double)y[idx] + gamma2 * gv;
+      const double ob = xobs[idx];
+      if (METHOD == M_C) {
+        const double vv = v / gamma2;
+        const double tt = vv - gkl_gamma * gkl_alpha;
+        const double p = 0.5 * (tt + sqrt(tt * tt + 4.0 * gkl_gamma * ob));
+        y[idx] = (float)(v - gamma2 * p);
+      } else {
+        y[idx] = (float)v;
+        const double dd = v / gamma2 - ob;
+        d2 += dd * dd;
+      }
+      if (record) {
+        const double a = xn[idx], o = xo[idx];
+        e2 += (a - o) * (a - o);
+        n2 += o * o;
+        if (xtrue) {
+          const double qv = (double)xtrue[idx] - a;
+          t2 += qv * qv;
+        }
+      }
+    }
+  }
+  // 32 x 32 cell = 16 threads (tx) x 2 thread rows (ty pair) = lanes {c, c+32 : c in 16-lane group}
+  auto cell_sum = [](double v) {
+    v += __shfl_xor(v, 32, 64);
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+  };
+  d2 = cell_sum(d2);
+  e2 = cell_sum(e2);
+  n2 = cell_sum(n2);
+  t2 = cell_sum(t2);
+  const int lane = threadIdx.x & 63;
+  if ((lane & 47) == 0) {                              // lanes 0 and 16: the wave's two cells
+    const int gy = i0 / 32 + (ty >> 1), gx = j0 / 32 + (tx >> 4);
+    if (gy * 32 < H && gx < cells_x) {
+      double* p = partials + (((size_t)b * cells + (size_t)gy * cells_x + gx) * C + c) * 4;
+      p[0] = d2; p[1] = e2; p[2] = n2; p[3] = t2;
+    }
+  }
+}
+
+// =====================================================================================
 // comparisonB-2 (ADMM with denoiser, iteration.py:127-132, admm.py:30-44): elementwise
 // linear combinations and the per-image c_n / PSNR partial sums.
 // =====================================================================================
@@ -545,9 +784,32 @@ inline TileGrid tile_grid(int H, int W) {
   return g;
 }
 
+static bool rb_ok(const OpDesc& op, int C) { return op.kind == OP_BLUR && op.dense_fwd && op.Rd > 0 && C >= 1; }
+
+template <class T>
+static void launch_k1_rb(dim3 grid, hipStream_t st, const float* x, const float* y, const float* s, float* u32,
+                         half_t* u16, float* w, const OpDesc& op, int C, int H, int W, int tiles_x, float gamma1,
+                         int clamp_in, int method_b) {
+  hipLaunchKernelGGL((k1_blur_rb<T>), grid, dim3(256), 0, st, x, y, s, u32, u16, w, reinterpret_cast<const f2_t*>(op.dense_adj), C, H, W, tiles_x,
+                     gamma1, clamp_in, method_b);
+}
+
 void launch_k1(int kind, const float* x, const float* y, const float* s, float* u32, half_t* u16, float* w,
                const OpDesc& op, int B, int C, int H, int W, float gamma1, int clamp_in, int method_b,
                hipStream_t st) {
+  if (kind == OP_BLUR && rb_ok(op, C)) {
+    const int tx = (W + kRbW - 1) / kRbW, ty = (H + kRbH - 1) / kRbH;
+    const dim3 grid(tx * ty, B * C);
+#define K1RB(TT) launch_k1_rb<TT>(grid, st, x, y, s, u32, u16, w, op, C, H, W, tx, gamma1, clamp_in, method_b)
+    switch (op.taps_id) {
+      case TAPS_BLUR_1: K1RB(Taps_blur_1_Adj); break;
+      case TAPS_SQUARE_MINI: K1RB(Taps_square_mini_Adj); break;
+      default:
+        switch (op.Rd) { case 2: K1RB(DenseTaps<2>); break; case 4: K1RB(DenseTaps<4>); break; default: K1RB(DenseTaps<8>); }
+    }
+#undef K1RB
+    return;
+  }
   const TileGrid g = tile_grid(H, W);
   dim3 grid(g.tiles, B);
 #define K1_ARGS x, y, s, u32, u16, w, op, C, H, W, g.tiles_x, gamma1, clamp_in, method_b
@@ -570,11 +832,38 @@ static void launch_k2_kind(int method, dim3 grid, hipStream_t st, const float* x
 #undef K2_ARGS
 }
 
+template <class T>
+static void launch_k2_rb(int method, dim3 grid, hipStream_t st, const float* xn, const float* xo, float* y,
+                         const float* xobs, const float* xtrue, float* s, const float* w, const float* theta,
+                         double* partials, const OpDesc& op, int C, int H, int W, int tiles_x, int cells_x, int cells,
+                         double gamma2, double gkl_gamma, double gkl_alpha, int record) {
+#define K2RB_ARGS xn, xo, y, xobs, xtrue, s, w, theta, partials, reinterpret_cast<const f2_t*>(op.dense_fwd), C, H, W, tiles_x, cells_x, cells, gamma2, \
+                  gkl_gamma, gkl_alpha, record
+  if (method == M_A) hipLaunchKernelGGL((k2_blur_rb<T, M_A>), grid, dim3(256), 0, st, K2RB_ARGS);
+  else if (method == M_B) hipLaunchKernelGGL((k2_blur_rb<T, M_B>), grid, dim3(256), 0, st, K2RB_ARGS);
+  else hipLaunchKernelGGL((k2_blur_rb<T, M_C>), grid, dim3(256), 0, st, K2RB_ARGS);
+#undef K2RB_ARGS
+}
+
 void launch_k2(int kind, int method, const float* xn, const float* xo, float* y, const float* xobs,
                const float* xtrue, float* s, const float* w, const float* theta, double* partials,
                const OpDesc& op, int B, int C, int H, int W, double gamma2, double gkl_gamma, double gkl_alpha,
                int record, hipStream_t st) {
   const TileGrid g = tile_grid(H, W);
+  if (kind == OP_BLUR && rb_ok(op, C)) {
+    const int tx = (W + kRbW - 1) / kRbW, ty = (H + kRbH - 1) / kRbH;
+    const dim3 grid(tx * ty, B * C);
+#define K2RB(TT) launch_k2_rb<TT>(method, grid, st, xn, xo, y, xobs, xtrue, s, w, theta, partials, op, C, H, W, tx, \
+                                  g.tiles_x, g.tiles, gamma2, gkl_gamma, gkl_alpha, record)
+    switch (op.taps_id) {
+      case TAPS_BLUR_1: K2RB(Taps_blur_1_Fwd); break;
+      case TAPS_SQUARE_MINI: K2RB(Taps_square_mini_Fwd); break;
+      default:
+        switch (op.Rd) { case 2: K2RB(DenseTaps<2>); break; case 4: K2RB(DenseTaps<4>); break; default: K2RB(DenseTaps<8>); }
+    }
+#undef K2RB
+    return;
+  }
   dim3 grid(g.tiles, B);
   if (kind == OP_BLUR)
     launch_k2_kind<OP_BLUR>(method, grid, st, xn, xo, y, xobs, xtrue, s, w, theta, partials, op, C, H, W,
@@ -589,10 +878,40 @@ void launch_k2(int kind, int method, const float* xn, const float* xo, float* y,
 
 int partial_tiles(int H, int W) { return tile_grid(H, W).tiles; }
 
-void launch_k3(int method, float* y, const float* xobs, const double* partials, int B, int C, int H, int W,
-               double gamma2, double eps, double* metrics, int it, int cap, int record, int has_true,
+template <class TF, class TA>
+static bool taps_match(int Rd, const uint32_t* fwd_cols, const uint32_t* adj_cols) {
+  if (TF::kR != Rd || TA::kR != Rd) return false;
+  for (int k = 0; k < 2 * Rd + 1; ++k)
+    if (TF::col(k) != fwd_cols[k] || TA::col(k) != adj_cols[k]) return false;
+  return true;
+}
+
+void pack_tap_pairs(int Rd, const float* Wc, float* out) {
+  const int D = 2 * Rd + 1;
+  auto w = [&](int cx, int cy) { return cx >= 0 && cx < D ? Wc[(size_t)cx * D + cy] : 0.f; };
+  for (int p = 0; p <= Rd; ++p)
+    for (int dy = 0; dy < D; ++dy) {
+      float* o = out + ((size_t)p * D + dy) * 4;
+      o[0] = w(2 * p, dy);      o[1] = w(2 * p - 1, dy);   // LDS column A: (out col 0, out col 1)
+      o[2] = w(2 * p + 1, dy);  o[3] = w(2 * p, dy);       // LDS column B
+    }
+}
+
+int match_taps(int Rd, const uint32_t* fwd_cols, const uint32_t* adj_cols) {
+  if (taps_match<Taps_blur_1_Fwd, Taps_blur_1_Adj>(Rd, fwd_cols, adj_cols)) return TAPS_BLUR_1;
+  if (taps_match<Taps_square_mini_Fwd, Taps_square_mini_Adj>(Rd, fwd_cols, adj_cols)) return TAPS_SQUARE_MINI;
+  return TAPS_DENSE;
+}
+
+int k2_partials(const OpDesc& op, int C, int H, int W) {
+  return rb_ok(op, C) ? tile_grid(H, W).tiles * C : tile_grid(H, W).tiles;
+}
+
+void launch_k3(int method, float* y, const float* xobs, const double* partials, const OpDesc& op, int B, int C,
+               int H, int W, double gamma2, double eps, double* metrics, int it, int cap, int record, int has_true,
                hipStream_t st) {
-  const TileGrid g = tile_grid(H, W);
+  TileGrid g = tile_grid(H, W);
+  g.tiles = k2_partials(op, C, H, W);
   const size_t n = (size_t)C * H * W;
   if (method == M_C) {
     if (record) hipLaunchKernelGGL(k3_metrics, dim3(B), dim3(256), 0, st, partials, g.tiles, n, metrics, it, cap,
