@@ -498,7 +498,7 @@ __global__ __launch_bounds__(256) void pack_input_kernel(const float* __restrict
 // scalar loads per kernel column, zeros skipped by a uniform branch.
 // Per-tile partial sums are written per 32 x 32 cell (the k3 reduction grid).
 // =====================================================================================
-constexpr int kRbW = 64, kRbH = 128, kRbRows = 16;
+constexpr int kRbW = 64, kRbH = 64, kRbRows = 8;   // 8 waves x 2 thread rows x 8 rows
 
 // Periodic ('wrap') halo fill of the (128+2R) x (64+2R) tile.  The loads of a batch of
 // kRbFill elements per thread are issued before any LDS store (all addresses clamped in
@@ -702,24 +702,32 @@ __global__ __launch_bounds__(256) void k2_blur_rb(const float* __restrict__ xn, 
       }
     }
   }
-  // 32 x 32 cell = 16 threads (tx) x 2 thread rows (ty pair) = lanes {c, c+32 : c in 16-lane group}
-  auto cell_sum = [](double v) {
+  // 32 x 32 cell = 16 threads (tx) x 4 thread rows (ty) = two half-cells of two waves:
+  // reduce each half in its wave (lanes {c, c+32}: xor 32, then xor 8..1), then combine
+  // the two waves' halves through LDS in a fixed order.
+  auto half_sum = [](double v) {
     v += __shfl_xor(v, 32, 64);
 #pragma unroll
     for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
   };
-  d2 = cell_sum(d2);
-  e2 = cell_sum(e2);
-  n2 = cell_sum(n2);
-  t2 = cell_sum(t2);
-  const int lane = threadIdx.x & 63;
-  if ((lane & 47) == 0) {                              // lanes 0 and 16: the wave's two cells
-    const int gy = i0 / 32 + (ty >> 1), gx = j0 / 32 + (tx >> 4);
-    if (gy * 32 < H && gx < cells_x) {
-      double* p = partials + (((size_t)b * cells + (size_t)gy * cells_x + gx) * C + c) * 4;
-      p[0] = d2; p[1] = e2; p[2] = n2; p[3] = t2;
-    }
+  __shared__ double red[8][2][4];
+  d2 = half_sum(d2);
+  e2 = half_sum(e2);
+  n2 = half_sum(n2);
+  t2 = half_sum(t2);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if ((lane & 47) == 0) {                              // lanes 0 and 16: the wave's two half-cells
+    double* q = red[wave][lane >> 4];
+    q[0] = d2; q[1] = e2; q[2] = n2; q[3] = t2;
+  }
+  __syncthreads();
+  if (threadIdx.x < 16) {                              // 2 x 2 cells x 4 sums
+    const int cell = threadIdx.x >> 2, k = threadIdx.x & 3, cy = cell >> 1, cx = cell & 1;
+    const int gy = i0 / 32 + cy, gx = j0 / 32 + cx;
+    if (gy * 32 < H && gx < cells_x)
+      partials[(((size_t)b * cells + (size_t)gy * cells_x + gx) * C + c) * 4 + k] =
+          red[2 * cy][cx][k] + red[2 * cy + 1][cx][k];
   }
 }
 
