@@ -140,7 +140,7 @@ def main():
     ap.add_argument("--profile", type=int, default=1, help="HIP-event per-kernel timing in the timed region")
     ap.add_argument("--chunk", type=int, default=0, help="images per denoiser pass (0 = auto)")
     ap.add_argument("--chunk-sweep", type=str, default="", help="e.g. 4,8,16,256: time each (stderr)")
-    ap.add_argument("--variant", type=int, default=3, help="conv_body kernel variant (0..3)")
+    ap.add_argument("--variant", type=int, default=1, help="body layers per launch: 1 = two (fused), 0 = one")
     ap.add_argument("--variant-sweep", type=str, default="", help="e.g. 0,1: interleaved A/B (stderr)")
     args = ap.parse_args()
 
@@ -248,19 +248,31 @@ def main():
         if prof:
             kt = {k: round(v[0], 4) for k, v in prof.items()}
             line["kernel_ms"] = kt
-            body_ms = prof["conv_body"][0]
+            fused = "conv_body2" in prof          # two 64->64 layers per launch (intermediate in LDS)
+            kname = "conv_body2" if fused else "conv_body"
+            body_ms = prof[kname][0]
             m = images_per_launch(B, H, W, args.chunk)
-            fl = conv_flops_per_launch(m, H, W)
-            by = conv_bytes_per_launch(m, H, W)
+            nl = 2 if fused else 1
+            fl = nl * conv_flops_per_launch(m, H, W)
+            by = conv_bytes_per_launch(m, H, W)    # read + write the fp16 activations once per launch
             gbs = by / (body_ms * 1e-3) / 1e9
             tfl = fl / (body_ms * 1e-3) / 1e12
-            # arithmetic intensity 288 FLOP/B < ridge 2500/8 = 312.5: the HBM roof binds
-            line["roofline"] = {"kernel": "conv_body (64->64 3x3 implicit GEMM, fp16 MFMA)", "bound": "hbm",
-                                "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": measured_traffic("conv_body", B),
-                                "bytes_per_launch": by, "flops_per_launch": fl,
-                                "mfma_tflops": round(tfl, 1), "mfma_frac": round(tfl / FP16_PEAK_TFLOPS, 4),
-                                "traffic_source": TRAFFIC_JSON}
+            # per launch: 288 FLOP/B (one layer, below the 312 FLOP/B ridge: HBM roof) or 576 FLOP/B
+            # (two fused layers, above it: MFMA roof)
+            if fused:
+                line["roofline"] = {"kernel": "conv_body2 (two fused 64->64 3x3 layers, fp16 MFMA)", "bound": "mfma",
+                                    "achieved": round(tfl, 1), "peak": FP16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                                    "frac": round(tfl / FP16_PEAK_TFLOPS, 4),
+                                    "traffic": measured_traffic(kname, B), "bytes_per_launch": by,
+                                    "flops_per_launch": fl, "hbm_gbs": round(gbs, 1),
+                                    "hbm_frac": round(gbs / HBM_PEAK_GBS, 4), "traffic_source": TRAFFIC_JSON}
+            else:
+                line["roofline"] = {"kernel": "conv_body (64->64 3x3 implicit GEMM, fp16 MFMA)", "bound": "hbm",
+                                    "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                    "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": measured_traffic(kname, B),
+                                    "bytes_per_launch": by, "flops_per_launch": fl,
+                                    "mfma_tflops": round(tfl, 1), "mfma_frac": round(tfl / FP16_PEAK_TFLOPS, 4),
+                                    "traffic_source": TRAFFIC_JSON}
             pb = prox_bytes(B, C, H, W)
             line["prox_hbm"] = {k: {"GB/s": round(pb[k] / (prof[k][0] * 1e-3) / 1e9, 1),
                                     "frac": round(pb[k] / (prof[k][0] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}

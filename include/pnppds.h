@@ -106,8 +106,8 @@ int pnp_set_precision(pnp_ctx* ctx, int precision);
  * pair of a pass is sized to stay resident in the 256 MB Infinity Cache).             */
 enum pnp_tuning_key {
   PNP_TUNE_DENOISE_CHUNK = 1,
-  PNP_TUNE_BODY_VARIANT = 2   /* 64->64 conv kernel: 0 = 4 waves/WG, 1 = 8 waves/WG,
-                                 2 = warp-specialised, 3 = weights in registers (default) */
+  PNP_TUNE_BODY_VARIANT = 2   /* 64->64 body layers: 1 = two layers per launch, the intermediate
+                                 kept in LDS (default); 0 = one layer per launch */
 };
 int pnp_set_tuning(pnp_ctx* ctx, int key, int value);
 

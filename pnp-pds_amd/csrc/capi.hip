@@ -48,11 +48,7 @@ struct pnp_ctx {
   // denoiser
   int den_C = 0, den_depth = 0, den_act = 0, den_residual = 1, den_clamp = 1;
   int den_chunk = 0;   // images per denoiser pass; 0 = auto
-  int body_variant = 3;   // conv_body kernel: 0 = 4 waves x 2 rows, 1 = 8 waves x 1 row,
-                          // 2 = warp-specialised, 3 = weights in registers + 3-deep halo ring,
-                          // 4 = one wave per SIMD holding the whole layer's weights,
-                          // 5 / 6 = variant 3 on a channel-plane halo, 2- / 3-deep fragment ring
-  int ablate = 0;         // profiling only (env PNPPDS_ABLATE); results are wrong when set
+  int body_fused = 1;     // 1: body layers two per launch (conv_body2), 0: one per launch (conv_body_v3)
   bool den_ready = false;
   DevBuf head_w, head_b, body_w, body_b, tail_w, tail_b;
 
@@ -72,7 +68,6 @@ struct pnp_ctx {
 
   // scratch for single ops
   DevBuf scr_u32, scr_u16, scr_act[2], scr_part, scr_theta;
-  DevBuf trash;   // sink of masked-out conv epilogue stores
 
   // profiling
   bool prof = false;
@@ -209,16 +204,17 @@ void check_operator_shape(pnp_ctx* ctx, int H, int W) {
 }
 
 // -------- denoiser forward: u16 (padded NHWC4) + u32 (NCHW) -> xout --------------------
-size_t act_bytes(int B, int H, int W, int ch) {
-  // + slack: partial tiles read up to 8 rows / 34 pixels past the last image
-  return ((size_t)B * (H + 2) * (W + 2) + (size_t)10 * (W + 2) + 64) * ch * sizeof(half_t);
+size_t act_bytes(int B, int H, int W, int ch, int pad) {
+  // + slack: partial tiles read up to 12 rows / 36 pixels past the last image
+  const size_t Wp = (size_t)W + 2 * pad;
+  return ((size_t)B * (H + 2 * pad) * Wp + 16 * Wp + 64) * ch * sizeof(half_t);
 }
 
 // Padded activation images: the one-pixel border must be zero for the geometry in use.
 // Kernels never write the border, so a buffer is zeroed once per (B, H, W) it serves;
 // reusing it for another geometry (whose border lands on stale interior data) re-zeroes.
-void ensure_padded(pnp_ctx* ctx, DevBuf& b, int B, int H, int W, int ch, hipStream_t st) {
-  const size_t bytes = act_bytes(B, H, W, ch);
+void ensure_padded(pnp_ctx* ctx, DevBuf& b, int B, int H, int W, int ch, int pad, hipStream_t st) {
+  const size_t bytes = act_bytes(B, H, W, ch, pad);
   const long long geom = ((long long)B << 40) ^ ((long long)H << 20) ^ (long long)W;
   ensure(ctx, b, bytes);
   if (b.geom != geom) {
@@ -228,7 +224,7 @@ void ensure_padded(pnp_ctx* ctx, DevBuf& b, int B, int H, int W, int ch, hipStre
 }
 
 void ensure_act(pnp_ctx* ctx, DevBuf (&act)[2], int B, int H, int W, hipStream_t st) {
-  for (int i = 0; i < 2; ++i) ensure_padded(ctx, act[i], B, H, W, kWidth, st);
+  for (int i = 0; i < 2; ++i) ensure_padded(ctx, act[i], B, H, W, kWidth, kActPad, st);
 }
 
 // Images per denoiser pass.  Auto: the whole batch, unless its two fp16 activation
@@ -236,7 +232,7 @@ void ensure_act(pnp_ctx* ctx, DevBuf (&act)[2], int B, int H, int W, hipStream_t
 // 256 MB Infinity Cache measured no faster at 256x256: conv_body is not HBM-bound.)
 int denoise_chunk(pnp_ctx* ctx, int B, int H, int W) {
   if (ctx->den_chunk > 0) return std::min(ctx->den_chunk, B);
-  const double per_img = 2.0 * (H + 2) * (W + 2) * kWidth * sizeof(half_t);
+  const double per_img = 2.0 * (H + 2 * kActPad) * (W + 2 * kActPad) * kWidth * sizeof(half_t);
   const int m = (int)std::floor(8e9 / per_img);
   return std::max(1, std::min(m, B));
 }
@@ -251,9 +247,6 @@ void run_denoiser(pnp_ctx* ctx, const half_t* u16, const float* u32, float* xout
   for (int b0 = 0; b0 < B; b0 += m) {
     const int mb = std::min(m, B - b0);
     ConvShape s = make_conv_shape(mb, H, W);
-    s.ablate = ctx->ablate;
-    ensure(ctx, ctx->trash, 4096);
-    s.trash = P<half_t>(ctx->trash);
     const half_t* in4 = u16 + (size_t)b0 * (H + 2) * (W + 2) * 4;
     const float* xin = u32 + (size_t)b0 * C * H * W;
     float* xo = xout + (size_t)b0 * C * H * W;
@@ -264,11 +257,23 @@ void run_denoiser(pnp_ctx* ctx, const half_t* u16, const float* u32, float* xout
       check_launch(ctx, "conv_head");
     }
     int cur = 0;
-    for (int l = 0; l < ctx->den_depth - 2; ++l) {
-      ProfScope ps(ctx, "conv_body", st);
-      launch_conv_body(P<half_t>(act[cur]), P<half_t>(act[cur ^ 1]), (const char*)ctx->body_w.p + l * kBodyWBytes,
-                       P<float>(ctx->body_b) + l * kWidth, s, ctx->den_act, ctx->num_cus, ctx->body_variant, st);
-      check_launch(ctx, "conv_body");
+    const int nbody = ctx->den_depth - 2;
+    for (int l = 0; l < nbody;) {
+      const char* wl = (const char*)ctx->body_w.p + (size_t)l * kBodyWBytes;
+      const float* bl = P<float>(ctx->body_b) + l * kWidth;
+      if (ctx->body_fused && l + 1 < nbody) {      // layers l+1, l+2 of simple_CNN in one launch
+        ProfScope ps(ctx, "conv_body2", st);
+        launch_conv_body2(P<half_t>(act[cur]), P<half_t>(act[cur ^ 1]), wl, bl, wl + kBodyWBytes, bl + kWidth, s,
+                          ctx->den_act, ctx->num_cus, st);
+        check_launch(ctx, "conv_body2");
+        l += 2;
+      } else {
+        ProfScope ps(ctx, "conv_body", st);
+        launch_conv_body(P<half_t>(act[cur]), P<half_t>(act[cur ^ 1]), wl, bl, s, ctx->den_act, ctx->num_cus, 0,
+                         st);
+        check_launch(ctx, "conv_body");
+        l += 1;
+      }
       cur ^= 1;
     }
     {
@@ -422,7 +427,7 @@ void solver_setup(pnp_ctx* ctx, int method, const pnp_params* params, int B, int
     ensure(ctx, ctx->p, fb);
     ensure(ctx, ctx->t, fb);
   }
-  ensure_padded(ctx, ctx->u16, B, H, W, 4, ctx->stream);
+  ensure_padded(ctx, ctx->u16, B, H, W, 4, 1, ctx->stream);
   ensure(ctx, ctx->partials,
          (size_t)B * std::max(partial_tiles(H, W) * C, chunk_count((size_t)C * H * W)) * 4 * sizeof(double));
   ensure(ctx, ctx->metrics, (size_t)B * std::max(ctx->cap, 1) * 2 * sizeof(double));
@@ -504,7 +509,6 @@ int pnp_create(int device, pnp_ctx** out) {
         fail(ctx, PNP_E_UNSUPPORTED, "device %d is %s; this library is built for gfx950 only", device,
              prop.gcnArchName);
       ctx->num_cus = prop.multiProcessorCount;
-      if (const char* ab = std::getenv("PNPPDS_ABLATE")) ctx->ablate = std::atoi(ab);   // profiling only
       HIPCHK(ctx, hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
       HIPCHK(ctx, conv_kernels_init());
     } catch (const PnpError&) {
@@ -524,7 +528,7 @@ int pnp_destroy(pnp_ctx* ctx) {
                     &ctx->taps_fwd, &ctx->taps_adj, &ctx->mask, &ctx->x[0], &ctx->x[1], &ctx->y, &ctx->s,
                     &ctx->w, &ctx->xobs, &ctx->xtrue, &ctx->u32, &ctx->u16, &ctx->act[0], &ctx->act[1],
                     &ctx->partials, &ctx->metrics, &ctx->theta, &ctx->scr_u32, &ctx->scr_u16,
-                    &ctx->scr_act[0], &ctx->scr_act[1], &ctx->scr_part, &ctx->scr_theta, &ctx->trash,
+                    &ctx->scr_act[0], &ctx->scr_act[1], &ctx->scr_part, &ctx->scr_theta,
                     &ctx->z, &ctx->p, &ctx->t, &ctx->dense_fwd, &ctx->dense_adj};
   for (DevBuf* b : bufs) release(*b);
   for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
@@ -549,8 +553,8 @@ int pnp_set_tuning(pnp_ctx* ctx, int key, int value) {
       return;
     }
     if (key == PNP_TUNE_BODY_VARIANT) {
-      if (value < 0 || value > 6) fail(ctx, PNP_E_ARG, "body variant must be 0..6");
-      ctx->body_variant = value;
+      if (value < 0 || value > 1) fail(ctx, PNP_E_ARG, "body variant must be 0 (one layer/launch) or 1 (two)");
+      ctx->body_fused = value;
       return;
     }
     fail(ctx, PNP_E_UNSUPPORTED, "tuning key %d", key);
@@ -885,7 +889,7 @@ int pnp_op_denoise(pnp_ctx* ctx, const float* x, float* out, int B, int C, int H
     if (C != ctx->den_C) fail(ctx, PNP_E_ARG, "denoiser has %d channels, input has %d", ctx->den_C, C);
     hipStream_t st = pick_stream(ctx, stream);
     ensure(ctx, ctx->scr_u32, (size_t)B * C * H * W * sizeof(float));
-    ensure_padded(ctx, ctx->scr_u16, B, H, W, 4, st);
+    ensure_padded(ctx, ctx->scr_u16, B, H, W, 4, 1, st);
     launch_pack_input(x, P<float>(ctx->scr_u32), P<half_t>(ctx->scr_u16), B, C, H, W, ctx->den_clamp, st);
     check_launch(ctx, "pack_input");
     run_denoiser(ctx, P<half_t>(ctx->scr_u16), P<float>(ctx->scr_u32), out, ctx->scr_act, B, H, W, st);

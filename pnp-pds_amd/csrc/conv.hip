@@ -4,18 +4,18 @@
 // 18 x [conv + LeakyReLU], out_conv + x_in) and models/denoiser.py:34-46 (clamp in/out);
 // KAIR variant models/network_dncnn.py:42-77 (ReLU, x - n, no clamps).
 //
-// GEMM view per layer: D[cout][pixel] = sum_k W[cout][k] * X[k][pixel],
-// k = (tap, cin).  A operand = packed weights (host-packed in MFMA fragment order,
-// staged once per workgroup into LDS), B operand = activations read from an LDS
-// halo tile.  fp16 operands, fp32 accumulation (v_mfma_f32_32x32x16_f16 for the
-// 64-channel layers, v_mfma_f32_16x16x32_f16 for the 64->C tail).
+// GEMM view per layer: D[cout][pixel] = sum_k W[cout][k] * X[k][pixel], k = (tap, cin).
+// A operand = host-packed weights (MFMA fragment order), B operand = activations from an
+// LDS halo tile, fp16 operands, fp32 accumulation (v_mfma_f32_32x32x16_f16 for the
+// 64-channel layers, v_mfma_f32_16x16x32_f16 for the 64 -> C tail).
 //
-// Workgroup = 4 waves, persistent over 8x32-pixel output tiles; wave w owns output
-// rows 2w, 2w+1 (two 32-pixel N-tiles) x all 64 output channels (two 32-row M-tiles)
-// = 4 accumulators of 32x32.  Per K-step: 2 weight + 2 activation ds_read_b128 and
-// 4 MFMAs.
-#include <type_traits>
-
+// Hidden activations are fp16 NHWC64 images with a zero border of s.pad = 2 pixels (each
+// pixel one 128-B line): the two-layer fused body kernel reads a 2-pixel halo.
+//
+//   conv_head      C -> 64, from the padded NHWC4 fp16 input
+//   conv_body_v3   64 -> 64, one layer per launch
+//   conv_body2     64 -> 64 -> 64, two layers per launch (halves the activation traffic)
+//   conv_tail      64 -> C + residual + clamp, fp32 NCHW out
 #include "kernels.h"
 
 namespace pnp {
@@ -29,78 +29,13 @@ __device__ __forceinline__ void decode_tile(int t, const ConvShape& s, int& b, i
   tx0 = (r - ty * s.tiles_x) * kTileW;
 }
 
-// The 10 x 34 x 64-channel halo tile (padded coords [ty0, ty0+10) x [tx0, tx0+34)) is
-// 2720 16-byte chunks: 11 per thread.  Consecutive threads read consecutive 16 B of a
-// pixel row (coalesced); 8 lanes write one 128-B pixel of the swizzled LDS image.
-constexpr int kHaloChunks = kHaloPix * 8;
-constexpr int kHaloPerThread = (kHaloChunks + 255) / 256;
-
-// Issue the global loads of a halo tile into registers (no wait: T14 issue-early).
-// Every lane loads unconditionally (surplus lanes re-read the last pixel): a guarded load
-// makes hipcc merge the destination through a branch and wait vmcnt right after issue.
-__device__ __forceinline__ void halo_load(uint4 (&v)[kHaloPerThread], const half_t* __restrict__ in,
-                                          const ConvShape& s, int b, int ty0, int tx0) {
-  const half_t* base = in + (((size_t)b * s.Hp + ty0) * s.Wp + tx0) * kWidth;
-#pragma unroll
-  for (int k = 0; k < kHaloPerThread; ++k) {
-    const int q = threadIdx.x + 256 * k;
-    const int p = min(q >> 3, kHaloPix - 1), c = q & 7;
-    const int pr = p / kHaloW, pc = p - pr * kHaloW;
-    v[k] = *reinterpret_cast<const uint4*>(base + ((size_t)pr * s.Wp + pc) * kWidth + c * 8);
-  }
-}
-
-// Write a loaded halo tile into an LDS image (write-late).
-__device__ __forceinline__ void halo_store(unsigned char* hl, const uint4 (&v)[kHaloPerThread]) {
-#pragma unroll
-  for (int k = 0; k < kHaloPerThread; ++k) {
-    const int q = threadIdx.x + 256 * k;
-    if (q < kHaloChunks) *reinterpret_cast<uint4*>(hl + halo_chunk_offset(q >> 3, q & 7)) = v[k];
-  }
-}
-
-__device__ __forceinline__ void stage_halo64(unsigned char* hl, const half_t* __restrict__ in,
-                                             const ConvShape& s, int b, int ty0, int tx0) {
-  uint4 v[kHaloPerThread];
-  halo_load(v, in, s, b, ty0, tx0);
-  halo_store(hl, v);
-}
-
-// LDS-DMA (global_load_lds_dwordx4) staging of a halo tile: no register destination, so
-// the loads stay in flight across the MFMA loop.  One wave-instruction writes 1 KiB of
-// LDS = 8 pixels: slot g (g = 4j + wave, 43 slots) covers pixels 8g .. 8g+7.  The LDS
-// destination is lane-linear, so the XOR swizzle is applied to the per-lane SOURCE
-// address (lane l loads logical chunk (l&7) ^ swz(p) of pixel p into slot l&7).  Slots
-// past pixel 339 re-read pixel 339 into the 4-pixel pad (never read back).
-constexpr int kDmaSlots = (kHaloPix + 7) / 8;                 // 43
-constexpr int kHaloDmaBytes = kDmaSlots * 1024;               // 44032
-template <int NW = 4>
-__device__ __forceinline__ void halo_dma(unsigned char* hl, const half_t* __restrict__ in, const ConvShape& s,
-                                         int b, int ty0, int tx0) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const half_t* base = in + (((size_t)b * s.Hp + ty0) * s.Wp + tx0) * kWidth;
-#pragma unroll
-  for (int j = 0; j < (kDmaSlots + NW - 1) / NW; ++j) {
-    const int g = NW * j + wave;
-    if (g < kDmaSlots) {
-      const int p = 8 * g + (lane >> 3);
-      const int pl = min(p, kHaloPix - 1);
-      const int pr = pl / kHaloW, pc = pl - pr * kHaloW;
-      const int c = (lane & 7) ^ ((pc >> 1) & 7);
-      const half_t* src = base + ((size_t)pr * s.Wp + pc) * kWidth + c * 8;
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                       (__attribute__((address_space(3))) void*)(hl + g * 1024), 16, 0, 0);
-    }
-  }
-}
-
-// Epilogue shared by head and body: bias + activation, fp16, two 16-B stores per
-// (M-tile) into the padded NHWC64 output.  Lane (col, h) owns channels 32m+16h .. +15.
+// Epilogue of the head: bias + activation, fp16, two 16-B stores per M-tile into the
+// padded NHWC64 output.  Lane (col, h) owns channels 32m+16h .. +15.
 __device__ __forceinline__ void store_act64(half_t* __restrict__ out, const ConvShape& s, int b, int y,
                                             int x, int h, const floatx16& acc0, const floatx16& acc1,
                                             const float (&bias)[2][16], int act) {
   if (y >= s.H || x >= s.W) return;
-  half_t* o = out + (((size_t)b * s.Hp + y + 1) * s.Wp + x + 1) * kWidth + 16 * h;
+  half_t* o = out + (((size_t)b * s.Hp + y + s.pad) * s.Wp + x + s.pad) * kWidth + 16 * h;
   half8_t v0, v1, v2, v3;
 #pragma unroll
   for (int r = 0; r < 8; ++r) {
@@ -115,524 +50,23 @@ __device__ __forceinline__ void store_act64(half_t* __restrict__ out, const Conv
   *reinterpret_cast<half8_t*>(o + 40) = v3;
 }
 
-// Coalesced epilogue: bias + activation + fp16 of NT 32-pixel N-tiles held by one wave,
-// written into that wave's private LDS staging region (pixel-major, 16-B chunks XOR-
-// swizzled by pixel&7: conflict-free ds_write_b128), then read back so that each
-// wave-instruction stores 8 whole pixels = 1 KiB contiguous (8 full 128-B lines).
-// The scattered direct store (64 separate 16-B pieces per instruction) cost 0.5 ms of a
-// 1.45 ms layer at 256x256x256 (ablation).
-template <int NT>
-__device__ __forceinline__ void epilogue_coalesced(unsigned char* stage, half_t* __restrict__ out,
-                                                   const ConvShape& s, int b, const int (&rows)[NT], int tx0,
-                                                   const floatx16 (&acc)[2][NT], const float (&bias)[2][16],
-                                                   int act) {
-  const int lane = threadIdx.x & 63, h = lane >> 5, col = lane & 31;
-#pragma unroll
-  for (int n = 0; n < NT; ++n) {
-    const int pix = n * 32 + col;
-#pragma unroll
-    for (int m = 0; m < 2; ++m) {
-      half8_t lo, hi;
-#pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        lo[r] = (half_t)act_fn(acc[m][n][r] + bias[m][r], act);
-        hi[r] = (half_t)act_fn(acc[m][n][r + 8] + bias[m][r + 8], act);
-      }
-      const int q = 4 * m + 2 * h;       // 16-B chunk index of channels 32m+16h .. +7
-      *reinterpret_cast<half8_t*>(stage + pix * 128 + 16 * (q ^ (pix & 7))) = lo;
-      *reinterpret_cast<half8_t*>(stage + pix * 128 + 16 * ((q + 1) ^ (pix & 7))) = hi;
-    }
-  }
-  // own region only: a wave-level LDS fence suffices before reading back
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  // Stores through one buffer descriptor per output row whose record count covers exactly
-  // the valid pixels: the hardware range check drops out-of-image lanes, so every wave
-  // issues exactly NT*4 store instructions with no branches, and the caller's counted
-  // vmcnt(NT*4) waits for the (older) prefetch DMA only, leaving these stores in flight.
-  typedef int v4i_t __attribute__((ext_vector_type(4)));
-  v4i_t v[NT * 4];
-#pragma unroll
-  for (int j = 0; j < NT * 4; ++j) {
-    const int pix = 8 * j + (lane >> 3), c = lane & 7;
-    v[j] = *reinterpret_cast<const v4i_t*>(stage + pix * 128 + 16 * (c ^ (pix & 7)));
-  }
-  const int ncols = min(kTileW, s.W - tx0);
-#pragma unroll
-  for (int n = 0; n < NT; ++n) {
-    const int y = __builtin_amdgcn_readfirstlane(rows[n]);          // wave-uniform (T20)
-    half_t* row = out + (((size_t)b * s.Hp + y + 1) * s.Wp + tx0 + 1) * kWidth;
-    const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc(row, (short)0, y < s.H ? ncols * 128 : 0, 0x00020000);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int j = 4 * n + q, pix = 8 * j + (lane >> 3), c = lane & 7;
-      __builtin_amdgcn_raw_buffer_store_b128(v[j], rs, (pix & 31) * 128 + c * 16, 0, 0);
-    }
-  }
-}
-
-// Deferred form of the same epilogue: stage + read back now, issue the 4*NT stores later
-// (spread over the next tile's MFMA loop, where their issue hides in MFMA gaps).
 typedef int v4i_t __attribute__((ext_vector_type(4)));
-template <int NT>
-struct PendingStores {
-  v4i_t v[NT * 4];
-  __amdgpu_buffer_rsrc_t rs[NT];
-};
-
-template <int NT>
-__device__ __forceinline__ void pending_clear(PendingStores<NT>& ps, half_t* out) {
-#pragma unroll
-  for (int n = 0; n < NT; ++n) ps.rs[n] = __builtin_amdgcn_make_buffer_rsrc(out, (short)0, 0, 0x00020000);
-#pragma unroll
-  for (int j = 0; j < NT * 4; ++j) ps.v[j] = v4i_t{0, 0, 0, 0};
-}
-
-template <int NT>
-__device__ __forceinline__ void epilogue_stage(unsigned char* stage, half_t* __restrict__ out, const ConvShape& s,
-                                               int b, const int (&rows)[NT], int tx0, const floatx16 (&acc)[2][NT],
-                                               const float (&bias)[2][16], int act, PendingStores<NT>& ps) {
-  const int lane = threadIdx.x & 63, h = lane >> 5, col = lane & 31;
-#pragma unroll
-  for (int n = 0; n < NT; ++n) {
-    const int pix = n * 32 + col;
-#pragma unroll
-    for (int m = 0; m < 2; ++m) {
-      half8_t lo, hi;
-#pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        lo[r] = (half_t)act_fn(acc[m][n][r] + bias[m][r], act);
-        hi[r] = (half_t)act_fn(acc[m][n][r + 8] + bias[m][r + 8], act);
-      }
-      const int q = 4 * m + 2 * h;
-      *reinterpret_cast<half8_t*>(stage + pix * 128 + 16 * (q ^ (pix & 7))) = lo;
-      *reinterpret_cast<half8_t*>(stage + pix * 128 + 16 * ((q + 1) ^ (pix & 7))) = hi;
-    }
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-  for (int j = 0; j < NT * 4; ++j) {
-    const int pix = 8 * j + (lane >> 3), c = lane & 7;
-    ps.v[j] = *reinterpret_cast<const v4i_t*>(stage + pix * 128 + 16 * (c ^ (pix & 7)));
-  }
-  const int ncols = min(kTileW, s.W - tx0);
-#pragma unroll
-  for (int n = 0; n < NT; ++n) {
-    const int y = __builtin_amdgcn_readfirstlane(rows[n]);
-    half_t* row = out + (((size_t)b * s.Hp + y + 1) * s.Wp + tx0 + 1) * kWidth;
-    ps.rs[n] = __builtin_amdgcn_make_buffer_rsrc(row, (short)0, y < s.H ? ncols * 128 : 0, 0x00020000);
-  }
-}
-
-template <int NT>
-__device__ __forceinline__ void pending_store(const PendingStores<NT>& ps, int j) {
-  const int lane = threadIdx.x & 63;
-  const int pix = 8 * j + (lane >> 3), c = lane & 7;
-  __builtin_amdgcn_raw_buffer_store_b128(ps.v[j], ps.rs[j >> 2], (pix & 31) * 128 + c * 16, 0, 0);
-}
-
-// End of a pipelined tile: this wave's prefetch DMA (issued before its NSTORES epilogue
-// stores) has landed, all of this wave's LDS reads are done, then the workgroup barrier.
-template <int NSTORES>
-__device__ __forceinline__ void tile_boundary() {
-  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NSTORES) : "memory");
-  __builtin_amdgcn_s_barrier();
-}
 
 // ------------------------------------------------------------------------------------
-// Body layer 64 -> 64 (basic_models.py:16-17,29-33).  LDS: 72 KiB weights + two 42.5 KiB
-// halo buffers = 157 KiB -> one workgroup (4 waves) per CU, persistent over tiles.
-// Software pipeline per tile: issue the global loads of tile t+1 into registers, run
-// tile t's 144 MFMAs/wave from LDS buffer `cur`, store tile t, then write tile t+1 into
-// buffer `cur^1`; one barrier per tile.
+// LDS-DMA halo staging (buffer_load_dword... lds).  The 10 x 34 halo of an 8 x 32 tile
+// is 340 pixels = 43 slots of 8 pixels (1 KiB); lane l of a slot loads 16-B chunk
+// (l&7) ^ swz(pc) of pixel 8g + l/8 into the lane-linear destination, so the LDS image is
+// the XOR-swizzled layout of halo_off() (common.h).  The tile base is in SGPRs and the
+// per-lane offsets of a wave's slots are tile-invariant (computed once per launch).
 // ------------------------------------------------------------------------------------
-
-__global__ __launch_bounds__(256, 1) void conv_body_kernel(const half_t* __restrict__ in,
-                                                            half_t* __restrict__ out,
-                                                            const uint4* __restrict__ wpk,
-                                                            const float* __restrict__ bias,
-                                                            ConvShape s, int act) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  unsigned char* wl = smem;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int h = lane >> 5, col = lane & 31;
-
-  for (int i = tid; i < kBodyWBytes / 16; i += 256) reinterpret_cast<uint4*>(wl)[i] = wpk[i];
-  float bias_r[2][16];
-#pragma unroll
-  for (int m = 0; m < 2; ++m)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) bias_r[m][r] = bias[32 * m + 16 * h + r];
-
-  int t = blockIdx.x;
-  int cur = 0;
-  if (t < s.tiles) {
-    int b, ty0, tx0;
-    decode_tile(t, s, b, ty0, tx0);
-    halo_dma(smem + kBodyWBytes, in, s, b, ty0, tx0);
-  }
-  __syncthreads();                            // drains the DMA (vmcnt(0)) + barrier
-  for (; t < s.tiles; t += gridDim.x) {
-    int b, ty0, tx0;
-    decode_tile(t, s, b, ty0, tx0);
-    const int tn = t + gridDim.x;
-    if (tn < s.tiles) {                       // next tile -> the other buffer, in flight
-      int bn, tyn, txn;
-      decode_tile(tn, s, bn, tyn, txn);
-      if (!(s.ablate & 1)) halo_dma(smem + kBodyWBytes + (cur ^ 1) * kHaloDmaBytes, in, s, bn, tyn, txn);
-    }
-    const unsigned char* hl = smem + kBodyWBytes + cur * kHaloDmaBytes;
-    auto ldA = [&](int ks, int m) {
-      return *reinterpret_cast<const half8_t*>(wl + ((ks * 2 + m) * 64 + lane) * 16);
-    };
-    auto ldB = [&](int ks, int n) {           // this lane's pixel at tap (0,0): (2*wave, col)
-      const int tap = ks >> 2, sub = ks & 3;
-      return *reinterpret_cast<const half8_t*>(
-          hl + halo_off(2 * wave + n + tap / 3, col + tap % 3, 2 * sub + h));
-    };
-
-    // K loop over a 3-slot fragment ring: the LDS reads of step ks+2 are issued while
-    // step ks's MFMAs run, so each read has at least one full step (4 MFMAs, ~128
-    // cycles) to land — at one wave per SIMD nothing else hides LDS latency.
-    floatx16 acc00 = {}, acc01 = {}, acc10 = {}, acc11 = {};
-    half8_t fa[3][2], fb[3][2];
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      fa[q][0] = ldA(q, 0); fa[q][1] = ldA(q, 1);
-      fb[q][0] = ldB(q, 0); fb[q][1] = ldB(q, 1);
-    }
-#pragma unroll
-    for (int ks = 0; ks < kBodyKSteps; ++ks) {
-      const int r = ks % 3;
-      if (ks + 2 < kBodyKSteps) {
-        const int w = (ks + 2) % 3;
-        fa[w][0] = ldA(ks + 2, 0); fa[w][1] = ldA(ks + 2, 1);
-        fb[w][0] = ldB(ks + 2, 0); fb[w][1] = ldB(ks + 2, 1);
-      }
-      // hipcc's scheduler otherwise sinks the reads to just before their consumers
-      __builtin_amdgcn_sched_barrier(0);
-      acc00 = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[r][0], fb[r][0], acc00, 0, 0, 0);
-      acc10 = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[r][1], fb[r][0], acc10, 0, 0, 0);
-      acc01 = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[r][0], fb[r][1], acc01, 0, 0, 0);
-      acc11 = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[r][1], fb[r][1], acc11, 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if (!(s.ablate & 2)) {
-      // every wave is done reading halo buffer `cur`: reuse it as the store staging area
-      // (raw barrier: no vmcnt(0), the next tile's DMA stays in flight)
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      const int rows[2] = {ty0 + 2 * wave, ty0 + 2 * wave + 1};
-      const floatx16 acc[2][2] = {{acc00, acc01}, {acc10, acc11}};
-      epilogue_coalesced<2>(smem + kBodyWBytes + cur * kHaloDmaBytes + wave * 8192, out, s, b, rows, tx0, acc,
-                            bias_r, act);
-      tile_boundary<8>();                     // next tile landed; stores stay in flight
-    } else {
-      if (acc00[0] + acc01[0] + acc10[0] + acc11[0] == -1e30f) out[0] = (half_t)0;   // keeps MFMAs live
-      __syncthreads();
-    }
-    cur ^= 1;
-  }
-}
-
-// ------------------------------------------------------------------------------------
-// Body layer, 8-wave variant: 512 threads = two waves per SIMD, wave w owns output row
-// w of the 8x32 tile (one 32-pixel N-tile) x 64 channels (two M-tiles).  Per K-step
-// 2 weight + 1 activation ds_read_b128 and 2 MFMAs.  The partner wave on the same SIMD
-// issues its MFMAs while this one waits on LDS, runs its epilogue or issues DMA.
-// ------------------------------------------------------------------------------------
-__global__ __launch_bounds__(512, 2) void conv_body8_kernel(const half_t* __restrict__ in,
-                                                             half_t* __restrict__ out,
-                                                             const uint4* __restrict__ wpk,
-                                                             const float* __restrict__ bias,
-                                                             ConvShape s, int act) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  unsigned char* wl = smem;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int h = lane >> 5, col = lane & 31;
-
-  for (int i = tid; i < kBodyWBytes / 16; i += 512) reinterpret_cast<uint4*>(wl)[i] = wpk[i];
-  float bias_r[2][16];
-#pragma unroll
-  for (int m = 0; m < 2; ++m)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) bias_r[m][r] = bias[32 * m + 16 * h + r];
-
-  int t = blockIdx.x;
-  int cur = 0;
-  if (t < s.tiles) {
-    int b, ty0, tx0;
-    decode_tile(t, s, b, ty0, tx0);
-    halo_dma<8>(smem + kBodyWBytes, in, s, b, ty0, tx0);
-  }
-  __syncthreads();
-  PendingStores<1> ps;                        // stores of the previous tile (none yet:
-  pending_clear(ps, out);                     // zero-record descriptor, dropped by hardware)
-  for (; t < s.tiles; t += gridDim.x) {
-    int b, ty0, tx0;
-    decode_tile(t, s, b, ty0, tx0);
-    const int tn = t + gridDim.x;
-    if (tn < s.tiles) {
-      int bn, tyn, txn;
-      decode_tile(tn, s, bn, tyn, txn);
-      if (!(s.ablate & 1)) halo_dma<8>(smem + kBodyWBytes + (cur ^ 1) * kHaloDmaBytes, in, s, bn, tyn, txn);
-    }
-    const unsigned char* hl = smem + kBodyWBytes + cur * kHaloDmaBytes;
-    auto ldA = [&](int ks, int m) {
-      return *reinterpret_cast<const half8_t*>(wl + ((ks * 2 + m) * 64 + lane) * 16);
-    };
-    auto ldB = [&](int ks) {
-      const int tap = ks >> 2, sub = ks & 3;
-      return *reinterpret_cast<const half8_t*>(hl + halo_off(wave + tap / 3, col + tap % 3, 2 * sub + h));
-    };
-    floatx16 acc0 = {}, acc1 = {};
-    half8_t fa0 = ldA(0, 0), fa1 = ldA(0, 1), fb = ldB(0);
-    if (s.ablate & 4) {                       // profiling: memory path only
-#pragma unroll
-      for (int j = 0; j < 4; ++j) pending_store(ps, j);
-      acc0[0] = (float)fa0[0] + (float)fb[0];
-      acc1[0] = (float)fa1[0];
-    } else
-#pragma unroll
-    for (int ks = 0; ks < kBodyKSteps; ++ks) {
-      half8_t na0, na1, nb;
-      if (ks + 1 < kBodyKSteps) { na0 = ldA(ks + 1, 0); na1 = ldA(ks + 1, 1); nb = ldB(ks + 1); }
-      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa0, fb, acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa1, fb, acc1, 0, 0, 0);
-      if (ks + 1 < kBodyKSteps) { fa0 = na0; fa1 = na1; fb = nb; }
-      if ((ks & 7) == 4) {                    // previous tile's stores, one per 8 K-steps
-        __builtin_amdgcn_sched_barrier(0);
-        pending_store(ps, ks >> 3);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-    // every wave is done reading halo buffer `cur`: reuse it as the staging area
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (!(s.ablate & 2)) {
-      const int rows[1] = {ty0 + wave};
-      const floatx16 acc[2][1] = {{acc0}, {acc1}};
-      epilogue_stage<1>(smem + kBodyWBytes + cur * kHaloDmaBytes + wave * 4096, out, s, b, rows, tx0, acc, bias_r,
-                        act, ps);
-    } else if (acc0[0] + acc1[0] == -1e30f) {
-      out[0] = (half_t)0;                     // keeps every MFMA live (rule 17)
-    }
-    tile_boundary<4>();                       // DMA of the next tile landed (4 stores younger)
-    cur ^= 1;
-  }
-#pragma unroll
-  for (int j = 0; j < 4; ++j) pending_store(ps, j);   // last tile's stores
-}
-
-// ------------------------------------------------------------------------------------
-// Body layer, wave-specialised variant (2): 8 waves = 4 compute + 4 memory waves, one of
-// each per SIMD.  Compute waves (0-3) only read LDS and issue MFMAs (2 rows x 64 ch each);
-// memory waves (4-7) move bytes: they read the previous tile's staged outputs from LDS,
-// issue its coalesced stores and the next tile's LDS-DMA, and wait for that DMA — so a
-// store or DMA that stalls at issue never stalls the MFMA stream.  Per tile:
-//   compute: MFMA(t) from buf c   | memory: staged(t-1) from buf c^1 -> regs, DMA(t+1) -> c^1, stores(t-1)
-//   --- barrier B1 ---
-//   compute: stage outputs(t) -> buf c (8 KiB per compute wave)
-//   --- barrier B2 ---
-// Memory wave i re-fills by DMA only LDS it has itself just read (staging region i = DMA
-// slots 8i..8i+7) or that nobody reads (slots 32..42), so no barrier is needed between
-// its reads and the DMA.
-// ------------------------------------------------------------------------------------
-__device__ __forceinline__ void dma_slot(unsigned char* hl, const half_t* __restrict__ base, const ConvShape& s,
-                                         int g) {
-  const int lane = threadIdx.x & 63;
-  const int p = 8 * g + (lane >> 3);
-  const int pl = min(p, kHaloPix - 1);
-  const int pr = pl / kHaloW, pc = pl - pr * kHaloW;
-  const int c = (lane & 7) ^ ((pc >> 1) & 7);
-  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(base + ((size_t)pr * s.Wp + pc) *
-                                                                                       kWidth + c * 8),
-                                   (__attribute__((address_space(3))) void*)(hl + g * 1024), 16, 0, 0);
-}
-
-// DMA slots owned by memory wave mw: 8mw..8mw+7 and 32+3mw .. min(32+3mw+2, 42).
-__device__ __forceinline__ void dma_owned(unsigned char* hl, const half_t* __restrict__ in, const ConvShape& s,
-                                          int b, int ty0, int tx0, int mw) {
-  const half_t* base = in + (((size_t)b * s.Hp + ty0) * s.Wp + tx0) * kWidth;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) dma_slot(hl, base, s, 8 * mw + k);
-#pragma unroll
-  for (int k = 0; k < 3; ++k)
-    if (32 + 3 * mw + k < kDmaSlots) dma_slot(hl, base, s, 32 + 3 * mw + k);
-}
-
-__global__ __launch_bounds__(512, 2) void conv_body_ws_kernel(const half_t* __restrict__ in,
-                                                               half_t* __restrict__ out,
-                                                               const uint4* __restrict__ wpk,
-                                                               const float* __restrict__ bias,
-                                                               ConvShape s, int act) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  unsigned char* wl = smem;
-  unsigned char* hbuf = smem + kBodyWBytes;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const bool is_mem = wave >= 4;
-  const int cw = wave & 3;                    // compute wave index / memory wave index
-  const int h = lane >> 5, col = lane & 31;
-  float* bias_l = reinterpret_cast<float*>(smem + kBodyWBytes + 2 * kHaloDmaBytes);   // 256 B, not registers
-
-  for (int i = tid; i < kBodyWBytes / 16; i += 512) reinterpret_cast<uint4*>(wl)[i] = wpk[i];
-  if (tid < kWidth) bias_l[tid] = bias[tid];
-
-  int t = blockIdx.x;
-  if (is_mem && t < s.tiles) {
-    int b, ty0, tx0;
-    decode_tile(t, s, b, ty0, tx0);
-    dma_owned(hbuf, in, s, b, ty0, tx0, cw);
-  }
-  __syncthreads();                            // vmcnt(0): first tile landed
-  int cur = 0;
-  int pb = 0, pty0 = 0, ptx0 = 0;             // previous tile (its outputs are staged)
-  bool have_prev = false;
-  for (; t < s.tiles; t += gridDim.x) {
-    int b, ty0, tx0;
-    decode_tile(t, s, b, ty0, tx0);
-    floatx16 acc00 = {}, acc01 = {}, acc10 = {}, acc11 = {};
-    if (is_mem) {
-      unsigned char* other = hbuf + (cur ^ 1) * kHaloDmaBytes;
-      v4i_t v[8];
-      if (have_prev) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int pix = 8 * j + (lane >> 3), c = lane & 7;
-          v[j] = *reinterpret_cast<const v4i_t*>(other + cw * 8192 + pix * 128 + 16 * (c ^ (pix & 7)));
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // data in registers before the DMA lands
-      }
-      const int tn = t + gridDim.x;
-      if (tn < s.tiles) {
-        int bn, tyn, txn;
-        decode_tile(tn, s, bn, tyn, txn);
-        dma_owned(other, in, s, bn, tyn, txn, cw);
-      }
-      if (have_prev) {
-        const int ncols = min(kTileW, s.W - ptx0);
-#pragma unroll
-        for (int n = 0; n < 2; ++n) {
-          const int y = pty0 + 2 * cw + n;
-          half_t* row = out + (((size_t)pb * s.Hp + y + 1) * s.Wp + ptx0 + 1) * kWidth;
-          const __amdgpu_buffer_rsrc_t rs =
-              __builtin_amdgcn_make_buffer_rsrc(row, (short)0, y < s.H ? ncols * 128 : 0, 0x00020000);
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const int j = 4 * n + q, pix = 8 * j + (lane >> 3), c = lane & 7;
-            __builtin_amdgcn_raw_buffer_store_b128(v[j], rs, (pix & 31) * 128 + c * 16, 0, 0);
-          }
-        }
-        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");     // the DMA (older than the stores)
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-    } else {
-      const unsigned char* hl = hbuf + cur * kHaloDmaBytes;
-      auto ldA = [&](int ks, int m) {
-        return *reinterpret_cast<const half8_t*>(wl + ((ks * 2 + m) * 64 + lane) * 16);
-      };
-      auto ldB = [&](int ks, int n) {
-        const int tap = ks >> 2, sub = ks & 3;
-        return *reinterpret_cast<const half8_t*>(
-            hl + halo_off(2 * cw + n + tap / 3, col + tap % 3, 2 * sub + h));
-      };
-      half8_t fa[2][2], fb[2][2];             // 2-slot ring: step ks+1 read while ks computes
-      fa[0][0] = ldA(0, 0); fa[0][1] = ldA(0, 1);
-      fb[0][0] = ldB(0, 0); fb[0][1] = ldB(0, 1);
-#pragma unroll
-      for (int ks = 0; ks < kBodyKSteps; ++ks) {
-        const int r = ks & 1;
-        if (ks + 1 < kBodyKSteps) {
-          const int w = r ^ 1;
-          fa[w][0] = ldA(ks + 1, 0); fa[w][1] = ldA(ks + 1, 1);
-          fb[w][0] = ldB(ks + 1, 0); fb[w][1] = ldB(ks + 1, 1);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        acc00 = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[r][0], fb[r][0], acc00, 0, 0, 0);
-        acc10 = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[r][1], fb[r][0], acc10, 0, 0, 0);
-        acc01 = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[r][0], fb[r][1], acc01, 0, 0, 0);
-        acc11 = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[r][1], fb[r][1], acc11, 0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();             // B1: buf cur fully read; DMA(t+1) landed
-    if (!is_mem) {                            // stage tile t's outputs into buf cur
-      unsigned char* stage = hbuf + cur * kHaloDmaBytes + cw * 8192;
-      const floatx16 acc[2][2] = {{acc00, acc01}, {acc10, acc11}};
-#pragma unroll
-      for (int n = 0; n < 2; ++n) {
-        const int pix = n * 32 + col;
-#pragma unroll
-        for (int m = 0; m < 2; ++m) {
-          const float* bl = bias_l + 32 * m + 16 * h;
-          half8_t lo, hi;
-#pragma unroll
-          for (int r = 0; r < 8; ++r) {
-            lo[r] = (half_t)act_fn(acc[m][n][r] + bl[r], act);
-            hi[r] = (half_t)act_fn(acc[m][n][r + 8] + bl[r + 8], act);
-          }
-          const int q = 4 * m + 2 * h;
-          *reinterpret_cast<half8_t*>(stage + pix * 128 + 16 * (q ^ (pix & 7))) = lo;
-          *reinterpret_cast<half8_t*>(stage + pix * 128 + 16 * ((q + 1) ^ (pix & 7))) = hi;
-        }
-      }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();             // B2: tile t staged
-    pb = b; pty0 = ty0; ptx0 = tx0;
-    have_prev = true;
-    cur ^= 1;
-  }
-  if (is_mem && have_prev) {                  // the last tile's outputs
-    const unsigned char* other = hbuf + (cur ^ 1) * kHaloDmaBytes;
-    const int ncols = min(kTileW, s.W - ptx0);
-#pragma unroll
-    for (int n = 0; n < 2; ++n) {
-      const int y = pty0 + 2 * cw + n;
-      half_t* row = out + (((size_t)pb * s.Hp + y + 1) * s.Wp + ptx0 + 1) * kWidth;
-      const __amdgpu_buffer_rsrc_t rs =
-          __builtin_amdgcn_make_buffer_rsrc(row, (short)0, y < s.H ? ncols * 128 : 0, 0x00020000);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int j = 4 * n + q, pix = 8 * j + (lane >> 3), c = lane & 7;
-        const v4i_t v = *reinterpret_cast<const v4i_t*>(other + cw * 8192 + pix * 128 + 16 * (c ^ (pix & 7)));
-        __builtin_amdgcn_raw_buffer_store_b128(v, rs, (pix & 31) * 128 + c * 16, 0, 0);
-      }
-    }
-  }
-}
-
-// ------------------------------------------------------------------------------------
-// Body layer, variant 3: weights in registers + 3-deep halo ring.
-// 8 waves; wave w owns output channels 32m..32m+31 (m = w&1) of tile rows 2(w>>1) and
-// 2(w>>1)+1, and keeps its 36 A-fragments (the whole K extent of its M-tile, 144 VGPRs) in
-// registers for the launch.  The K-loop reads only 2 activation fragments per 2 MFMAs from
-// LDS, and the 72 KiB that held the weights in variants 0-2 now holds a third halo buffer:
-// the DMA runs two tiles ahead.  Outputs go through a wave-private 4 KiB staging area
-// (64-B half pixels, read back 16 pixels x 64 B per instruction) and are stored during the
-// next tile's K-loop, so the only workgroup barrier per tile is the ring hand-over.
-// LDS: 3 x 42.5 KiB halo + 8 x 4 KiB staging + bias = 163584 B.
-// ------------------------------------------------------------------------------------
-constexpr int kV3Halo = kHaloPix * 128;  // 43520: the last DMA slot is issued by half a wave
-constexpr int kV3Stage = 3 * kV3Halo;
-constexpr int kV3Bias = kV3Stage + 8 * 4096;
-constexpr int kV3Lds = kV3Bias + 256;                           // 163584 B
+constexpr int kDmaSlots = (kHaloPix + 7) / 8;                 // 43
+constexpr int kV3Halo = kHaloPix * 128;                        // 43520: slot 42 is issued by half a wave
 
 template <int NW>
 __device__ __forceinline__ int dma_count(int wave) {           // slots issued by `wave`
   return (kDmaSlots - wave + NW - 1) / NW;
 }
 
-// Halo DMA through a buffer descriptor: the tile base lives in SGPRs and the per-lane
-// byte offsets of this wave's slots are tile-invariant (computed once per launch), so an
-// issue costs one VGPR per slot instead of a 64-bit address.
 // UNIFORM: every wave issues kSlots (the extra slots re-read pixel 339 into padding past
 // the halo), so the issue has no control flow and the compiler's own vmcnt accounting for
 // loads issued before it stays exact; the buffer must then hold NW * kSlots KiB.
@@ -655,7 +89,8 @@ struct RingDma {                                               // one wave's sha
                                         int wave) const {
     int b, ty0, tx0;
     decode_tile(t, s, b, ty0, tx0);
-    const half_t* base = in + (((size_t)b * s.Hp + ty0) * s.Wp + tx0) * kWidth;
+    // halo origin: image pixel (ty0 - 1, tx0 - 1) = padded (ty0 + pad - 1, tx0 + pad - 1)
+    const half_t* base = in + (((size_t)b * s.Hp + ty0 + s.pad - 1) * s.Wp + tx0 + s.pad - 1) * kWidth;
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, 0x7fffffff, 0x00020000);
     const int lane = threadIdx.x & 63;
@@ -669,41 +104,25 @@ struct RingDma {                                               // one wave's sha
   }
 };
 
-// Channel-plane halo image (variant 3 PLANES): chunk c (channels 8c..8c+7) of halo pixel p
-// at c*5440 + 16p.  A 16-lane ds_read_b128 group over consecutive pixels is then 256
-// contiguous bytes (conflict-free without a swizzle) and every fragment address is one
-// per-lane base plus an immediate.  Wave w DMAs plane w: 6 instructions of 64 pixels
-// (the last one 20), each lane one 16-B chunk; the 8 waves read the 8 chunks of the same
-// 128-B pixel lines together, so the lines are fetched from L2 once.
-constexpr int kPlaneBytes = kHaloPix * 16;                     // 5440
-struct PlaneDma {
-  unsigned off[6];
-  __device__ __forceinline__ void init(const ConvShape& s, int wave) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int j = 0; j < 6; ++j) {
-      const int pl = min(64 * j + lane, kHaloPix - 1);
-      const int pr = pl / kHaloW, pc = pl - pr * kHaloW;
-      off[j] = (unsigned)(((pr * s.Wp + pc) * kWidth + wave * 8) * 2);
-    }
-  }
-  __device__ __forceinline__ void issue(unsigned char* hl, const half_t* __restrict__ in, const ConvShape& s, int t,
-                                        int wave) const {
-    int b, ty0, tx0;
-    decode_tile(t, s, b, ty0, tx0);
-    const half_t* base = in + (((size_t)b * s.Hp + ty0) * s.Wp + tx0) * kWidth;
-    const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, 0x7fffffff, 0x00020000);
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int j = 0; j < 6; ++j)
-      if (j < 5 || lane < kHaloPix - 320)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            rs, (__attribute__((address_space(3))) void*)(hl + wave * kPlaneBytes + 1024 * j), 16, off[j], 0, 0, 0);
-  }
-};
+// ------------------------------------------------------------------------------------
+// Body layer (one per launch): weights in registers + 3-deep halo ring.
+// 8 waves; wave w owns output channels 32m..32m+31 (m = w&1) of tile rows 2(w>>1) and
+// 2(w>>1)+1, and keeps its 36 A-fragments (the whole K extent of its M-tile, 144 VGPRs) in
+// registers for the launch, so the K-loop reads only 2 activation fragments per 2 MFMAs
+// from LDS and the LDS holds three halo buffers: the DMA runs two tiles ahead.  Outputs go
+// through a wave-private 4 KiB staging area (64-B half pixels, read back 16 pixels x 64 B
+// per instruction) and are stored during the next tile's K-loop (range-checked buffer
+// stores), so the only workgroup barrier per tile is the ring hand-over, after a counted
+// vmcnt that waits for the next tile's DMA only.
+// LDS: 3 x 42.5 KiB halo + 8 x 4 KiB staging + bias = 163584 B.
+// (Round-1 alternatives measured slower and removed: weights in LDS with 4 or 8 waves,
+// warp-specialised DMA waves, one wave per SIMD holding the whole layer, a channel-plane
+// halo; DESIGN.md.)
+// ------------------------------------------------------------------------------------
+constexpr int kV3Stage = 3 * kV3Halo;
+constexpr int kV3Bias = kV3Stage + 8 * 4096;
+constexpr int kV3Lds = kV3Bias + 256;                           // 163584 B
 
-template <bool PLANES, int NFRAG>
 __global__ __launch_bounds__(512, 2) void conv_body_v3_kernel(const half_t* __restrict__ in,
                                                                half_t* __restrict__ out,
                                                                const uint4* __restrict__ wpk,
@@ -725,12 +144,12 @@ __global__ __launch_bounds__(512, 2) void conv_body_v3_kernel(const half_t* __re
                                                ((ks * 2 + m) * 64 + lane) * 16);
 
   auto buf = [&](int i) { return smem + i * kV3Halo; };
-  typename std::conditional<PLANES, PlaneDma, RingDma<8>>::type dma;
+  RingDma<8> dma;
   dma.init(s, wave);
   auto issue_dma = [&](int tt, int bi) {      // clamped: always the same instruction count
     dma.issue(buf(bi), in, s, tt < s.tiles ? tt : s.tiles - 1, wave);
   };
-  const int ndma = PLANES ? 6 : dma_count<8>(wave);
+  const int ndma = dma_count<8>(wave);
 
   int t = blockIdx.x;
   if (t < s.tiles) {
@@ -758,33 +177,27 @@ __global__ __launch_bounds__(512, 2) void conv_body_v3_kernel(const half_t* __re
     const int nxt2 = cur >= 1 ? cur - 1 : 2;  // (cur + 2) % 3
     issue_dma(t + 2 * gridDim.x, nxt2);
     const unsigned char* hl = buf(cur);
-    // PLANES: one per-lane base, every tap / chunk offset an instruction immediate
-    const unsigned char* pb = hl + h * kPlaneBytes + (2 * rp * kHaloW + col) * 16;
     auto ldB = [&](int ks, int n) {
       const int tap = ks >> 2, sub = ks & 3;
-      if (PLANES)
-        return *reinterpret_cast<const half8_t*>(pb + 2 * sub * kPlaneBytes +
-                                                 ((n + tap / 3) * kHaloW + tap % 3) * 16);
       return *reinterpret_cast<const half8_t*>(
           hl + halo_off(2 * rp + n + tap / 3, col + tap % 3, 2 * sub + h));
     };
     floatx16 acc0 = {}, acc1 = {};
-    half8_t fb[NFRAG][2];
+    half8_t fb[2][2];
     v4i_t sv;
 #pragma unroll
-    for (int k = 0; k < NFRAG - 1; ++k) { fb[k][0] = ldB(k, 0); fb[k][1] = ldB(k, 1); }
+    for (int k = 0; k < 1; ++k) { fb[k][0] = ldB(k, 0); fb[k][1] = ldB(k, 1); }
 #pragma unroll
     for (int ks = 0; ks < kBodyKSteps; ++ks) {
-      const int r = ks % NFRAG;
+      const int r = ks & 1;
       if ((ks & 7) == 2) {                    // previous tile's stores, one per 8 K-steps
         __builtin_amdgcn_sched_barrier(0);
         sv = stage_read(ks >> 3);
         __builtin_amdgcn_sched_barrier(0);
       }
-      if (ks + NFRAG - 1 < kBodyKSteps) {
-        const int kn = ks + NFRAG - 1;
-        fb[kn % NFRAG][0] = ldB(kn, 0);
-        fb[kn % NFRAG][1] = ldB(kn, 1);
+      if (ks + 1 < kBodyKSteps) {
+        fb[r ^ 1][0] = ldB(ks + 1, 0);
+        fb[r ^ 1][1] = ldB(ks + 1, 1);
       }
       acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(wA[ks], fb[r][0], acc0, 0, 0, 0);
       acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(wA[ks], fb[r][1], acc1, 0, 0, 0);
@@ -793,7 +206,6 @@ __global__ __launch_bounds__(512, 2) void conv_body_v3_kernel(const half_t* __re
         stage_store(ks >> 3, sv);
         __builtin_amdgcn_sched_barrier(0);
       }
-      if (NFRAG > 2) __builtin_amdgcn_sched_barrier(0);   // keep the reads NFRAG-1 steps ahead
     }
     {                                         // bias + activation -> fp16 -> staging (wave-private)
       const float* bl = bias_l + 32 * m + 16 * h;
@@ -815,7 +227,7 @@ __global__ __launch_bounds__(512, 2) void conv_body_v3_kernel(const half_t* __re
 #pragma unroll
       for (int n = 0; n < 2; ++n) {
         const int y = ty0 + 2 * rp + n;
-        half_t* row = out + (((size_t)b * s.Hp + y + 1) * s.Wp + tx0 + 1) * kWidth;
+        half_t* row = out + (((size_t)b * s.Hp + y + s.pad) * s.Wp + tx0 + s.pad) * kWidth;
         rs[n] = __builtin_amdgcn_make_buffer_rsrc(row, (short)0, y < s.H ? ncols * 128 : 0, 0x00020000);
       }
     }
@@ -827,139 +239,245 @@ __global__ __launch_bounds__(512, 2) void conv_body_v3_kernel(const half_t* __re
   }
 #pragma unroll
   for (int j = 0; j < 4; ++j) stage_store(j, stage_read(j));
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA may land after the workgroup ends
 }
 
-// ------------------------------------------------------------------------------------
-// Body layer, variant 4: one wave per SIMD holding the WHOLE layer's weights.
-// 4 waves; wave w computes all 64 output channels of tile rows 2w, 2w+1.  Its 72
-// A-fragments (288 registers) stay resident for the launch, so every activation fragment
-// read from LDS feeds 2 MFMAs (half the LDS reads of variant 3 per MFMA), and the fragment
-// ring runs two K-steps (8 MFMAs) ahead with counted lgkmcnt waits.  Staging is
-// wave-private (8 KiB: 64 whole 128-B pixels) and its 8 full-line stores per wave are
-// issued during the next tile's K-loop.  Same LDS map as variant 3 (3-deep halo ring).
-// ------------------------------------------------------------------------------------
-constexpr int kV4Stage = 3 * kV3Halo;
-constexpr int kV4Bias = kV4Stage + 4 * 8192;
-constexpr int kV4Lds = kV4Bias + 256;                           // 163584 B
 
-__global__ __launch_bounds__(256, 1) void conv_body_v4_kernel(const half_t* __restrict__ in,
-                                                               half_t* __restrict__ out,
-                                                               const uint4* __restrict__ wpk,
-                                                               const float* __restrict__ bias,
-                                                               ConvShape s, int act) {
+// ------------------------------------------------------------------------------------
+// Two body layers per launch (l+1 and l+2 of basic_models.py:29-33): the intermediate
+// activation never leaves LDS, so each pair of layers reads and writes the fp16 image
+// once (half the HBM traffic of two one-layer launches) for 25 % more MFMA work.
+//
+// Tile: 8 x 16 output pixels.  Stage 1 computes layer l+1 on the 10 x 18 region around
+// the tile (180 pixels = 6 N-tiles of 32, zero outside the image = layer l+2's padding)
+// from the 12 x 20 input halo; stage 2 computes layer l+2 on the 8 x 16 tile (4 N-tiles
+// of 2 rows x 16) from that intermediate.
+//
+// 8 waves, 2 per SIMD.  Waves 0-3 run stage 1 and hold layer l+1's weights for M-tile
+// m = w&1 (144 VGPRs); waves 4-7 run stage 2 with layer l+2's weights: every SIMD carries
+// one wave of each stage.  The stages are software-pipelined over the CU's tiles: in step
+// k stage 1 builds tile k's intermediate while stage 2 finishes tile k-1 from the other
+// intermediate buffer, and stage-1 waves stream the 12 x 20 halo of tile k+2 into a 3-deep
+// LDS-DMA ring (8 uniform 1-KiB slots per wave).  One workgroup barrier per step.
+// Stage-2 outputs go through wave-private staging and are stored during the next step.
+// LDS: 3 x 32 KiB input ring + 2 x 22.5 KiB intermediate + 4 x 4 KiB staging + bias.
+// ------------------------------------------------------------------------------------
+constexpr int kB2TH = 8, kB2TW = 16;                        // output tile
+constexpr int kB2IW = kB2TW + 4, kB2IH = kB2TH + 4;         // input halo 12 x 20
+constexpr int kB2MW = kB2TW + 2, kB2MH = kB2TH + 2;         // intermediate 10 x 18
+constexpr int kB2InPix = kB2IW * kB2IH;                     // 240
+constexpr int kB2MidPix = kB2MW * kB2MH;                    // 180
+constexpr int kB2InBytes = 32 * 1024;                       // 32 uniform DMA slots (30 used)
+constexpr int kB2MidBytes = kB2MidPix * 128;                // 23040
+constexpr int kB2Mid = 3 * kB2InBytes;
+constexpr int kB2Stage = kB2Mid + 2 * kB2MidBytes;
+constexpr int kB2Bias = kB2Stage + 4 * 4096;
+constexpr int kB2Lds = kB2Bias + 2 * 64 * 4;                // 161280 B
+
+// XOR-swizzled pixel-major LDS image of width `w` (as halo_off, common.h)
+__device__ __forceinline__ int img_off(int pr, int pc, int w, int chunk) {
+  return (pr * w + pc) * 128 + 16 * (chunk ^ ((pc >> 1) & 7));
+}
+
+__device__ __forceinline__ void decode_tile2(int t, const ConvShape& s, int& b, int& ty0, int& tx0) {
+  const int tx = (s.W + kB2TW - 1) / kB2TW, ty = (s.H + kB2TH - 1) / kB2TH;
+  const int per_img = tx * ty;
+  b = t / per_img;
+  const int r = t - b * per_img;
+  const int yy = r / tx;
+  ty0 = yy * kB2TH;
+  tx0 = (r - yy * tx) * kB2TW;
+}
+
+__global__ __launch_bounds__(512, 2) void conv_body2_kernel(const half_t* __restrict__ in,
+                                                             half_t* __restrict__ out,
+                                                             const uint4* __restrict__ w1,
+                                                             const float* __restrict__ b1,
+                                                             const uint4* __restrict__ w2,
+                                                             const float* __restrict__ b2,
+                                                             ConvShape s, int tiles, int act) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  float* bias_l = reinterpret_cast<float*>(smem + kV4Bias);
+  float* bias_l = reinterpret_cast<float*>(smem + kB2Bias);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool st1 = wave < 4;
+  const int m = wave & 1, part = (wave >> 1) & 1;
   const int h = lane >> 5, col = lane & 31;
-  unsigned char* stg = smem + kV4Stage + wave * 8192;
-  if (tid < kWidth) bias_l[tid] = bias[tid];
+  if (tid < kWidth) bias_l[tid] = b1[tid];
+  else if (tid < 2 * kWidth) bias_l[tid] = b2[tid - kWidth];
 
-  half8_t wA[kBodyKSteps][2];                 // the layer's weights, resident for the launch
+  half8_t wA[kBodyKSteps];                    // this wave's layer's weights, M-tile m
+  {
+    const unsigned char* wsrc = reinterpret_cast<const unsigned char*>(st1 ? w1 : w2);
 #pragma unroll
-  for (int ks = 0; ks < kBodyKSteps; ++ks)
-#pragma unroll
-    for (int m = 0; m < 2; ++m)
-      wA[ks][m] = *reinterpret_cast<const half8_t*>(reinterpret_cast<const unsigned char*>(wpk) +
-                                                    ((ks * 2 + m) * 64 + lane) * 16);
+    for (int ks = 0; ks < kBodyKSteps; ++ks)
+      wA[ks] = *reinterpret_cast<const half8_t*>(wsrc + ((ks * 2 + m) * 64 + lane) * 16);
+  }
+  auto inbuf = [&](int i) { return smem + i * kB2InBytes; };
+  auto midbuf = [&](int i) { return smem + kB2Mid + i * kB2MidBytes; };
 
-  auto buf = [&](int i) { return smem + i * kV3Halo; };
-  RingDma<4> dma;
-  dma.init(s, wave);
-  auto issue_dma = [&](int tt, int bi) {      // clamped: always the same instruction count
-    dma.issue(buf(bi), in, s, tt < s.tiles ? tt : s.tiles - 1, wave);
+  // stage-1 waves: 8 DMA slots each (slot g = wave + 4j).  The per-lane offsets are
+  // recomputed at each issue (a few VALU per slot) rather than held in 8 VGPRs.
+  auto dma_off = [&](int j, int ln) {
+    const int p = 8 * (4 * j + (wave & 3)) + (ln >> 3);
+    const int pl = min(p, kB2InPix - 1);
+    const int pr = pl / kB2IW, pc = pl - pr * kB2IW;
+    const int c = (ln & 7) ^ ((pc >> 1) & 7);
+    return (unsigned)(((pr * s.Wp + pc) * kWidth + c * 8) * 2);
   };
-  const bool full = dma_count<4>(wave) == 11; // waves 0-2 issue 11 slots, wave 3 issues 10
+  auto issue_dma = [&](int tt, int bi) {      // stage-1 waves only; clamped tile: fixed op count
+    int b, ty0, tx0;
+    decode_tile2(tt < tiles ? tt : tiles - 1, s, b, ty0, tx0);
+    // input halo origin: image (ty0 - 2, tx0 - 2) = padded (ty0 + pad - 2, tx0 + pad - 2)
+    const half_t* base = in + (((size_t)b * s.Hp + ty0 + s.pad - 2) * s.Wp + tx0 + s.pad - 2) * kWidth;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, 0x7fffffff, 0x00020000);
+    unsigned char* hl = inbuf(bi);
+    int ln = lane;
+    asm volatile("" : "+v"(ln));              // opaque: keeps the offsets from being hoisted (and spilled)
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rs, (__attribute__((address_space(3))) void*)(hl + (4 * j + (wave & 3)) * 1024), 16, dma_off(j, ln), 0, 0, 0);
+  };
 
-  int t = blockIdx.x;
-  if (t < s.tiles) {
-    issue_dma(t, 0);
-    issue_dma(t + gridDim.x, 1);
-    if (full) asm volatile("s_waitcnt vmcnt(11)" ::: "memory");     // tile t landed
-    else asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+  const int t0 = blockIdx.x;
+  const int nt = t0 < tiles ? (tiles - 1 - t0) / (int)gridDim.x + 1 : 0;   // tiles of this workgroup
+  if (st1 && nt > 0) {
+    issue_dma(t0, 0);
+    issue_dma(t0 + gridDim.x, 1);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");                          // tile 0's halo landed
   }
   __syncthreads();
-  __amdgpu_buffer_rsrc_t rs[2];
-  rs[0] = rs[1] = __builtin_amdgcn_make_buffer_rsrc(out, (short)0, 0, 0x00020000);   // first tile: dropped
-  auto stage_read = [&](int j) {              // 8 whole pixels per instruction
-    const int pix = 8 * j + (lane >> 3), c = lane & 7;
-    return *reinterpret_cast<const v4i_t*>(stg + pix * 128 + 16 * (c ^ (pix & 7)));
+
+  // stage-2 deferred stores (previous step's tile): 16 pixels x 64 B (channel half m) each
+  unsigned char* stg = smem + kB2Stage + (wave & 3) * 4096;
+  __amdgpu_buffer_rsrc_t rs[4];
+  rs[0] = rs[1] = rs[2] = rs[3] = __builtin_amdgcn_make_buffer_rsrc(out, (short)0, 0, 0x00020000);
+  auto stage_read = [&](int j) {              // j = output row (of this wave's 4) ; 16 px x 4 chunks
+    const int pix = 16 * j + (lane >> 2), c = lane & 3;
+    return *reinterpret_cast<const v4i_t*>(stg + pix * 64 + 16 * (c ^ ((pix >> 1) & 3)));
   };
   auto stage_store = [&](int j, const v4i_t& v) {
-    const int pix = 8 * j + (lane >> 3), c = lane & 7;
-    __builtin_amdgcn_raw_buffer_store_b128(v, rs[j >> 2], (pix & 31) * 128 + 16 * c, 0, 0);
+    const int pix = 16 * j + (lane >> 2), c = lane & 3;
+    __builtin_amdgcn_raw_buffer_store_b128(v, rs[j], (pix & 15) * 128 + 64 * m + 16 * c, 0, 0);
   };
-  int cur = 0;
-  for (; t < s.tiles; t += gridDim.x) {
-    int b, ty0, tx0;
-    decode_tile(t, s, b, ty0, tx0);
-    const int nxt2 = cur >= 1 ? cur - 1 : 2;  // (cur + 2) % 3
-    issue_dma(t + 2 * gridDim.x, nxt2);
-    const unsigned char* hl = buf(cur);
-    auto ldB = [&](int ks, int n) {
-      const int tap = ks >> 2, sub = ks & 3;
-      return *reinterpret_cast<const half8_t*>(
-          hl + halo_off(2 * wave + n + tap / 3, col + tap % 3, 2 * sub + h));
-    };
-    floatx16 acc[2][2] = {};
-    half8_t fb[3][2];
-    v4i_t sv;
-    fb[0][0] = ldB(0, 0); fb[0][1] = ldB(0, 1);
-    fb[1][0] = ldB(1, 0); fb[1][1] = ldB(1, 1);
+
+  for (int k = 0; k <= nt; ++k) {
+    if (st1) {
+      if (k < nt) {
+        // ---------------- stage 1: layer l+1 on the 10 x 18 region of tile k ----------------
+        int b, ty0, tx0;
+        decode_tile2(t0 + k * gridDim.x, s, b, ty0, tx0);
+        issue_dma(t0 + (k + 2) * gridDim.x, (k + 2) % 3);
+        const unsigned char* hl = inbuf(k % 3);
+        unsigned char* mid = midbuf(k & 1);
+        const float* bl = bias_l + 32 * m + 16 * h;
+#pragma unroll 1
+        for (int i = 0; i < 3; ++i) {
+          const int n = 32 * (part + 2 * i) + col;           // intermediate pixel (flattened 10 x 18)
+          const int nc = min(n, kB2MidPix - 1);
+          const int r1 = nc / kB2MW, c1 = nc - r1 * kB2MW;
+          auto ldB = [&](int ks) {
+            const int tap = ks >> 2, sub = ks & 3;
+            return *reinterpret_cast<const half8_t*>(
+                hl + img_off(r1 + tap / 3, c1 + tap % 3, kB2IW, 2 * sub + h));
+          };
+          floatx16 acc = {};
+          half8_t fb[4];
+          fb[0] = ldB(0); fb[1] = ldB(1); fb[2] = ldB(2);
 #pragma unroll
-    for (int ks = 0; ks < kBodyKSteps; ++ks) {
-      const int r = ks % 3;
-      if ((ks & 3) == 1 && ks < 32) {         // previous tile's stores: 8, one per 4 K-steps
-        __builtin_amdgcn_sched_barrier(0);
-        sv = stage_read(ks >> 2);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      if (ks + 2 < kBodyKSteps) { fb[(ks + 2) % 3][0] = ldB(ks + 2, 0); fb[(ks + 2) % 3][1] = ldB(ks + 2, 1); }
-#pragma unroll
-      for (int n = 0; n < 2; ++n)
-#pragma unroll
-        for (int m = 0; m < 2; ++m)
-          acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wA[ks][m], fb[r][n], acc[m][n], 0, 0, 0);
-      if ((ks & 3) == 3 && ks < 32) {
-        __builtin_amdgcn_sched_barrier(0);
-        stage_store(ks >> 2, sv);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-    {                                         // bias + activation -> fp16 -> staging (wave-private)
-#pragma unroll
-      for (int n = 0; n < 2; ++n) {
-        const int pix = n * 32 + col;
-#pragma unroll
-        for (int m = 0; m < 2; ++m) {
-          const float* bl = bias_l + 32 * m + 16 * h;
+          for (int ks = 0; ks < kBodyKSteps; ++ks) {
+            if (ks + 3 < kBodyKSteps) fb[(ks + 3) & 3] = ldB(ks + 3);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wA[ks], fb[ks & 3], acc, 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);               // keep the reads 3 steps ahead
+          }
+          // bias + act -> fp16 -> intermediate; zero outside the image (layer l+2's padding)
+          const int y = ty0 - 1 + r1, x = tx0 - 1 + c1;
+          const bool inside = y >= 0 && y < s.H && x >= 0 && x < s.W;
           half8_t lo, hi;
 #pragma unroll
           for (int r = 0; r < 8; ++r) {
-            lo[r] = (half_t)act_fn(acc[m][n][r] + bl[r], act);
-            hi[r] = (half_t)act_fn(acc[m][n][r + 8] + bl[r + 8], act);
+            lo[r] = inside ? (half_t)act_fn(acc[r] + bl[r], act) : (half_t)0.f;
+            hi[r] = inside ? (half_t)act_fn(acc[r + 8] + bl[r + 8], act) : (half_t)0.f;
           }
-          const int q = 4 * m + 2 * h;
-          *reinterpret_cast<half8_t*>(stg + pix * 128 + 16 * (q ^ (pix & 7))) = lo;
-          *reinterpret_cast<half8_t*>(stg + pix * 128 + 16 * ((q + 1) ^ (pix & 7))) = hi;
+          if (n < kB2MidPix) {
+            const int q = 4 * m + 2 * h;
+            *reinterpret_cast<half8_t*>(mid + img_off(r1, c1, kB2MW, q)) = lo;
+            *reinterpret_cast<half8_t*>(mid + img_off(r1, c1, kB2MW, q + 1)) = hi;
+          }
         }
       }
-      const int ncols = min(kTileW, s.W - tx0);
+      // halo of tile k+1 landed: only the 8 DMA ops of tile k+2 are younger
+      asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
+    } else {
+      if (k >= 1) {
+        // ---------------- stage 2: layer l+2 on tile k-1 ----------------
+        int b, ty0, tx0;
+        decode_tile2(t0 + (k - 1) * gridDim.x, s, b, ty0, tx0);
+        const unsigned char* mid = midbuf((k - 1) & 1);
+        const int orow = 4 * part + 2 * 0;          // this wave's output rows 4part .. 4part+3
+        auto ldB = [&](int ks, int nn) {            // N-tile nn (0,1): rows orow + 2nn + col/16
+          const int tap = ks >> 2, sub = ks & 3;
+          const int rr = orow + 2 * nn + (col >> 4), cc = col & 15;
+          return *reinterpret_cast<const half8_t*>(
+              mid + img_off(rr + tap / 3, cc + tap % 3, kB2MW, 2 * sub + h));
+        };
+        floatx16 acc0 = {}, acc1 = {};
+        half8_t fb[3][2];
+        v4i_t sv;
+        fb[0][0] = ldB(0, 0); fb[0][1] = ldB(0, 1);
+        fb[1][0] = ldB(1, 0); fb[1][1] = ldB(1, 1);
 #pragma unroll
-      for (int n = 0; n < 2; ++n) {
-        const int y = ty0 + 2 * wave + n;
-        half_t* row = out + (((size_t)b * s.Hp + y + 1) * s.Wp + tx0 + 1) * kWidth;
-        rs[n] = __builtin_amdgcn_make_buffer_rsrc(row, (short)0, y < s.H ? ncols * 128 : 0, 0x00020000);
+        for (int ks = 0; ks < kBodyKSteps; ++ks) {
+          if ((ks & 7) == 1 && ks < 32) {           // previous step's stores, one per 8 K-steps
+            __builtin_amdgcn_sched_barrier(0);
+            sv = stage_read(ks >> 3);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+          if (ks + 2 < kBodyKSteps) { fb[(ks + 2) % 3][0] = ldB(ks + 2, 0); fb[(ks + 2) % 3][1] = ldB(ks + 2, 1); }
+          acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(wA[ks], fb[ks % 3][0], acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(wA[ks], fb[ks % 3][1], acc1, 0, 0, 0);
+          if ((ks & 7) == 4 && ks < 32) {
+            __builtin_amdgcn_sched_barrier(0);
+            stage_store(ks >> 3, sv);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        // bias + act -> fp16 -> wave-private staging [64 px][64 B], px = 16 * row + col
+        const float* bl = bias_l + kWidth + 32 * m + 16 * h;
+#pragma unroll
+        for (int nn = 0; nn < 2; ++nn) {
+          const floatx16& a = nn == 0 ? acc0 : acc1;
+          const int pix = 32 * nn + col;            // rows 2nn + col/16 of this wave, col%16
+          const int sw = (pix >> 1) & 3;
+          half8_t lo, hi;
+#pragma unroll
+          for (int r = 0; r < 8; ++r) {
+            lo[r] = (half_t)act_fn(a[r] + bl[r], act);
+            hi[r] = (half_t)act_fn(a[r + 8] + bl[r + 8], act);
+          }
+          *reinterpret_cast<half8_t*>(stg + pix * 64 + 16 * ((2 * h) ^ sw)) = lo;
+          *reinterpret_cast<half8_t*>(stg + pix * 64 + 16 * ((2 * h + 1) ^ sw)) = hi;
+        }
+        const int ncols = min(kB2TW, s.W - tx0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int y = ty0 + orow + j;
+          half_t* row = out + (((size_t)b * s.Hp + y + s.pad) * s.Wp + tx0 + s.pad) * kWidth;
+          rs[j] = __builtin_amdgcn_make_buffer_rsrc(row, (short)0, y < s.H ? ncols * 128 : 0, 0x00020000);
+        }
       }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
-    // tile t+1 landed: only the DMA of t+2 and this tile's 8 stores are younger
-    if (full) asm volatile("s_waitcnt vmcnt(19) lgkmcnt(0)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(18) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    cur = cur == 2 ? 0 : cur + 1;
   }
+  if (!st1) {
 #pragma unroll
-  for (int j = 0; j < 8; ++j) stage_store(j, stage_read(j));
+    for (int j = 0; j < 4; ++j) stage_store(j, stage_read(j));
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA may land after the workgroup ends
 }
 
 // ------------------------------------------------------------------------------------
@@ -986,10 +504,11 @@ __global__ __launch_bounds__(256) void conv_head_kernel(const half_t* __restrict
     int b, ty0, tx0;
     decode_tile(t, s, b, ty0, tx0);
     __syncthreads();
-    const uint2* base = reinterpret_cast<const uint2*>(in4) + ((size_t)b * s.Hp + ty0) * s.Wp + tx0;
+    const int Wp4 = s.W + 2;                  // u16: NHWC4 with a one-pixel zero border
+    const uint2* base = reinterpret_cast<const uint2*>(in4) + ((size_t)b * (s.H + 2) + ty0) * Wp4 + tx0;
     for (int p = tid; p < kHaloPix; p += 256) {
       const int pr = p / kHaloW, pc = p - pr * kHaloW;
-      hl[p] = base[(size_t)pr * s.Wp + pc];
+      hl[p] = base[(size_t)pr * Wp4 + pc];
     }
     __syncthreads();
     floatx16 acc00 = {}, acc01 = {}, acc10 = {}, acc11 = {};
@@ -1140,6 +659,7 @@ __global__ __launch_bounds__(256, 1) void conv_tail_kernel(const half_t* __restr
     __builtin_amdgcn_s_barrier();
     cur = cur == 2 ? 0 : cur + 1;
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA may land after the workgroup ends
 }
 
 // ------------------------------------------------------------------------------------
@@ -1202,34 +722,22 @@ void pack_tail_weights(const float* W, int C, uint16_t* out) {
 // ------------------------------------------------------------------------------------
 ConvShape make_conv_shape(int B, int H, int W) {
   ConvShape s;
-  s.B = B; s.H = H; s.W = W; s.Hp = H + 2; s.Wp = W + 2;
+  s.B = B; s.H = H; s.W = W;
+  s.pad = kActPad;
+  s.Hp = H + 2 * kActPad; s.Wp = W + 2 * kActPad;
   s.tiles_x = (W + kTileW - 1) / kTileW;
   s.tiles_y = (H + kTileH - 1) / kTileH;
   s.tiles = B * s.tiles_x * s.tiles_y;
-  s.ablate = 0;
-  s.trash = nullptr;
   return s;
 }
 
-constexpr int kBodyLds = kBodyWBytes + 2 * kHaloDmaBytes + 256;   // 162048 B of the 160 KiB (+ bias)
-
 hipError_t conv_kernels_init() {
-  hipError_t e = hipFuncSetAttribute((const void*)conv_body_kernel,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, kBodyLds);
+  hipError_t e = hipFuncSetAttribute((const void*)conv_body_v3_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     kV3Lds);
   if (e != hipSuccess) return e;
-  e = hipFuncSetAttribute((const void*)conv_body8_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, kBodyLds);
+  e = hipFuncSetAttribute((const void*)conv_body2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, kB2Lds);
   if (e != hipSuccess) return e;
-  e = hipFuncSetAttribute((const void*)conv_body_ws_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, kBodyLds);
-  if (e != hipSuccess) return e;
-  for (const void* k : {(const void*)conv_body_v3_kernel<false, 2>, (const void*)conv_body_v3_kernel<true, 2>,
-                        (const void*)conv_body_v3_kernel<true, 3>}) {
-    e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kV3Lds);
-    if (e != hipSuccess) return e;
-  }
-  e = hipFuncSetAttribute((const void*)conv_body_v4_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, kV4Lds);
-  if (e != hipSuccess) return e;
-  return hipFuncSetAttribute((const void*)conv_tail_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             kTailLds);
+  return hipFuncSetAttribute((const void*)conv_tail_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, kTailLds);
 }
 
 void launch_conv_head(const half_t* in4, half_t* out, const void* w, const float* bias, const ConvShape& s,
@@ -1239,29 +747,18 @@ void launch_conv_head(const half_t* in4, half_t* out, const void* w, const float
 }
 
 void launch_conv_body(const half_t* in, half_t* out, const void* w, const float* bias, const ConvShape& s,
-                      int act, int num_cus, int variant, hipStream_t st) {
+                      int act, int num_cus, int /*variant*/, hipStream_t st) {
   const int grid = s.tiles < num_cus ? s.tiles : num_cus;
-  if (variant == 4)
-    hipLaunchKernelGGL(conv_body_v4_kernel, dim3(grid), dim3(256), kV4Lds, st, in, out, (const uint4*)w, bias,
-                       s, act);
-  else if (variant == 5)
-    hipLaunchKernelGGL((conv_body_v3_kernel<true, 2>), dim3(grid), dim3(512), kV3Lds, st, in, out, (const uint4*)w,
-                       bias, s, act);
-  else if (variant == 6)
-    hipLaunchKernelGGL((conv_body_v3_kernel<true, 3>), dim3(grid), dim3(512), kV3Lds, st, in, out, (const uint4*)w,
-                       bias, s, act);
-  else if (variant == 3)
-    hipLaunchKernelGGL((conv_body_v3_kernel<false, 2>), dim3(grid), dim3(512), kV3Lds, st, in, out, (const uint4*)w, bias,
-                       s, act);
-  else if (variant == 2)
-    hipLaunchKernelGGL(conv_body_ws_kernel, dim3(grid), dim3(512), kBodyLds, st, in, out, (const uint4*)w, bias,
-                       s, act);
-  else if (variant == 1)
-    hipLaunchKernelGGL(conv_body8_kernel, dim3(grid), dim3(512), kBodyLds, st, in, out, (const uint4*)w, bias,
-                       s, act);
-  else
-    hipLaunchKernelGGL(conv_body_kernel, dim3(grid), dim3(256), kBodyLds, st, in, out, (const uint4*)w, bias,
-                       s, act);
+  hipLaunchKernelGGL(conv_body_v3_kernel, dim3(grid), dim3(512), kV3Lds, st, in, out, (const uint4*)w, bias, s,
+                     act);
+}
+
+void launch_conv_body2(const half_t* in, half_t* out, const void* w1, const float* b1, const void* w2,
+                       const float* b2, const ConvShape& s, int act, int num_cus, hipStream_t st) {
+  const int tiles = s.B * ((s.W + kB2TW - 1) / kB2TW) * ((s.H + kB2TH - 1) / kB2TH);
+  const int grid = tiles < num_cus ? tiles : num_cus;
+  hipLaunchKernelGGL(conv_body2_kernel, dim3(grid), dim3(512), kB2Lds, st, in, out, (const uint4*)w1, b1,
+                     (const uint4*)w2, b2, s, tiles, act);
 }
 
 void launch_conv_tail(const half_t* in, const float* xin, float* xout, const void* w, const float* bias,

@@ -6,12 +6,12 @@
 namespace pnp {
 
 // ---- denoiser (conv.hip) -----------------------------------------------------------
+constexpr int kActPad = 2;   // zero border of the hidden activation images (two-layer halo)
 struct ConvShape {
   int B, H, W;       // image size (unpadded)
-  int Hp, Wp;        // padded (H+2, W+2)
+  int pad;           // zero border of the activation images (kActPad)
+  int Hp, Wp;        // padded (H + 2 pad, W + 2 pad)
   int tiles_x, tiles_y, tiles;
-  int ablate;        // profiling only (env PNPPDS_ABLATE): bit0 skip prefetch DMA, bit1 skip stores
-  half_t* trash;     // >= 1 KiB scratch: destination of masked-out epilogue stores
 };
 ConvShape make_conv_shape(int B, int H, int W);
 hipError_t conv_kernels_init();
@@ -20,9 +20,12 @@ void pack_head_weights(const float* W, int C, uint16_t* out);
 void pack_tail_weights(const float* W, int C, uint16_t* out);
 void launch_conv_head(const half_t* in4, half_t* out, const void* w, const float* bias, const ConvShape& s,
                       int act, int num_cus, hipStream_t st);
-// variant 0: 4 waves x (2 rows x 64 ch); variant 1: 8 waves x (1 row x 64 ch)
+// one 64 -> 64 layer (variant kept for the tuning ABI; one kernel)
 void launch_conv_body(const half_t* in, half_t* out, const void* w, const float* bias, const ConvShape& s,
                       int act, int num_cus, int variant, hipStream_t st);
+// two 64 -> 64 layers in one launch (the intermediate stays in LDS); in needs pad >= 2
+void launch_conv_body2(const half_t* in, half_t* out, const void* w1, const float* b1, const void* w2,
+                       const float* b2, const ConvShape& s, int act, int num_cus, hipStream_t st);
 void launch_conv_tail(const half_t* in, const float* xin, float* xout, const void* w, const float* bias,
                       const ConvShape& s, int C, int residual_sign, int clamp_out, int num_cus, hipStream_t st);
 

@@ -167,7 +167,8 @@ class Context:
         self._check(self.lib.pnp_set_tuning(self.h, TUNE_DENOISE_CHUNK, int(images)))
 
     def set_body_variant(self, variant: int):
-        """64->64 conv kernel variant (0: 4 waves/WG, 1: 8 waves/WG).  Performance only."""
+        """Body layers per launch: 1 = two fused layers (default), 0 = one.  Performance only
+        (bit-identical results)."""
         self._check(self.lib.pnp_set_tuning(self.h, TUNE_BODY_VARIANT, int(variant)))
 
     def set_operator(self, kind: int, h=None, mask=None, key=None):

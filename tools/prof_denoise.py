@@ -19,7 +19,7 @@ def main():
     ap.add_argument("--size", type=int, default=256)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--chunk", type=int, default=0)
-    ap.add_argument("--variant", type=int, default=3)
+    ap.add_argument("--variant", type=int, default=1)
     a = ap.parse_args()
     import torch
     from pnppds import _lib
