@@ -142,6 +142,7 @@ def main():
     ap.add_argument("--chunk-sweep", type=str, default="", help="e.g. 4,8,16,256: time each (stderr)")
     ap.add_argument("--variant", type=int, default=1, help="body layers per launch: 1 = two (fused), 0 = one")
     ap.add_argument("--variant-sweep", type=str, default="", help="e.g. 0,1: interleaved A/B (stderr)")
+    ap.add_argument("--ablate", type=int, default=0, help="profiling only (results wrong): 1 DMA, 2 stores, 4 MFMA")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -208,6 +209,8 @@ def main():
         for v in vs:
             log(f"[variant] {v}: ms/iter median {sorted(res[v])[1]:.2f} min {min(res[v]):.2f}")
     ctx.set_body_variant(args.variant)
+    if args.ablate:
+        ctx.set_ablate(args.ablate)
     if args.chunk_sweep or vs:                 # restart the trajectory after the sweep
         ctx.set_denoise_chunk(args.chunk)
         ctx.solver_load_device(d_obs.data_ptr(), d_obs.data_ptr(), d_true.data_ptr())

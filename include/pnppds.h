@@ -106,8 +106,10 @@ int pnp_set_precision(pnp_ctx* ctx, int precision);
  * pair of a pass is sized to stay resident in the 256 MB Infinity Cache).             */
 enum pnp_tuning_key {
   PNP_TUNE_DENOISE_CHUNK = 1,
-  PNP_TUNE_BODY_VARIANT = 2   /* 64->64 body layers: 1 = two layers per launch, the intermediate
-                                 kept in LDS (default); 0 = one layer per launch */
+  PNP_TUNE_BODY_VARIANT = 2,  /* 64->64 body layers: 1 = two layers per launch, the intermediate
+                                 kept in LDS; 0 = one layer per launch (default) */
+  PNP_TUNE_ABLATE = 3         /* profiling only, results are wrong: one-layer body kernel with parts
+                                 skipped (1 = halo DMA, 2 = output stores, 4 = MFMA K-loop) */
 };
 int pnp_set_tuning(pnp_ctx* ctx, int key, int value);
 

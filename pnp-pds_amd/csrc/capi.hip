@@ -48,7 +48,8 @@ struct pnp_ctx {
   // denoiser
   int den_C = 0, den_depth = 0, den_act = 0, den_residual = 1, den_clamp = 1;
   int den_chunk = 0;   // images per denoiser pass; 0 = auto
-  int body_fused = 1;     // 1: body layers two per launch (conv_body2), 0: one per launch (conv_body_v3)
+  int body_fused = 0;     // 1: body layers two per launch (conv_body2), 0: one per launch (conv_body_v3)
+  int ablate = 0;         // profiling only (PNP_TUNE_ABLATE): parts of conv_body_v3 skipped, results wrong
   bool den_ready = false;
   DevBuf head_w, head_b, body_w, body_b, tail_w, tail_b;
 
@@ -269,8 +270,8 @@ void run_denoiser(pnp_ctx* ctx, const half_t* u16, const float* u32, float* xout
         l += 2;
       } else {
         ProfScope ps(ctx, "conv_body", st);
-        launch_conv_body(P<half_t>(act[cur]), P<half_t>(act[cur ^ 1]), wl, bl, s, ctx->den_act, ctx->num_cus, 0,
-                         st);
+        launch_conv_body(P<half_t>(act[cur]), P<half_t>(act[cur ^ 1]), wl, bl, s, ctx->den_act, ctx->num_cus,
+                         ctx->ablate, st);
         check_launch(ctx, "conv_body");
         l += 1;
       }
@@ -555,6 +556,10 @@ int pnp_set_tuning(pnp_ctx* ctx, int key, int value) {
     if (key == PNP_TUNE_BODY_VARIANT) {
       if (value < 0 || value > 1) fail(ctx, PNP_E_ARG, "body variant must be 0 (one layer/launch) or 1 (two)");
       ctx->body_fused = value;
+      return;
+    }
+    if (key == PNP_TUNE_ABLATE) {          // profiling only
+      ctx->ablate = value;
       return;
     }
     fail(ctx, PNP_E_UNSUPPORTED, "tuning key %d", key);

@@ -123,6 +123,7 @@ constexpr int kV3Stage = 3 * kV3Halo;
 constexpr int kV3Bias = kV3Stage + 8 * 4096;
 constexpr int kV3Lds = kV3Bias + 256;                           // 163584 B
 
+template <int ABL>   // profiling ablation (PNP_TUNE_ABLATE), compile-time: ABL = 0 is the product kernel
 __global__ __launch_bounds__(512, 2) void conv_body_v3_kernel(const half_t* __restrict__ in,
                                                                half_t* __restrict__ out,
                                                                const uint4* __restrict__ wpk,
@@ -168,14 +169,14 @@ __global__ __launch_bounds__(512, 2) void conv_body_v3_kernel(const half_t* __re
   };
   auto stage_store = [&](int j, const v4i_t& v) {
     const int pix = 16 * j + (lane >> 2), c = lane & 3;
-    __builtin_amdgcn_raw_buffer_store_b128(v, rs[j >> 1], (pix & 31) * 128 + 64 * m + 16 * c, 0, 0);
+    if constexpr ((ABL & 2) == 0) __builtin_amdgcn_raw_buffer_store_b128(v, rs[j >> 1], (pix & 31) * 128 + 64 * m + 16 * c, 0, 0);
   };
   int cur = 0;
   for (; t < s.tiles; t += gridDim.x) {
     int b, ty0, tx0;
     decode_tile(t, s, b, ty0, tx0);
     const int nxt2 = cur >= 1 ? cur - 1 : 2;  // (cur + 2) % 3
-    issue_dma(t + 2 * gridDim.x, nxt2);
+    if constexpr ((ABL & 1) == 0) issue_dma(t + 2 * gridDim.x, nxt2);
     const unsigned char* hl = buf(cur);
     auto ldB = [&](int ks, int n) {
       const int tap = ks >> 2, sub = ks & 3;
@@ -187,6 +188,10 @@ __global__ __launch_bounds__(512, 2) void conv_body_v3_kernel(const half_t* __re
     v4i_t sv;
 #pragma unroll
     for (int k = 0; k < 1; ++k) { fb[k][0] = ldB(k, 0); fb[k][1] = ldB(k, 1); }
+    if constexpr ((ABL & 4) != 0) {           // profiling: memory path only
+#pragma unroll
+      for (int j = 0; j < 4; ++j) stage_store(j, stage_read(j));
+    } else
 #pragma unroll
     for (int ks = 0; ks < kBodyKSteps; ++ks) {
       const int r = ks & 1;
@@ -242,6 +247,18 @@ __global__ __launch_bounds__(512, 2) void conv_body_v3_kernel(const half_t* __re
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA may land after the workgroup ends
 }
 
+
+#define PNP_V3_INST(A)                                                                                  \
+  template __global__ void conv_body_v3_kernel<A>(const half_t* __restrict__, half_t* __restrict__,    \
+                                                  const uint4* __restrict__, const float* __restrict__, \
+                                                  ConvShape, int);
+PNP_V3_INST(0)
+PNP_V3_INST(1)
+PNP_V3_INST(2)
+PNP_V3_INST(3)
+PNP_V3_INST(4)
+PNP_V3_INST(6)
+#undef PNP_V3_INST
 
 // ------------------------------------------------------------------------------------
 // Two body layers per launch (l+1 and l+2 of basic_models.py:29-33): the intermediate
@@ -732,9 +749,13 @@ ConvShape make_conv_shape(int B, int H, int W) {
 }
 
 hipError_t conv_kernels_init() {
-  hipError_t e = hipFuncSetAttribute((const void*)conv_body_v3_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     kV3Lds);
-  if (e != hipSuccess) return e;
+  hipError_t e = hipSuccess;
+  for (const void* k : {(const void*)conv_body_v3_kernel<0>, (const void*)conv_body_v3_kernel<1>,
+                        (const void*)conv_body_v3_kernel<2>, (const void*)conv_body_v3_kernel<3>,
+                        (const void*)conv_body_v3_kernel<4>, (const void*)conv_body_v3_kernel<6>}) {
+    e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kV3Lds);
+    if (e != hipSuccess) return e;
+  }
   e = hipFuncSetAttribute((const void*)conv_body2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, kB2Lds);
   if (e != hipSuccess) return e;
   return hipFuncSetAttribute((const void*)conv_tail_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, kTailLds);
@@ -747,10 +768,19 @@ void launch_conv_head(const half_t* in4, half_t* out, const void* w, const float
 }
 
 void launch_conv_body(const half_t* in, half_t* out, const void* w, const float* bias, const ConvShape& s,
-                      int act, int num_cus, int /*variant*/, hipStream_t st) {
+                      int act, int num_cus, int ablate, hipStream_t st) {
   const int grid = s.tiles < num_cus ? s.tiles : num_cus;
-  hipLaunchKernelGGL(conv_body_v3_kernel, dim3(grid), dim3(512), kV3Lds, st, in, out, (const uint4*)w, bias, s,
-                     act);
+#define V3(A) hipLaunchKernelGGL((conv_body_v3_kernel<A>), dim3(grid), dim3(512), kV3Lds, st, in, out, (const uint4*)w, \
+                                 bias, s, act)
+  switch (ablate) {
+    case 1: V3(1); break;
+    case 2: V3(2); break;
+    case 3: V3(3); break;
+    case 4: V3(4); break;
+    case 6: V3(6); break;
+    default: V3(0);
+  }
+#undef V3
 }
 
 void launch_conv_body2(const half_t* in, half_t* out, const void* w1, const float* b1, const void* w2,

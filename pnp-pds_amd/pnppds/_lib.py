@@ -22,6 +22,7 @@ METHOD_A, METHOD_B, METHOD_C, METHOD_ADMM_B2 = 0, 1, 2, 3
 OP_ID, OP_BLUR, OP_RANDOM_SAMPLING = 0, 1, 2
 TUNE_DENOISE_CHUNK = 1
 TUNE_BODY_VARIANT = 2
+TUNE_ABLATE = 3
 
 
 class PnpError(RuntimeError):
@@ -165,6 +166,11 @@ class Context:
     def set_denoise_chunk(self, images: int):
         """Images per denoiser pass (0 = auto).  Performance only."""
         self._check(self.lib.pnp_set_tuning(self.h, TUNE_DENOISE_CHUNK, int(images)))
+
+    def set_ablate(self, bits: int):
+        """Profiling only (results wrong): skip parts of the one-layer body kernel
+        (1 = halo DMA, 2 = stores, 4 = MFMA K-loop)."""
+        self._check(self.lib.pnp_set_tuning(self.h, TUNE_ABLATE, int(bits)))
 
     def set_body_variant(self, variant: int):
         """Body layers per launch: 1 = two fused layers (default), 0 = one.  Performance only

@@ -19,7 +19,9 @@ def main():
     ap.add_argument("--size", type=int, default=256)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--chunk", type=int, default=0)
-    ap.add_argument("--variant", type=int, default=1)
+    ap.add_argument("--variant", type=int, default=0)
+    ap.add_argument("--random", action="store_true", help="uniform-random input instead of structured images")
+    ap.add_argument("--ablate", type=int, default=0, help="profiling only: 1 DMA, 2 stores, 4 MFMA skipped")
     a = ap.parse_args()
     import torch
     from pnppds import _lib
@@ -28,8 +30,14 @@ def main():
     ctx.set_denoiser(resolve_weights("DnCNN_nobn_nch_3_nlev_0.01", 3))
     ctx.set_denoise_chunk(a.chunk)
     ctx.set_body_variant(a.variant)
+    ctx.set_ablate(a.ablate)
     B, C, H, W = a.batch, 3, a.size, a.size
-    x = torch.rand((B, C, H, W), device="cuda:0")
+    if a.random:
+        x = torch.rand((B, C, H, W), device="cuda:0")
+    else:                                   # the bench's structured synthetic images (denoiser input range)
+        sys.path.insert(0, REPO)
+        from bench import synthetic_batch
+        x = torch.from_numpy(synthetic_batch(B, C, H, W, seed=1)).cuda()
     y = torch.empty_like(x)
     for _ in range(a.reps):
         ctx.op_denoise(x.data_ptr(), y.data_ptr(), B, C, H, W)
