@@ -140,7 +140,7 @@ def main():
     ap.add_argument("--profile", type=int, default=1, help="HIP-event per-kernel timing in the timed region")
     ap.add_argument("--chunk", type=int, default=0, help="images per denoiser pass (0 = auto)")
     ap.add_argument("--chunk-sweep", type=str, default="", help="e.g. 4,8,16,256: time each (stderr)")
-    ap.add_argument("--variant", type=int, default=1, help="body layers per launch: 1 = two (fused), 0 = one")
+    ap.add_argument("--variant", type=int, default=0, help="body layers per launch: 0 = one (default), 1 = two fused")
     ap.add_argument("--variant-sweep", type=str, default="", help="e.g. 0,1: interleaved A/B (stderr)")
     ap.add_argument("--ablate", type=int, default=0, help="profiling only (results wrong): 1 DMA, 2 stores, 4 MFMA")
     args = ap.parse_args()

@@ -50,6 +50,28 @@ __device__ __forceinline__ void store_act64(half_t* __restrict__ out, const Conv
   *reinterpret_cast<half8_t*>(o + 40) = v3;
 }
 
+
+// bias + activation of 8 accumulator rows -> 8 fp16 (packed adds/muls; LeakyReLU(x) = max(x, 0.01x),
+// ReLU(x) = max(x, 0): bit-identical to act_fn, half the VALU of the select form)
+typedef float f2v_t __attribute__((ext_vector_type(2)));
+template <int ACT>
+__device__ __forceinline__ half8_t bias_act8(const floatx16& a, int off, const float* bl) {
+  half8_t o;
+#pragma unroll
+  for (int r = 0; r < 8; r += 2) {
+    f2v_t v = f2v_t{a[off + r], a[off + r + 1]} + f2v_t{bl[r], bl[r + 1]};
+    if (ACT == 0) {
+      const f2v_t t = v * 0.01f;
+      v = f2v_t{fmaxf(v.x, t.x), fmaxf(v.y, t.y)};
+    } else {
+      v = f2v_t{fmaxf(v.x, 0.f), fmaxf(v.y, 0.f)};
+    }
+    o[r] = (half_t)v.x;
+    o[r + 1] = (half_t)v.y;
+  }
+  return o;
+}
+
 typedef int v4i_t __attribute__((ext_vector_type(4)));
 
 // ------------------------------------------------------------------------------------
@@ -123,12 +145,14 @@ constexpr int kV3Stage = 3 * kV3Halo;
 constexpr int kV3Bias = kV3Stage + 8 * 4096;
 constexpr int kV3Lds = kV3Bias + 256;                           // 163584 B
 
-template <int ABL>   // profiling ablation (PNP_TUNE_ABLATE), compile-time: ABL = 0 is the product kernel
+// ABL: profiling ablation (PNP_TUNE_ABLATE), compile-time; ABL = 0 is the product kernel.
+// ACT: 0 = LeakyReLU(0.01) (simple_CNN), 1 = ReLU (KAIR DnCNN).
+template <int ABL, int ACT>
 __global__ __launch_bounds__(512, 2) void conv_body_v3_kernel(const half_t* __restrict__ in,
                                                                half_t* __restrict__ out,
                                                                const uint4* __restrict__ wpk,
                                                                const float* __restrict__ bias,
-                                                               ConvShape s, int act) {
+                                                               ConvShape s) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float* bias_l = reinterpret_cast<float*>(smem + kV3Bias);
   const int tid = threadIdx.x, lane = tid & 63;
@@ -219,14 +243,8 @@ __global__ __launch_bounds__(512, 2) void conv_body_v3_kernel(const half_t* __re
       for (int n = 0; n < 2; ++n) {
         const int pix = n * 32 + col;
         const floatx16& a = n == 0 ? acc0 : acc1;
-        half8_t lo, hi;
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-          lo[r] = (half_t)act_fn(a[r] + bl[r], act);
-          hi[r] = (half_t)act_fn(a[r + 8] + bl[r + 8], act);
-        }
-        *reinterpret_cast<half8_t*>(stg + pix * 64 + 16 * ((2 * h) ^ sw)) = lo;
-        *reinterpret_cast<half8_t*>(stg + pix * 64 + 16 * ((2 * h + 1) ^ sw)) = hi;
+        *reinterpret_cast<half8_t*>(stg + pix * 64 + 16 * ((2 * h) ^ sw)) = bias_act8<ACT>(a, 0, bl);
+        *reinterpret_cast<half8_t*>(stg + pix * 64 + 16 * ((2 * h + 1) ^ sw)) = bias_act8<ACT>(a, 8, bl + 8);
       }
       const int ncols = min(kTileW, s.W - tx0);
 #pragma unroll
@@ -248,16 +266,17 @@ __global__ __launch_bounds__(512, 2) void conv_body_v3_kernel(const half_t* __re
 }
 
 
-#define PNP_V3_INST(A)                                                                                  \
-  template __global__ void conv_body_v3_kernel<A>(const half_t* __restrict__, half_t* __restrict__,    \
-                                                  const uint4* __restrict__, const float* __restrict__, \
-                                                  ConvShape, int);
-PNP_V3_INST(0)
-PNP_V3_INST(1)
-PNP_V3_INST(2)
-PNP_V3_INST(3)
-PNP_V3_INST(4)
-PNP_V3_INST(6)
+#define PNP_V3_INST(A, F)                                                                                  \
+  template __global__ void conv_body_v3_kernel<A, F>(const half_t* __restrict__, half_t* __restrict__,    \
+                                                     const uint4* __restrict__, const float* __restrict__, \
+                                                     ConvShape);
+PNP_V3_INST(0, 0)
+PNP_V3_INST(0, 1)
+PNP_V3_INST(1, 0)
+PNP_V3_INST(2, 0)
+PNP_V3_INST(3, 0)
+PNP_V3_INST(4, 0)
+PNP_V3_INST(6, 0)
 #undef PNP_V3_INST
 
 // ------------------------------------------------------------------------------------
@@ -306,13 +325,39 @@ __device__ __forceinline__ void decode_tile2(int t, const ConvShape& s, int& b, 
   tx0 = (r - yy * tx) * kB2TW;
 }
 
+// Stage-1 waves' share of the 12 x 20 input-halo DMA of a fused tile: 8 uniform slots each
+// (slot g = wave + 4j; slots 30, 31 re-read pixel 239 into padding).  The per-lane offsets
+// are recomputed at each issue (a few VALU per slot) rather than held in 8 VGPRs; the
+// opaque copy of the lane id keeps the compiler from hoisting (and spilling) them.
+__device__ __forceinline__ void b2_halo_dma(unsigned char* hl, const half_t* __restrict__ in, const ConvShape& s,
+                                            int t, int wave, int lane) {
+  int b, ty0, tx0;
+  decode_tile2(t, s, b, ty0, tx0);
+  // input halo origin: image (ty0 - 2, tx0 - 2) = padded (ty0 + pad - 2, tx0 + pad - 2)
+  const half_t* base = in + (((size_t)b * s.Hp + ty0 + s.pad - 2) * s.Wp + tx0 + s.pad - 2) * kWidth;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, 0x7fffffff, 0x00020000);
+  int ln = lane;
+  asm volatile("" : "+v"(ln));
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int p = 8 * (4 * j + (wave & 3)) + (ln >> 3);
+    const int pl = min(p, kB2InPix - 1);
+    const int pr = pl / kB2IW, pc = pl - pr * kB2IW;
+    const int c = (ln & 7) ^ ((pc >> 1) & 7);
+    const unsigned off = (unsigned)(((pr * s.Wp + pc) * kWidth + c * 8) * 2);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(
+        rs, (__attribute__((address_space(3))) void*)(hl + (4 * j + (wave & 3)) * 1024), 16, off, 0, 0, 0);
+  }
+}
+
+template <int ACT>
 __global__ __launch_bounds__(512, 2) void conv_body2_kernel(const half_t* __restrict__ in,
                                                              half_t* __restrict__ out,
                                                              const uint4* __restrict__ w1,
                                                              const float* __restrict__ b1,
                                                              const uint4* __restrict__ w2,
                                                              const float* __restrict__ b2,
-                                                             ConvShape s, int tiles, int act) {
+                                                             ConvShape s, int tiles) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float* bias_l = reinterpret_cast<float*>(smem + kB2Bias);
   const int tid = threadIdx.x, lane = tid & 63;
@@ -333,29 +378,8 @@ __global__ __launch_bounds__(512, 2) void conv_body2_kernel(const half_t* __rest
   auto inbuf = [&](int i) { return smem + i * kB2InBytes; };
   auto midbuf = [&](int i) { return smem + kB2Mid + i * kB2MidBytes; };
 
-  // stage-1 waves: 8 DMA slots each (slot g = wave + 4j).  The per-lane offsets are
-  // recomputed at each issue (a few VALU per slot) rather than held in 8 VGPRs.
-  auto dma_off = [&](int j, int ln) {
-    const int p = 8 * (4 * j + (wave & 3)) + (ln >> 3);
-    const int pl = min(p, kB2InPix - 1);
-    const int pr = pl / kB2IW, pc = pl - pr * kB2IW;
-    const int c = (ln & 7) ^ ((pc >> 1) & 7);
-    return (unsigned)(((pr * s.Wp + pc) * kWidth + c * 8) * 2);
-  };
   auto issue_dma = [&](int tt, int bi) {      // stage-1 waves only; clamped tile: fixed op count
-    int b, ty0, tx0;
-    decode_tile2(tt < tiles ? tt : tiles - 1, s, b, ty0, tx0);
-    // input halo origin: image (ty0 - 2, tx0 - 2) = padded (ty0 + pad - 2, tx0 + pad - 2)
-    const half_t* base = in + (((size_t)b * s.Hp + ty0 + s.pad - 2) * s.Wp + tx0 + s.pad - 2) * kWidth;
-    const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, 0x7fffffff, 0x00020000);
-    unsigned char* hl = inbuf(bi);
-    int ln = lane;
-    asm volatile("" : "+v"(ln));              // opaque: keeps the offsets from being hoisted (and spilled)
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rs, (__attribute__((address_space(3))) void*)(hl + (4 * j + (wave & 3)) * 1024), 16, dma_off(j, ln), 0, 0, 0);
+    b2_halo_dma(inbuf(bi), in, s, tt < tiles ? tt : tiles - 1, wave, lane);
   };
 
   const int t0 = blockIdx.x;
@@ -412,12 +436,9 @@ __global__ __launch_bounds__(512, 2) void conv_body2_kernel(const half_t* __rest
           // bias + act -> fp16 -> intermediate; zero outside the image (layer l+2's padding)
           const int y = ty0 - 1 + r1, x = tx0 - 1 + c1;
           const bool inside = y >= 0 && y < s.H && x >= 0 && x < s.W;
-          half8_t lo, hi;
-#pragma unroll
-          for (int r = 0; r < 8; ++r) {
-            lo[r] = inside ? (half_t)act_fn(acc[r] + bl[r], act) : (half_t)0.f;
-            hi[r] = inside ? (half_t)act_fn(acc[r + 8] + bl[r + 8], act) : (half_t)0.f;
-          }
+          const half8_t z = {};
+          const half8_t lo = inside ? bias_act8<ACT>(acc, 0, bl) : z;
+          const half8_t hi = inside ? bias_act8<ACT>(acc, 8, bl + 8) : z;
           if (n < kB2MidPix) {
             const int q = 4 * m + 2 * h;
             *reinterpret_cast<half8_t*>(mid + img_off(r1, c1, kB2MW, q)) = lo;
@@ -469,14 +490,8 @@ __global__ __launch_bounds__(512, 2) void conv_body2_kernel(const half_t* __rest
           const floatx16& a = nn == 0 ? acc0 : acc1;
           const int pix = 32 * nn + col;            // rows 2nn + col/16 of this wave, col%16
           const int sw = (pix >> 1) & 3;
-          half8_t lo, hi;
-#pragma unroll
-          for (int r = 0; r < 8; ++r) {
-            lo[r] = (half_t)act_fn(a[r] + bl[r], act);
-            hi[r] = (half_t)act_fn(a[r + 8] + bl[r + 8], act);
-          }
-          *reinterpret_cast<half8_t*>(stg + pix * 64 + 16 * ((2 * h) ^ sw)) = lo;
-          *reinterpret_cast<half8_t*>(stg + pix * 64 + 16 * ((2 * h + 1) ^ sw)) = hi;
+          *reinterpret_cast<half8_t*>(stg + pix * 64 + 16 * ((2 * h) ^ sw)) = bias_act8<ACT>(a, 0, bl);
+          *reinterpret_cast<half8_t*>(stg + pix * 64 + 16 * ((2 * h + 1) ^ sw)) = bias_act8<ACT>(a, 8, bl + 8);
         }
         const int ncols = min(kB2TW, s.W - tx0);
 #pragma unroll
@@ -750,14 +765,17 @@ ConvShape make_conv_shape(int B, int H, int W) {
 
 hipError_t conv_kernels_init() {
   hipError_t e = hipSuccess;
-  for (const void* k : {(const void*)conv_body_v3_kernel<0>, (const void*)conv_body_v3_kernel<1>,
-                        (const void*)conv_body_v3_kernel<2>, (const void*)conv_body_v3_kernel<3>,
-                        (const void*)conv_body_v3_kernel<4>, (const void*)conv_body_v3_kernel<6>}) {
+  for (const void* k : {(const void*)conv_body_v3_kernel<0, 0>, (const void*)conv_body_v3_kernel<0, 1>,
+                        (const void*)conv_body_v3_kernel<1, 0>, (const void*)conv_body_v3_kernel<2, 0>,
+                        (const void*)conv_body_v3_kernel<3, 0>, (const void*)conv_body_v3_kernel<4, 0>,
+                        (const void*)conv_body_v3_kernel<6, 0>}) {
     e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kV3Lds);
     if (e != hipSuccess) return e;
   }
-  e = hipFuncSetAttribute((const void*)conv_body2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, kB2Lds);
-  if (e != hipSuccess) return e;
+  for (const void* k : {(const void*)conv_body2_kernel<0>, (const void*)conv_body2_kernel<1>}) {
+    e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kB2Lds);
+    if (e != hipSuccess) return e;
+  }
   return hipFuncSetAttribute((const void*)conv_tail_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, kTailLds);
 }
 
@@ -770,15 +788,19 @@ void launch_conv_head(const half_t* in4, half_t* out, const void* w, const float
 void launch_conv_body(const half_t* in, half_t* out, const void* w, const float* bias, const ConvShape& s,
                       int act, int num_cus, int ablate, hipStream_t st) {
   const int grid = s.tiles < num_cus ? s.tiles : num_cus;
-#define V3(A) hipLaunchKernelGGL((conv_body_v3_kernel<A>), dim3(grid), dim3(512), kV3Lds, st, in, out, (const uint4*)w, \
-                                 bias, s, act)
+#define V3(A, F) hipLaunchKernelGGL((conv_body_v3_kernel<A, F>), dim3(grid), dim3(512), kV3Lds, st, in, out, \
+                                    (const uint4*)w, bias, s)
+  if (act != 0) {
+    V3(0, 1);
+    return;
+  }
   switch (ablate) {
-    case 1: V3(1); break;
-    case 2: V3(2); break;
-    case 3: V3(3); break;
-    case 4: V3(4); break;
-    case 6: V3(6); break;
-    default: V3(0);
+    case 1: V3(1, 0); break;
+    case 2: V3(2, 0); break;
+    case 3: V3(3, 0); break;
+    case 4: V3(4, 0); break;
+    case 6: V3(6, 0); break;
+    default: V3(0, 0);
   }
 #undef V3
 }
@@ -787,8 +809,12 @@ void launch_conv_body2(const half_t* in, half_t* out, const void* w1, const floa
                        const float* b2, const ConvShape& s, int act, int num_cus, hipStream_t st) {
   const int tiles = s.B * ((s.W + kB2TW - 1) / kB2TW) * ((s.H + kB2TH - 1) / kB2TH);
   const int grid = tiles < num_cus ? tiles : num_cus;
-  hipLaunchKernelGGL(conv_body2_kernel, dim3(grid), dim3(512), kB2Lds, st, in, out, (const uint4*)w1, b1,
-                     (const uint4*)w2, b2, s, tiles, act);
+  if (act == 0)
+    hipLaunchKernelGGL((conv_body2_kernel<0>), dim3(grid), dim3(512), kB2Lds, st, in, out, (const uint4*)w1, b1,
+                       (const uint4*)w2, b2, s, tiles);
+  else
+    hipLaunchKernelGGL((conv_body2_kernel<1>), dim3(grid), dim3(512), kB2Lds, st, in, out, (const uint4*)w1, b1,
+                       (const uint4*)w2, b2, s, tiles);
 }
 
 void launch_conv_tail(const half_t* in, const float* xin, float* xout, const void* w, const float* bias,

@@ -39,6 +39,14 @@ def test_library_exports_every_declared_symbol(lib):
     assert not missing, missing
 
 
+def test_no_unresolved_library_symbols(lib):
+    """Every kernel the library launches is defined in it (an uninstantiated kernel template
+    shows up as an undefined pnp:: symbol and only fails at load on the GPU box)."""
+    out = subprocess.run(["nm", "-D", "--undefined-only", LIB], capture_output=True, text=True, check=True).stdout
+    bad = [ln.split()[-1] for ln in out.splitlines() if "pnp" in ln]
+    assert not bad, bad
+
+
 def test_exports_are_plain_c(lib):
     out = subprocess.run(["nm", "-D", "--defined-only", LIB], capture_output=True, text=True, check=True).stdout
     exported = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
