@@ -232,7 +232,7 @@ def main():
         dist.barrier()
         t_el = max_over_ranks(t_el, device=f"cuda:{local}")   # job time = slowest rank
     prof = ctx.profile_read() if args.profile else {}
-    x_out, s_out, c_hist, psnr_hist = ctx.solver_fetch()
+    x_out, s_out, c_hist, psnr_hist, ssim_hist = ctx.solver_fetch()
 
     value = B * world * K / t_el
     if rank == 0:
@@ -281,6 +281,7 @@ def main():
                                     "frac": round(pb[k] / (prof[k][0] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
                                 for k in pb if k in prof}
         line["psnr_img0_db"] = [round(float(psnr_hist[0, 0]), 4), round(float(psnr_hist[0, cap - 1]), 4)]
+        line["ssim_img0"] = [round(float(ssim_hist[0, 0]), 5), round(float(ssim_hist[0, cap - 1]), 5)]
         if world == 1 and not args.no_cpu_baseline:
             rate, n_cpu, ps_cpu, thr = cpu_baseline(x_true[0], d_obs[0].cpu().numpy(), h, args.cpu_budget, cap)
             line["cpu_baseline"] = {"value": round(rate, 3), "unit": "image-iterations/s", "cores": thr,

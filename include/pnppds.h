@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define PNP_ABI_VERSION 1
+#define PNP_ABI_VERSION 2
 
 typedef struct pnp_ctx pnp_ctx;
 
@@ -81,6 +81,7 @@ typedef struct pnp_params {
   double poisson_alpha;           /* Poisson scale                                     */
   double r;                       /* sampling rate; also scales the B-method balls     */
   int32_t record_metrics;         /* 1: c_n and PSNR every iteration (iteration.py:187-188) */
+  int32_t record_ssim;            /* 1 (with record_metrics): also SSIM (iteration.py:189)  */
 } pnp_params;
 
 /* ---- library / context -------------------------------------------------------- */
@@ -122,12 +123,14 @@ int pnp_set_operator(pnp_ctx* ctx, int kind, const double* h, int kh, int kw,
 
 /* ---- whole solver (iteration.test_iter) ---------------------------------------- */
 /* Batched test_iter: B independent images.  x0/xobs: B*C*H*W float32; xtrue may be
- * NULL (then psnr_out is NaN).  Outputs (any may be NULL): x_out, s_out (= s + 0.5 as
- * iteration.py:196 returns), c_out and psnr_out (B x max_iter float64, row-major),
+ * NULL (then psnr_out and ssim_out are NaN).  Outputs (any may be NULL): x_out, s_out
+ * (= s + 0.5 as iteration.py:196 returns), c_out, psnr_out and ssim_out (B x max_iter
+ * float64, row-major; ssim_out is NaN unless params->record_ssim),
  * avg_time_s = wall seconds per iteration on the device.                            */
 int pnp_run(pnp_ctx* ctx, int method, const pnp_params* params, int B, int C, int H, int W,
             const float* x0, const float* xobs, const float* xtrue, int max_iter,
-            float* x_out, float* s_out, double* c_out, double* psnr_out, double* avg_time_s);
+            float* x_out, float* s_out, double* c_out, double* psnr_out, double* ssim_out,
+            double* avg_time_s);
 
 /* Staged form of pnp_run, with state resident in HBM between calls (bench / drivers). */
 int pnp_solver_setup(pnp_ctx* ctx, int method, const pnp_params* params, int B, int C, int H,
@@ -136,7 +139,8 @@ int pnp_solver_load(pnp_ctx* ctx, const float* x0, const float* xobs, const floa
 int pnp_solver_load_device(pnp_ctx* ctx, const float* d_x0, const float* d_xobs,
                            const float* d_xtrue);
 int pnp_solver_iterate(pnp_ctx* ctx, int n_iter);   /* enqueue only (async) */
-int pnp_solver_fetch(pnp_ctx* ctx, float* x_out, float* s_out, double* c_out, double* psnr_out);
+int pnp_solver_fetch(pnp_ctx* ctx, float* x_out, float* s_out, double* c_out, double* psnr_out,
+                     double* ssim_out);
 int pnp_solver_iterations_done(pnp_ctx* ctx, int* n);
 /* Device pointers of the solver's primal / dual state (read-only views, B*C*H*W). */
 int pnp_solver_state(pnp_ctx* ctx, const float** d_x, const float** d_y, const float** d_s);
@@ -161,6 +165,13 @@ int pnp_op_denoise(pnp_ctx* ctx, const float* x, float* out, int B, int C, int H
 /* psnr_out: host array of B doubles (synchronous). */
 int pnp_op_psnr(pnp_ctx* ctx, const float* x_true, const float* x, int B, int64_t n, double* psnr_out,
                 void* stream);
+
+/* utils_eval.py:9-12 eval_ssim per image: skimage structural_similarity(x_true, x,
+ * data_range = x.max() - x.min(), channel_axis = 0) with scikit-image 0.22 defaults.
+ * C == 1 images are the reference's (H, W) grayscale arrays (mean of per-row 1-D SSIMs).
+ * ssim_out: host array of B doubles (synchronous).                                  */
+int pnp_op_ssim(pnp_ctx* ctx, const float* x_true, const float* x, int B, int C, int H, int W,
+                double* ssim_out, void* stream);
 
 #ifdef __cplusplus
 }

@@ -115,6 +115,49 @@ def psnr(x_true, x):
     return 10 * np.log10(1.0 / mse)
 
 
+def _ssim_single(im1, im2, data_range, win_size=7):
+    """skimage.metrics.structural_similarity (scikit-image 0.22.0, pinned in the reference's
+    requirements.txt), channel_axis=None path, default arguments: uniform 7-wide window
+    (scipy.ndimage.uniform_filter, axis by axis), K1 = 0.01, K2 = 0.03, sample covariance,
+    float32 arithmetic for float32 inputs, mean over the map cropped by (win-1)/2."""
+    from scipy.ndimage import uniform_filter
+    ft = np.float32
+    im1 = im1.astype(ft, copy=False)
+    im2 = im2.astype(ft, copy=False)
+    NP = win_size ** im1.ndim
+    cov_norm = NP / (NP - 1)
+    ux = uniform_filter(im1, size=win_size)
+    uy = uniform_filter(im2, size=win_size)
+    uxx = uniform_filter(im1 * im1, size=win_size)
+    uyy = uniform_filter(im2 * im2, size=win_size)
+    uxy = uniform_filter(im1 * im2, size=win_size)
+    vx = cov_norm * (uxx - ux * ux)
+    vy = cov_norm * (uyy - uy * uy)
+    vxy = cov_norm * (uxy - ux * uy)
+    R = data_range
+    C1 = (0.01 * R) ** 2
+    C2 = (0.03 * R) ** 2
+    A1, A2, B1, B2 = (2 * ux * uy + C1, 2 * vxy + C2, ux ** 2 + uy ** 2 + C1, vx + vy + C2)
+    S = (A1 * A2) / (B1 * B2)
+    pad = (win_size - 1) // 2
+    crop = tuple(slice(pad, n - pad) for n in S.shape)
+    return S[crop].mean(dtype=np.float64)
+
+
+def ssim(x_true, x):
+    """utils/utils_eval.py:9-12: structural_similarity(x_true, x, data_range = x.max() -
+    x.min(), channel_axis=0).  channel_axis=0 makes skimage loop over axis 0 and average:
+    an RGB (C,H,W) image gives the mean of C 2-D SSIMs; a grayscale (H,W) image gives the
+    mean of H 1-D SSIMs over its rows (the reference's quirk).
+    PARITY UNPINNED: scikit-image is absent here, so this restatement of its published
+    algorithm is checked against no reference output."""
+    x_true = np.asarray(x_true, np.float32)
+    x = np.asarray(x, np.float32)
+    data_range = x.max() - x.min()
+    vals = np.array([_ssim_single(x_true[i], x[i], data_range) for i in range(x.shape[0])], np.float32)
+    return float(vals.mean())
+
+
 # ---------------------------------------------------------------------------
 # Denoiser (models/denoiser.py:34-46, models/basic_models.py:25-38,
 #           KAIR variant models/network_dncnn.py:42-77)

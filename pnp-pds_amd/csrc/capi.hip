@@ -66,6 +66,7 @@ struct pnp_ctx {
   int cur = 0;
   DevBuf x[2], y, s, w, xobs, xtrue, u32, u16, act[2], partials, metrics, theta;
   DevBuf z, p, t;   // comparisonB-2 only
+  DevBuf ssim_scr;  // SSIM partials (record_ssim)
 
   // scratch for single ops
   DevBuf scr_u32, scr_u16, scr_act[2], scr_part, scr_theta;
@@ -293,6 +294,16 @@ double l2_eps(pnp_ctx* ctx, size_t n) {
   return std::sqrt((double)n * (1.0 - p.sp_nl)) * r * p.alpha_n * p.gaussian_nl;
 }
 
+// iteration.py:189: ssim_data[i] = eval_ssim(x_true, x_n), only when asked (record_ssim)
+void record_ssim(pnp_ctx* ctx, const float* xn, hipStream_t st) {
+  const pnp_params& p = ctx->prm;
+  if (!(p.record_metrics && p.record_ssim && ctx->has_true && ctx->it < ctx->cap)) return;
+  ProfScope ps(ctx, "ssim", st);
+  launch_ssim(P<float>(ctx->xtrue), xn, ctx->ssim_scr.p, P<double>(ctx->metrics), ctx->B, ctx->C, ctx->H, ctx->W,
+              ctx->it, ctx->cap, st);
+  check_launch(ctx, "ssim");
+}
+
 void solver_iteration(pnp_ctx* ctx) {
   hipStream_t st = ctx->stream;
   const pnp_params& p = ctx->prm;
@@ -331,6 +342,7 @@ void solver_iteration(pnp_ctx* ctx) {
               l2_eps(ctx, n), P<double>(ctx->metrics), ctx->it, ctx->cap, record, ctx->has_true, st);
     check_launch(ctx, "k3");
   }
+  record_ssim(ctx, xn, st);
   ctx->cur ^= 1;
   ctx->it += 1;
 }
@@ -389,6 +401,7 @@ void solver_iteration_admm(pnp_ctx* ctx) {
                      P<double>(ctx->metrics), B, n, ctx->it, ctx->cap, st);
     check_launch(ctx, "admm_zy");
   }
+  record_ssim(ctx, xn, st);
   ctx->cur ^= 1;
   ctx->it += 1;
 }
@@ -431,7 +444,8 @@ void solver_setup(pnp_ctx* ctx, int method, const pnp_params* params, int B, int
   ensure_padded(ctx, ctx->u16, B, H, W, 4, 1, ctx->stream);
   ensure(ctx, ctx->partials,
          (size_t)B * std::max(partial_tiles(H, W) * C, chunk_count((size_t)C * H * W)) * 4 * sizeof(double));
-  ensure(ctx, ctx->metrics, (size_t)B * std::max(ctx->cap, 1) * 2 * sizeof(double));
+  ensure(ctx, ctx->metrics, (size_t)B * std::max(ctx->cap, 1) * kMetrics * sizeof(double));
+  if (params->record_ssim) ensure(ctx, ctx->ssim_scr, ssim_scratch_bytes(B, C, H, W));
   ensure(ctx, ctx->theta, (size_t)B * sizeof(float));
   ctx->loaded = false;
   ctx->it = 0;
@@ -443,7 +457,7 @@ void solver_reset_state(pnp_ctx* ctx) {
   HIPCHK(ctx, hipMemsetAsync(ctx->s.p, 0, fb, ctx->stream));          // iteration.py:27
   if (ctx->method == PNP_METHOD_ADMM_B2) HIPCHK(ctx, hipMemsetAsync(ctx->z.p, 0, fb, ctx->stream));
   if (ctx->cap) {
-    std::vector<double> nanbuf((size_t)ctx->B * ctx->cap * 2, std::nan(""));
+    std::vector<double> nanbuf((size_t)ctx->B * ctx->cap * kMetrics, std::nan(""));
     HIPCHK(ctx, hipMemcpyAsync(ctx->metrics.p, nanbuf.data(), nanbuf.size() * sizeof(double), hipMemcpyHostToDevice,
                                ctx->stream));
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
@@ -453,7 +467,7 @@ void solver_reset_state(pnp_ctx* ctx) {
   ctx->loaded = true;
 }
 
-void solver_fetch(pnp_ctx* ctx, float* x_out, float* s_out, double* c_out, double* psnr_out) {
+void solver_fetch(pnp_ctx* ctx, float* x_out, float* s_out, double* c_out, double* psnr_out, double* ssim_out) {
   if (!ctx->loaded) fail(ctx, PNP_E_STATE, "solver not loaded");
   const size_t N = (size_t)ctx->B * ctx->C * ctx->H * ctx->W;
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
@@ -462,12 +476,13 @@ void solver_fetch(pnp_ctx* ctx, float* x_out, float* s_out, double* c_out, doubl
     HIPCHK(ctx, hipMemcpy(s_out, ctx->s.p, N * sizeof(float), hipMemcpyDeviceToHost));
     for (size_t i = 0; i < N; ++i) s_out[i] += 0.5f;                // iteration.py:196
   }
-  if ((c_out || psnr_out) && ctx->cap) {
-    std::vector<double> m((size_t)ctx->B * ctx->cap * 2);
+  if ((c_out || psnr_out || ssim_out) && ctx->cap) {
+    std::vector<double> m((size_t)ctx->B * ctx->cap * kMetrics);
     HIPCHK(ctx, hipMemcpy(m.data(), ctx->metrics.p, m.size() * sizeof(double), hipMemcpyDeviceToHost));
     for (size_t i = 0; i < (size_t)ctx->B * ctx->cap; ++i) {
-      if (c_out) c_out[i] = m[2 * i];
-      if (psnr_out) psnr_out[i] = m[2 * i + 1];
+      if (c_out) c_out[i] = m[kMetrics * i];
+      if (psnr_out) psnr_out[i] = m[kMetrics * i + 1];
+      if (ssim_out) ssim_out[i] = m[kMetrics * i + 2];
     }
   }
 }
@@ -530,7 +545,7 @@ int pnp_destroy(pnp_ctx* ctx) {
                     &ctx->w, &ctx->xobs, &ctx->xtrue, &ctx->u32, &ctx->u16, &ctx->act[0], &ctx->act[1],
                     &ctx->partials, &ctx->metrics, &ctx->theta, &ctx->scr_u32, &ctx->scr_u16,
                     &ctx->scr_act[0], &ctx->scr_act[1], &ctx->scr_part, &ctx->scr_theta,
-                    &ctx->z, &ctx->p, &ctx->t, &ctx->dense_fwd, &ctx->dense_adj};
+                    &ctx->z, &ctx->p, &ctx->t, &ctx->dense_fwd, &ctx->dense_adj, &ctx->ssim_scr};
   for (DevBuf* b : bufs) release(*b);
   for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -744,9 +759,10 @@ int pnp_solver_iterate(pnp_ctx* ctx, int n_iter) {
   });
 }
 
-int pnp_solver_fetch(pnp_ctx* ctx, float* x_out, float* s_out, double* c_out, double* psnr_out) {
+int pnp_solver_fetch(pnp_ctx* ctx, float* x_out, float* s_out, double* c_out, double* psnr_out,
+                     double* ssim_out) {
   if (!ctx) return PNP_E_ARG;
-  return guarded(ctx, [&] { solver_fetch(ctx, x_out, s_out, c_out, psnr_out); });
+  return guarded(ctx, [&] { solver_fetch(ctx, x_out, s_out, c_out, psnr_out, ssim_out); });
 }
 
 int pnp_solver_iterations_done(pnp_ctx* ctx, int* n) {
@@ -767,7 +783,7 @@ int pnp_solver_state(pnp_ctx* ctx, const float** d_x, const float** d_y, const f
 
 int pnp_run(pnp_ctx* ctx, int method, const pnp_params* params, int B, int C, int H, int W, const float* x0,
             const float* xobs, const float* xtrue, int max_iter, float* x_out, float* s_out, double* c_out,
-            double* psnr_out, double* avg_time_s) {
+            double* psnr_out, double* ssim_out, double* avg_time_s) {
   if (!ctx) return PNP_E_ARG;
   return guarded(ctx, [&] {
     if (max_iter < 0) fail(ctx, PNP_E_ARG, "max_iter < 0");
@@ -785,7 +801,7 @@ int pnp_run(pnp_ctx* ctx, int method, const pnp_params* params, int B, int C, in
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     if (avg_time_s) *avg_time_s = max_iter ? dt / max_iter : 0.0;
-    solver_fetch(ctx, x_out, s_out, c_out, psnr_out);
+    solver_fetch(ctx, x_out, s_out, c_out, psnr_out, ssim_out);
   });
 }
 
@@ -920,6 +936,25 @@ int pnp_op_psnr(pnp_ctx* ctx, const float* x_true, const float* x, int B, int64_
       for (int k = 0; k < chunks; ++k) s += part[(size_t)b * chunks + k];
       psnr_out[b] = 10.0 * std::log10(1.0 / (s / (double)n));       // utils_eval.py:4-7
     }
+  });
+}
+
+int pnp_op_ssim(pnp_ctx* ctx, const float* x_true, const float* x, int B, int C, int H, int W, double* ssim_out,
+                void* stream) {
+  if (!ctx) return PNP_E_ARG;
+  return guarded(ctx, [&] {
+    if (!x_true || !x || !ssim_out || B < 1 || C < 1 || H < 1 || W < 1) fail(ctx, PNP_E_ARG, "bad arguments");
+    if (C == 1 ? W < 7 : (H < 7 || W < 7)) fail(ctx, PNP_E_ARG, "SSIM needs a 7x7 window inside the image");
+    ensure(ctx, ctx->scr_part, ssim_scratch_bytes(B, C, H, W) + (size_t)B * kMetrics * sizeof(double) + 256);
+    hipStream_t st = pick_stream(ctx, stream);
+    double* m = P<double>(ctx->scr_part);                     // metrics[b][0][kMetrics]
+    void* scr = reinterpret_cast<char*>(ctx->scr_part.p) + (((size_t)B * kMetrics * sizeof(double) + 255) & ~(size_t)255);
+    launch_ssim(x_true, x, scr, m, B, C, H, W, 0, 1, st);
+    check_launch(ctx, "ssim");
+    std::vector<double> h((size_t)B * kMetrics);
+    HIPCHK(ctx, hipMemcpyAsync(h.data(), m, h.size() * sizeof(double), hipMemcpyDeviceToHost, st));
+    HIPCHK(ctx, hipStreamSynchronize(st));
+    for (int b = 0; b < B; ++b) ssim_out[b] = h[(size_t)b * kMetrics + 2];
   });
 }
 

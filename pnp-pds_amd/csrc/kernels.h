@@ -76,6 +76,12 @@ void launch_sqdiff(const float* a, const float* c, double* partials, int B, size
 void launch_shrink(const float* v, float* out, const float* theta, int B, size_t n, hipStream_t st);
 void launch_gkl(const float* x, const float* x0, float* out, size_t count, double gamma, double alpha,
                 hipStream_t st);
+// per-iteration metrics: metrics[b][it][kMetrics] = {c_n, PSNR, SSIM}
+constexpr int kMetrics = 3;
+// SSIM of x against xt (utils_eval.py:9-12) into metrics[b][it][2]; scratch >= ssim_scratch_bytes
+size_t ssim_scratch_bytes(int B, int C, int H, int W);
+void launch_ssim(const float* xt, const float* x, void* scratch, double* metrics, int B, int C, int H, int W,
+                 int it, int cap, hipStream_t st);
 // comparisonB-2: out = k + ca*a + cb*b + cc*c + cd*d (null inputs skipped), fp64 arithmetic
 void launch_lincomb(float* out, double k, const float* a, double ca, const float* b, double cb, const float* c,
                     double cc, const float* d, double cd, size_t count, hipStream_t st);

@@ -228,7 +228,7 @@ __device__ __forceinline__ void reduce_partials(const double* __restrict__ parti
 
 __device__ __forceinline__ void write_metrics(double* metrics, int b, int it, int cap, const double (&a)[4],
                                               double n_elem, int has_true) {
-  double* m = metrics + ((size_t)b * cap + it) * 2;
+  double* m = metrics + ((size_t)b * cap + it) * kMetrics;
   m[0] = sqrt(a[1]) / sqrt(a[2]);                                   // iteration.py:187
   m[1] = has_true ? 10.0 * log10(1.0 / (a[3] / n_elem)) : __builtin_nan("");   // utils_eval.py:4-7
 }
@@ -732,6 +732,211 @@ __global__ __launch_bounds__(256) void k2_blur_rb(const float* __restrict__ xn, 
 }
 
 // =====================================================================================
+// SSIM (utils/utils_eval.py:9-12): skimage.metrics.structural_similarity(x_true, x,
+// data_range = x.max() - x.min(), channel_axis = 0), scikit-image 0.22.0 defaults:
+// 7-wide uniform window (scipy uniform_filter: axis 0 then axis 1, float32 between the
+// passes), K1 = 0.01, K2 = 0.03, sample covariance, float32 map, mean over the map
+// cropped by 3.  channel_axis=0: RGB (C,H,W) -> mean of C 2-D SSIMs; grayscale (H,W) ->
+// mean of H 1-D SSIMs over the rows (skimage loops over axis 0).  Cropped pixels' windows
+// never leave the image, so no boundary mode is needed.
+//   ssim_minmax:  per-image min/max partials of x           (data_range)
+//   ssim_rgb:     per (32x32 tile, channel) sums of the cropped SSIM map
+//   ssim_gray:    per-row means of the 1-D SSIM map
+//   ssim_final:   per image, fixed-order reduction -> metrics[b][it][2]
+// =====================================================================================
+__global__ __launch_bounds__(256) void ssim_minmax_kernel(const float* __restrict__ x, float* __restrict__ mm,
+                                                          size_t n, int chunks) {
+  __shared__ float red[2][4];
+  const int b = blockIdx.y;
+  const size_t beg = (size_t)blockIdx.x * 2048;
+  float lo = __builtin_inff(), hi = -__builtin_inff();
+  for (size_t k = beg + threadIdx.x; k < beg + 2048 && k < n; k += 256) {
+    const float v = x[(size_t)b * n + k];
+    lo = fminf(lo, v);
+    hi = fmaxf(hi, v);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    lo = fminf(lo, __shfl_xor(lo, o, 64));
+    hi = fmaxf(hi, __shfl_xor(hi, o, 64));
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { red[0][w] = lo; red[1][w] = hi; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float a = red[0][0], c = red[1][0];
+    for (int i = 1; i < 4; ++i) { a = fminf(a, red[0][i]); c = fmaxf(c, red[1][i]); }
+    mm[((size_t)b * chunks + blockIdx.x) * 2 + 0] = a;
+    mm[((size_t)b * chunks + blockIdx.x) * 2 + 1] = c;
+  }
+}
+
+// data_range of image b from the minmax partials: one wave, lanes stride the chunks
+__device__ __forceinline__ float ssim_range_wave(const float* __restrict__ mm, int b, int chunks, int lane) {
+  float lo = __builtin_inff(), hi = -__builtin_inff();
+  for (int k = lane; k < chunks; k += 64) {
+    lo = fminf(lo, mm[((size_t)b * chunks + k) * 2 + 0]);
+    hi = fmaxf(hi, mm[((size_t)b * chunks + k) * 2 + 1]);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    lo = fminf(lo, __shfl_xor(lo, o, 64));
+    hi = fmaxf(hi, __shfl_xor(hi, o, 64));
+  }
+  return hi - lo;                                  // im2.max() - im2.min() in float32
+}
+
+__device__ __forceinline__ float ssim_s(float ux, float uy, float uxx, float uyy, float uxy, float cov_norm,
+                                        float C1, float C2) {
+#pragma clang fp contract(off)   // numpy rounds every product and sum to float32
+  const float vx = cov_norm * (uxx - ux * ux);
+  const float vy = cov_norm * (uyy - uy * uy);
+  const float vxy = cov_norm * (uxy - ux * uy);
+  const float A1 = 2.f * ux * uy + C1, A2 = 2.f * vxy + C2;
+  const float B1 = ux * ux + uy * uy + C1, B2 = vx + vy + C2;
+  return (A1 * A2) / (B1 * B2);
+}
+
+// Window sums in float64 of float32 values (and of their float32 products) are exact for the
+// magnitudes in play, so running sums give scipy's axis-by-axis means bit for bit after the
+// float32 rounding; the mean is sum * (1/7) (within an ulp of float64 of scipy's division).
+constexpr double kInv7 = 1.0 / 7.0;
+constexpr int kSsTW = 64, kSsTH = 32;             // output tile; vertical sums for 70 columns
+constexpr int kSsVW = kSsTW + 6, kSsVS = 71;      // LDS row stride 71: conflict-free row segments
+
+// grid (tiles, B*C), block 256 = 4 waves.  Vertical pass: thread (column, 8-row segment) with
+// running sums straight from HBM/L2; horizontal pass: thread (row, 8-column segment) with
+// running sums over LDS.  ps[bc][tile] = sum of S over the tile's cropped pixels.
+__global__ __launch_bounds__(256) void ssim_rgb_kernel(const float* __restrict__ xt, const float* __restrict__ x,
+                                                       const float* __restrict__ mm, double* __restrict__ ps, int C,
+                                                       int H, int W, int tiles_x, int tiles, int chunks) {
+  __shared__ float v[5][kSsTH][kSsVS];             // axis-0 window means of x, y, xx, yy, xy
+  __shared__ double red[4];
+  __shared__ float cst[2];
+  const int tile = blockIdx.x, bc = blockIdx.y, b = bc / C;
+  const int i0 = (tile / tiles_x) * kSsTH, j0 = (tile % tiles_x) * kSsTW;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (wv == 0) {
+    const float R = ssim_range_wave(mm, b, chunks, lane);
+    if (lane == 0) { cst[0] = (0.01f * R) * (0.01f * R); cst[1] = (0.03f * R) * (0.03f * R); }
+  }
+  const float* pa = xt + (size_t)bc * H * W;
+  const float* pb = x + (size_t)bc * H * W;
+  // ---- vertical: columns j0-3+c (c < 70), rows i0 + 8*wv .. +8 ----
+  for (int c = lane; c < kSsVW; c += 64) {
+    const int gj = min(max(j0 - 3 + c, 0), W - 1);
+    const int r0 = i0 + 8 * wv;
+    double s0 = 0, s1 = 0, s2 = 0, s3 = 0, s4 = 0;
+    float ra[14], rb[14];
+#pragma unroll
+    for (int d = 0; d < 14; ++d) {
+      const int gi = min(max(r0 - 3 + d, 0), H - 1);
+      ra[d] = pa[(size_t)gi * W + gj];
+      rb[d] = pb[(size_t)gi * W + gj];
+    }
+#pragma unroll
+    for (int d = 0; d < 7; ++d) {
+      s0 += ra[d]; s1 += rb[d]; s2 += ra[d] * ra[d]; s3 += rb[d] * rb[d]; s4 += ra[d] * rb[d];
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (k) {
+        const float na = ra[k + 6], nb = rb[k + 6], oa = ra[k - 1], ob = rb[k - 1];
+        s0 += (double)na - (double)oa;
+        s1 += (double)nb - (double)ob;
+        s2 += (double)(na * na) - (double)(oa * oa);
+        s3 += (double)(nb * nb) - (double)(ob * ob);
+        s4 += (double)(na * nb) - (double)(oa * ob);
+      }
+      const int r = 8 * wv + k;
+      v[0][r][c] = (float)(s0 * kInv7);
+      v[1][r][c] = (float)(s1 * kInv7);
+      v[2][r][c] = (float)(s2 * kInv7);
+      v[3][r][c] = (float)(s3 * kInv7);
+      v[4][r][c] = (float)(s4 * kInv7);
+    }
+  }
+  __syncthreads();
+  // ---- horizontal + SSIM map: row r = t / 8, columns 8*(t % 8) .. +8 ----
+  const int r = threadIdx.x >> 3, c0 = (threadIdx.x & 7) * 8;
+  const int i = i0 + r;
+  const float C1 = cst[0], C2 = cst[1];
+  double acc = 0;
+  if (i >= 3 && i < H - 3) {
+    double h[5];
+#pragma unroll
+    for (int u = 0; u < 5; ++u) {
+      double t = 0;
+#pragma unroll
+      for (int d = 0; d < 7; ++d) t += v[u][r][c0 + d];
+      h[u] = t;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (k) {
+#pragma unroll
+        for (int u = 0; u < 5; ++u) h[u] += (double)v[u][r][c0 + k + 6] - (double)v[u][r][c0 + k - 1];
+      }
+      const int j = j0 + c0 + k;
+      if (j >= 3 && j < W - 3)
+        acc += (double)ssim_s((float)(h[0] * kInv7), (float)(h[1] * kInv7), (float)(h[2] * kInv7),
+                              (float)(h[3] * kInv7), (float)(h[4] * kInv7), 49.f / 48.f, C1, C2);
+    }
+  }
+  acc = block_sum(acc, red);
+  if (threadIdx.x == 0) ps[(size_t)bc * tiles + tile] = acc;
+}
+
+// grayscale: grid (ceil(H/4), B), one wave per row; rows[b][row] = mean S of the row (float32)
+__global__ __launch_bounds__(256) void ssim_gray_kernel(const float* __restrict__ xt, const float* __restrict__ x,
+                                                        const float* __restrict__ mm, float* __restrict__ rows,
+                                                        int H, int W, int chunks) {
+  const int b = blockIdx.y, row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= H) return;
+  const float R = ssim_range_wave(mm, b, chunks, lane);
+  const float C1 = (0.01f * R) * (0.01f * R), C2 = (0.03f * R) * (0.03f * R);
+  const float* a = xt + ((size_t)b * H + row) * W;
+  const float* e = x + ((size_t)b * H + row) * W;
+  double acc = 0;
+  for (int j = 3 + lane; j < W - 3; j += 64) {
+    double s[5] = {0, 0, 0, 0, 0};
+#pragma unroll
+    for (int d = -3; d <= 3; ++d) {
+      const float p = a[j + d], q = e[j + d];
+      s[0] += p; s[1] += q; s[2] += p * p; s[3] += q * q; s[4] += p * q;
+    }
+    acc += (double)ssim_s((float)(s[0] * kInv7), (float)(s[1] * kInv7), (float)(s[2] * kInv7),
+                          (float)(s[3] * kInv7), (float)(s[4] * kInv7), 7.f / 6.f, C1, C2);
+  }
+  acc = wave_sum(acc);
+  if (lane == 0) rows[(size_t)b * H + row] = (float)(acc / (double)(W - 6));
+}
+
+// per image: RGB mean over channels of (sum S / cropped count); gray mean over rows
+__global__ __launch_bounds__(256) void ssim_final_kernel(const double* __restrict__ ps, const float* __restrict__ rows,
+                                                         double* __restrict__ metrics, int C, int H, int W, int tiles,
+                                                         int gray, int it, int cap) {
+  __shared__ double red[4];
+  const int b = blockIdx.x;
+  double val;
+  if (gray) {
+    double a = 0;
+    for (int r = threadIdx.x; r < H; r += 256) a += rows[(size_t)b * H + r];
+    val = block_sum(a, red) / H;
+  } else {
+    const double cnt = (double)(H - 6) * (double)(W - 6);
+    double m = 0;
+    for (int c = 0; c < C; ++c) {
+      double a = 0;
+      for (int t = threadIdx.x; t < tiles; t += 256) a += ps[((size_t)b * C + c) * tiles + t];
+      m += (double)(float)(block_sum(a, red) / cnt);   // each channel's mssim is stored as float32
+    }
+    val = m / C;
+  }
+  if (threadIdx.x == 0) metrics[((size_t)b * cap + it) * kMetrics + 2] = (double)(float)val;
+}
+
+// =====================================================================================
 // comparisonB-2 (ADMM with denoiser, iteration.py:127-132, admm.py:30-44): elementwise
 // linear combinations and the per-image c_n / PSNR partial sums.
 // =====================================================================================
@@ -1006,6 +1211,36 @@ void launch_metrics(const float* xn, const float* xo, const float* xt, double* p
   const int chunks = chunk_count(n);
   hipLaunchKernelGGL(metric_partials_kernel, dim3(chunks, B), dim3(256), 0, st, xn, xo, xt, partials, n, chunks);
   hipLaunchKernelGGL(k3_metrics, dim3(B), dim3(256), 0, st, partials, chunks, n, metrics, it, cap, xt ? 1 : 0);
+}
+
+}  // namespace pnp
+
+namespace pnp {
+
+size_t ssim_scratch_bytes(int B, int C, int H, int W) {
+  const size_t n = (size_t)C * H * W;
+  const int tiles = ((W + kSsTW - 1) / kSsTW) * ((H + kSsTH - 1) / kSsTH);
+  return (size_t)B * chunk_count(n) * 2 * sizeof(float) + (size_t)B * C * tiles * sizeof(double) +
+         (size_t)B * H * sizeof(float) + 256;
+}
+
+void launch_ssim(const float* xt, const float* x, void* scratch, double* metrics, int B, int C, int H, int W,
+                 int it, int cap, hipStream_t st) {
+  const size_t n = (size_t)C * H * W;
+  const int chunks = chunk_count(n);
+  const int tx = (W + kSsTW - 1) / kSsTW, tiles = tx * ((H + kSsTH - 1) / kSsTH);
+  float* mm = static_cast<float*>(scratch);
+  double* ps = reinterpret_cast<double*>(
+      (reinterpret_cast<uintptr_t>(mm + (size_t)B * chunks * 2) + 255) & ~(uintptr_t)255);
+  float* rows = reinterpret_cast<float*>(ps + (size_t)B * C * tiles);
+  hipLaunchKernelGGL(ssim_minmax_kernel, dim3(chunks, B), dim3(256), 0, st, x, mm, n, chunks);
+  const int gray = C == 1;
+  if (gray)
+    hipLaunchKernelGGL(ssim_gray_kernel, dim3((H + 3) / 4, B), dim3(256), 0, st, xt, x, mm, rows, H, W, chunks);
+  else
+    hipLaunchKernelGGL(ssim_rgb_kernel, dim3(tiles, B * C), dim3(256), 0, st, xt, x, mm, ps, C, H, W, tx, tiles,
+                       chunks);
+  hipLaunchKernelGGL(ssim_final_kernel, dim3(B), dim3(256), 0, st, ps, rows, metrics, C, H, W, tiles, gray, it, cap);
 }
 
 }  // namespace pnp

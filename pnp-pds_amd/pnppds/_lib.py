@@ -35,9 +35,11 @@ class pnp_params(C.Structure):
     _fields_ = [("gamma1", C.c_double), ("gamma2", C.c_double), ("alpha_s", C.c_double),
                 ("alpha_n", C.c_double), ("my_lambda", C.c_double), ("m1", C.c_int32), ("m2", C.c_int32),
                 ("gamma_in_admm_step1", C.c_double), ("gaussian_nl", C.c_double), ("sp_nl", C.c_double),
-                ("poisson_alpha", C.c_double), ("r", C.c_double), ("record_metrics", C.c_int32)]
+                ("poisson_alpha", C.c_double), ("r", C.c_double), ("record_metrics", C.c_int32),
+                ("record_ssim", C.c_int32)]
 
 
+ABI_VERSION = 2   # include/pnppds.h PNP_ABI_VERSION
 _lib = None
 _lock = threading.Lock()
 
@@ -56,13 +58,13 @@ _SIGS = {
     "pnp_set_tuning": ([_P, C.c_int, C.c_int], C.c_int),
     "pnp_set_operator": ([_P, C.c_int, _D, C.c_int, C.c_int, C.POINTER(C.c_uint8), C.c_int, C.c_int], C.c_int),
     "pnp_run": ([_P, C.c_int, C.POINTER(pnp_params), C.c_int, C.c_int, C.c_int, C.c_int, _F, _F, _F, C.c_int,
-                 _F, _F, _D, _D, _D], C.c_int),
+                 _F, _F, _D, _D, _D, _D], C.c_int),
     "pnp_solver_setup": ([_P, C.c_int, C.POINTER(pnp_params), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int],
                          C.c_int),
     "pnp_solver_load": ([_P, _F, _F, _F], C.c_int),
     "pnp_solver_load_device": ([_P, _P, _P, _P], C.c_int),
     "pnp_solver_iterate": ([_P, C.c_int], C.c_int),
-    "pnp_solver_fetch": ([_P, _F, _F, _D, _D], C.c_int),
+    "pnp_solver_fetch": ([_P, _F, _F, _D, _D, _D], C.c_int),
     "pnp_solver_iterations_done": ([_P, C.POINTER(C.c_int)], C.c_int),
     "pnp_solver_state": ([_P, C.POINTER(_P), C.POINTER(_P), C.POINTER(_P)], C.c_int),
     "pnp_profile_enable": ([_P, C.c_int], C.c_int),
@@ -76,6 +78,7 @@ _SIGS = {
     "pnp_op_prox_gkl": ([_P, _P, _P, _P, C.c_int64, C.c_double, C.c_double, _P], C.c_int),
     "pnp_op_denoise": ([_P, _P, _P, C.c_int, C.c_int, C.c_int, C.c_int, _P], C.c_int),
     "pnp_op_psnr": ([_P, _P, _P, C.c_int, C.c_int64, _D, _P], C.c_int),
+    "pnp_op_ssim": ([_P, _P, _P, C.c_int, C.c_int, C.c_int, C.c_int, _D, _P], C.c_int),
 }
 
 
@@ -92,7 +95,7 @@ def load_library(path: str = LIB_PATH):
                 fn = getattr(lib, name)
                 fn.argtypes = args
                 fn.restype = res
-            if lib.pnp_abi_version() != 1:
+            if lib.pnp_abi_version() != ABI_VERSION:
                 raise RuntimeError("libpnppds ABI mismatch")
             _lib = lib
     return _lib
@@ -198,11 +201,12 @@ class Context:
         s_out = np.empty_like(x0) if want_s else None
         c_out = np.empty((B, max_iter), np.float64)
         p_out = np.empty((B, max_iter), np.float64)
+        m_out = np.empty((B, max_iter), np.float64)
         t = C.c_double(0)
         self._check(self.lib.pnp_run(self.h, method, C.byref(params), B, Cc, H, W, _fptr(x0), _fptr(xobs),
                                      _fptr(xtrue), max_iter, _fptr(x_out), _fptr(s_out), _dptr(c_out),
-                                     _dptr(p_out), C.byref(t)))
-        return x_out, s_out, c_out, p_out, t.value
+                                     _dptr(p_out), _dptr(m_out), C.byref(t)))
+        return x_out, s_out, c_out, p_out, m_out, t.value
 
     def solver_setup(self, method, params, B, Cc, H, W, cap):
         self._check(self.lib.pnp_solver_setup(self.h, method, C.byref(params), B, Cc, H, W, cap))
@@ -227,8 +231,9 @@ class Context:
         s = np.empty((B, Cc, H, W), np.float32)
         c = np.empty((B, max(self._cap, 0)), np.float64)
         p = np.empty((B, max(self._cap, 0)), np.float64)
-        self._check(self.lib.pnp_solver_fetch(self.h, _fptr(x), _fptr(s), _dptr(c), _dptr(p)))
-        return x, s, c, p
+        m = np.empty((B, max(self._cap, 0)), np.float64)
+        self._check(self.lib.pnp_solver_fetch(self.h, _fptr(x), _fptr(s), _dptr(c), _dptr(p), _dptr(m)))
+        return x, s, c, p, m
 
     def profile_enable(self, on=True):
         self._check(self.lib.pnp_profile_enable(self.h, 1 if on else 0))
@@ -265,6 +270,13 @@ class Context:
     def op_psnr(self, xt, x, B, n, stream=None):
         out = np.empty(B, np.float64)
         self._check(self.lib.pnp_op_psnr(self.h, _P(xt), _P(x), B, n, _dptr(out), _P(stream) if stream else None))
+        return out
+
+    def op_ssim(self, xt, x, B, Cc, H, W, stream=None):
+        """utils_eval.eval_ssim per image (Cc == 1: the reference's (H, W) grayscale arrays)."""
+        out = np.empty(B, np.float64)
+        self._check(self.lib.pnp_op_ssim(self.h, _P(xt), _P(x), B, Cc, H, W, _dptr(out),
+                                         _P(stream) if stream else None))
         return out
 
 

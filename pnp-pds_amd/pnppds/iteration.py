@@ -38,10 +38,11 @@ METHODS = {
 
 
 def make_params(gamma1, gamma2, alpha_s, alpha_n, myLambda, m1, m2, gammaInADMMStep1, gaussian_nl, sp_nl,
-                poisson_alpha, r, record_metrics=True) -> _lib.pnp_params:
+                poisson_alpha, r, record_metrics=True, record_ssim=True) -> _lib.pnp_params:
     return _lib.pnp_params(float(gamma1), float(gamma2), float(alpha_s), float(alpha_n), float(myLambda),
                            int(m1), int(m2), float(gammaInADMMStep1), float(gaussian_nl), float(sp_nl),
-                           float(poisson_alpha), float(r), 1 if record_metrics else 0)
+                           float(poisson_alpha), float(r), 1 if record_metrics else 0,
+                           1 if (record_metrics and record_ssim) else 0)
 
 
 def resolve_method(method: str) -> int:
@@ -68,9 +69,11 @@ def _check_ops(phi, adj_phi):
 
 def test_iter_batch(x_0, x_obsrv, x_true, phi, adj_phi, gamma1, gamma2, alpha_s, alpha_n, myLambda, m1, m2,
                     gammaInADMMStep1, gaussian_nl, sp_nl, poisson_alpha, path_prox, max_iter,
-                    method="A-Proposed", ch=3, r=1, record_metrics=True, ctx=None):
+                    method="A-Proposed", ch=3, r=1, record_metrics=True, record_ssim=True, ctx=None):
     """Batched test_iter over B independent images: arrays are [B, C, H, W].
-    Returns (x[B,C,H,W] f32, s+0.5 [B,C,H,W] f32, c[B,max_iter], psnr[B,max_iter], ssim, avg_time)."""
+    Returns (x[B,C,H,W] f32, s+0.5 [B,C,H,W] f32, c[B,max_iter], psnr[B,max_iter], ssim[B,max_iter],
+    avg_time).  ssim is computed on the device each iteration (iteration.py:189) when record_ssim;
+    C == 1 batches are scored as the reference's (H, W) grayscale arrays."""
     m = resolve_method(method)
     _check_ops(phi, adj_phi)
     x0 = np.asarray(x_0)
@@ -84,11 +87,10 @@ def test_iter_batch(x_0, x_obsrv, x_true, phi, adj_phi, gamma1, gamma2, alpha_s,
     den.configure(ctx)
     phi.configure(ctx, H, W)
     prm = make_params(gamma1, gamma2, alpha_s, alpha_n, myLambda, m1, m2, gammaInADMMStep1, gaussian_nl, sp_nl,
-                      poisson_alpha, r, record_metrics)
+                      poisson_alpha, r, record_metrics, record_ssim)
     xt = None if x_true is None else np.broadcast_to(np.asarray(x_true, np.float32), x0.shape)
     xo = np.broadcast_to(np.asarray(x_obsrv, np.float32), x0.shape)
-    x, s, c, psnr, t = ctx.run(m, prm, x0, xo, xt, int(max_iter))
-    ssim = np.full((B, int(max_iter)), np.nan)
+    x, s, c, psnr, ssim, t = ctx.run(m, prm, x0, xo, xt, int(max_iter))
     return x, s, c, psnr, ssim, t
 
 

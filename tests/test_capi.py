@@ -29,7 +29,7 @@ def lib():
 def test_header_declares_entry_points():
     syms = declared_symbols()
     for s in ("pnp_create", "pnp_run", "pnp_set_denoiser", "pnp_set_operator", "pnp_op_denoise",
-              "pnp_op_proj_l1_ball", "pnp_op_proj_l2_ball", "pnp_op_prox_gkl", "pnp_solver_iterate"):
+              "pnp_op_proj_l1_ball", "pnp_op_proj_l2_ball", "pnp_op_prox_gkl", "pnp_solver_iterate", "pnp_op_ssim"):
         assert s in syms
     assert len(syms) >= 25
 
@@ -55,7 +55,8 @@ def test_exports_are_plain_c(lib):
 
 
 def test_abi_version_and_errors_without_gpu(lib):
-    assert lib.pnp_abi_version() == 1
+    from pnppds import _lib
+    assert lib.pnp_abi_version() == _lib.ABI_VERSION == 2
     lib.pnp_last_error.restype = ctypes.c_char_p
     h = ctypes.c_void_p()
     rc = lib.pnp_create(0, ctypes.byref(h))
@@ -72,9 +73,10 @@ def test_null_context_is_rejected(lib):
 
 def test_params_struct_layout():
     from pnppds import _lib
-    # 5 doubles, 2 int32, 5 doubles, 1 int32 (+4 padding) as in pnppds.h
+    # 5 doubles, 2 int32, 5 doubles, 2 int32 as in pnppds.h
     assert ctypes.sizeof(_lib.pnp_params) == 8 * 5 + 4 * 2 + 8 * 5 + 8
     assert _lib.pnp_params.m1.offset == 40 and _lib.pnp_params.gamma_in_admm_step1.offset == 48
+    assert _lib.pnp_params.record_metrics.offset == 88 and _lib.pnp_params.record_ssim.offset == 92
 
 
 def test_product_does_not_import_oracle():
