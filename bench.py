@@ -166,15 +166,13 @@ def main():
     h = load_blur_kernel("blur_1")
     ctx.set_operator(_lib.OP_BLUR, h=h)
 
-    # ---- synthetic inputs, degraded on the device: x_obs = Phi(x_true) + sigma * n -------------
+    # ---- synthetic inputs, degraded on the device exactly as main.py:49-64 does ---------------
     t0 = time.perf_counter()
     x_true = synthetic_batch(B, C, H, W, seed=1000 * rank + 1)
     d_true = torch.from_numpy(x_true).cuda(local)
     d_obs = torch.empty_like(d_true)
-    ctx.op_phi(d_true.data_ptr(), d_obs.data_ptr(), B, C, H, W)
-    ctx.synchronize()
-    gen = torch.Generator(device=f"cuda:{local}").manual_seed(1234 + rank)
-    d_obs += SIGMA * torch.randn(d_obs.shape, device=f"cuda:{local}", generator=gen)
+    ctx.degrade(_lib.pnp_degrade_params(SIGMA, 0.0, 300.0, 0, 1234), d_true.data_ptr(), B, C, H, W,
+                xobs=d_obs.data_ptr())           # blur_1 + 0.01 * np.random.seed(1234) randn
     torch.cuda.synchronize()
     log(f"[rank {rank}] inputs ready in {time.perf_counter() - t0:.1f}s")
 
@@ -241,7 +239,8 @@ def main():
             "n_gpus": world, "steps": K, "warmup": Wm,
             "ms_per_step": round(1e3 * t_el / K, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "fp16-mfma/fp32-acc+state",
-            "data": "synthetic structured RGB images, x_obs = blur_1(x_true) + 0.01 N(0,1) on device; real "
+            "data": "synthetic structured RGB images, x_obs = blur_1(x_true) + 0.01 randn of np.random.seed(1234) "
+                    "(main.py:49-64, generated on device); real "
                     "DnCNN_nobn_nch_3_nlev_0.01 weights",
             "config": {"workload": f"ours-A (A-Proposed) blur, batch={B}/GPU RGB {H}x{W}", "global_batch": B * world,
                        "image": f"{C}x{H}x{W}", "deg_op": "blur_1", "method": "ours-A",

@@ -45,7 +45,8 @@ enum pnp_status {
   PNP_E_UNSUPPORTED = -2, /* method / operator / denoiser shape not supported          */
   PNP_E_HIP = -3,         /* HIP runtime error (message has the hipError string)      */
   PNP_E_OOM = -4,         /* device allocation failed                                 */
-  PNP_E_STATE = -5        /* call out of order (e.g. iterate before load)             */
+  PNP_E_STATE = -5,       /* call out of order (e.g. iterate before load)             */
+  PNP_E_INTERNAL = -6     /* internal limit reached (message says which)              */
 };
 
 /* iteration.py:48-63 ('A-Proposed' / 'B-Proposed' / 'C-Proposed'; README: ours-A/B/C)
@@ -165,6 +166,22 @@ int pnp_op_denoise(pnp_ctx* ctx, const float* x, float* out, int B, int C, int H
 /* psnr_out: host array of B doubles (synchronous). */
 int pnp_op_psnr(pnp_ctx* ctx, const float* x_true, const float* x, int B, int64_t n, double* psnr_out,
                 void* stream);
+
+/* ---- observation pipeline (main.py:49-64, utils/utils_noise.py) ------------------ */
+typedef struct pnp_degrade_params {
+  double gaussian_nl;      /* sigma of add_gaussian_noise (0: no Gaussian noise)          */
+  double sp_nl;            /* add_salt_and_pepper_noise rate (0: none)                     */
+  double poisson_alpha;    /* apply_poisson_noise scale                                    */
+  int32_t poisson_noise;   /* 1: Poisson noise, and x_0 = x_obs / poisson_alpha            */
+  uint32_t seed;           /* np.random.seed of utils_noise.py (1234)                      */
+} pnp_degrade_params;
+/* x_obs = SP(Poisson(Phi(x_true) + M(sigma g))) with the operator set by pnp_set_operator,
+ * reproducing numpy's legacy RandomState draws (every image gets the reference's noise
+ * field, as main.py reseeds per image).  Device pointers, B*C*H*W each; C is 1 ((H,W)
+ * gray) or 3.  Outputs may be NULL: d_xobs / d_x0 float32, d_xobs64 the float64 x_obs the
+ * reference hands to test_iter.  Synchronous on `stream`.                               */
+int pnp_degrade(pnp_ctx* ctx, const pnp_degrade_params* p, int B, int C, int H, int W,
+                const float* d_xtrue, float* d_xobs, float* d_x0, double* d_xobs64, void* stream);
 
 /* utils_eval.py:9-12 eval_ssim per image: skimage structural_similarity(x_true, x,
  * data_range = x.max() - x.min(), channel_axis = 0) with scikit-image 0.22 defaults.

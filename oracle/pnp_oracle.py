@@ -159,6 +159,65 @@ def ssim(x_true, x):
 
 
 # ---------------------------------------------------------------------------
+# Observation pipeline (main.py:49-64, utils/utils_noise.py) — numpy legacy RandomState,
+# the generator the reference itself calls (numpy's legacy stream is frozen across versions).
+# ---------------------------------------------------------------------------
+def add_gaussian_noise(img, noise_level, op):
+    """utils_noise.py:35-38."""
+    rs = np.random.RandomState(1234)
+    return img + op(noise_level * rs.randn(*img.shape))
+
+
+def apply_poisson_noise(img, alpha):
+    """utils_noise.py:40-43."""
+    rs = np.random.RandomState(1234)
+    return rs.poisson(img * alpha)
+
+
+def add_salt_and_pepper_noise(img, noise_level, op):
+    """utils_noise.py:3-33, with the O(n^2) list membership replaced by a set.  The loop's
+    ``i=i-1`` has no effect in a Python for-loop: exactly 2*noise_cnt pairs are drawn, the
+    accepted ones (target pixel == 1, first occurrence) become 0 (first noise_cnt) or 1.
+    Both coordinates are drawn in [0, img.shape[-2]) and keyed x*shape[-2]+y (as shipped)."""
+    H, W = img.shape[-2], img.shape[-1]
+    noise_cnt = int(H * W * noise_level / 2)
+    target = op(np.ones([H, W]))
+    rs = np.random.RandomState(1234)
+    seen, xs, ys = set(), [], []
+    for _ in range(noise_cnt * 2):
+        x = rs.randint(0, H)
+        y = rs.randint(0, H)
+        key = x * H + y
+        if target[x][y] == 1 and key not in seen:
+            seen.add(key)
+            xs.append(x)
+            ys.append(y)
+    xs, ys = np.array(xs, dtype=np.int64), np.array(ys, dtype=np.int64)
+    out = np.copy(img)
+    planes = [out] if out.ndim == 2 else [out[c] for c in range(3)]
+    for pl in planes:
+        pl[(xs[:noise_cnt], ys[:noise_cnt])] = 0
+        pl[(xs[noise_cnt:], ys[noise_cnt:])] = 1
+    return out
+
+
+def make_observation(x_true, deg_op, h, r, gaussian_nl, sp_nl, poisson_noise, poisson_alpha):
+    """main.py:49-64: returns (img_obsrv, x_0) with the reference's dtypes."""
+    phi, _ = observation_operators(deg_op, h, r)
+    ident = (lambda v: v)
+    noise_op = ident if deg_op in ("blur", "Id") else phi
+    obs = phi(x_true)
+    obs = add_gaussian_noise(obs, gaussian_nl, noise_op)
+    if poisson_noise:
+        obs = apply_poisson_noise(obs, poisson_alpha)
+    obs = add_salt_and_pepper_noise(obs, sp_nl, noise_op)
+    x0 = np.copy(obs)
+    if poisson_noise:
+        x0 = x0 / poisson_alpha
+    return obs, x0
+
+
+# ---------------------------------------------------------------------------
 # Denoiser (models/denoiser.py:34-46, models/basic_models.py:25-38,
 #           KAIR variant models/network_dncnn.py:42-77)
 # ---------------------------------------------------------------------------

@@ -57,7 +57,7 @@ struct pnp_ctx {
   int op_kind = PNP_OP_ID;
   int op_H = 0, op_W = 0;
   int op_ntaps = 0, op_R = 0, op_taps_id = 0;
-  DevBuf taps_fwd, taps_adj, mask, dense_fwd, dense_adj;
+  DevBuf taps_fwd, taps_adj, mask, dense_fwd, dense_adj, taps64;
 
   // solver
   int method = -1, B = 0, C = 0, H = 0, W = 0, cap = 0, it = 0;
@@ -67,6 +67,11 @@ struct pnp_ctx {
   DevBuf x[2], y, s, w, xobs, xtrue, u32, u16, act[2], partials, metrics, theta;
   DevBuf z, p, t;   // comparisonB-2 only
   DevBuf ssim_scr;  // SSIM partials (record_ssim)
+
+  // observation pipeline (pnp_degrade)
+  DevBuf dg_words, dg_flag, dg_rank, dg_scan, dg_noise, dg_img, dg_draws, dg_first, dg_status;
+  size_t dg_nwords = 0;
+  uint32_t dg_seed = 0;
 
   // scratch for single ops
   DevBuf scr_u32, scr_u16, scr_act[2], scr_part, scr_theta;
@@ -545,7 +550,9 @@ int pnp_destroy(pnp_ctx* ctx) {
                     &ctx->w, &ctx->xobs, &ctx->xtrue, &ctx->u32, &ctx->u16, &ctx->act[0], &ctx->act[1],
                     &ctx->partials, &ctx->metrics, &ctx->theta, &ctx->scr_u32, &ctx->scr_u16,
                     &ctx->scr_act[0], &ctx->scr_act[1], &ctx->scr_part, &ctx->scr_theta,
-                    &ctx->z, &ctx->p, &ctx->t, &ctx->dense_fwd, &ctx->dense_adj, &ctx->ssim_scr};
+                    &ctx->z, &ctx->p, &ctx->t, &ctx->dense_fwd, &ctx->dense_adj, &ctx->ssim_scr,
+                    &ctx->taps64, &ctx->dg_words, &ctx->dg_flag, &ctx->dg_rank, &ctx->dg_scan, &ctx->dg_noise,
+                    &ctx->dg_img, &ctx->dg_draws, &ctx->dg_first, &ctx->dg_status};
   for (DevBuf* b : bufs) release(*b);
   for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -652,6 +659,7 @@ int pnp_set_operator(pnp_ctx* ctx, int kind, const double* h, int kh, int kw, co
       //                    Phi^T y[i,j] = sum h[a,b] x[i + a - ma, j + b - ma], ma = l//2
       const int l = kh, mf = (l - 1) / 2, ma = l / 2;
       std::vector<int4> fwd, adj;
+      std::vector<Tap64> f64;
       int R = 0;
       for (int a = 0; a < kh; ++a)
         for (int b = 0; b < kw; ++b) {
@@ -661,6 +669,7 @@ int pnp_set_operator(pnp_ctx* ctx, int kind, const double* h, int kh, int kw, co
           int bits;
           std::memcpy(&bits, &fv, 4);
           fwd.push_back(make_int4(mf - a, mf - b, bits, 0));
+          f64.push_back(Tap64{mf - a, mf - b, v});
           adj.push_back(make_int4(a - ma, b - ma, bits, 0));
           R = std::max({R, std::abs(mf - a), std::abs(mf - b), std::abs(a - ma), std::abs(b - ma)});
         }
@@ -694,6 +703,9 @@ int pnp_set_operator(pnp_ctx* ctx, int kind, const double* h, int kh, int kw, co
         HIPCHK(ctx, hipMemcpy(ctx->dense_fwd.p, pf.data(), pf.size() * sizeof(float), hipMemcpyHostToDevice));
         HIPCHK(ctx, hipMemcpy(ctx->dense_adj.p, pa.data(), pa.size() * sizeof(float), hipMemcpyHostToDevice));
       }
+      if (f64.empty()) f64.push_back(Tap64{0, 0, 0.0});
+      ensure(ctx, ctx->taps64, f64.size() * sizeof(Tap64));
+      HIPCHK(ctx, hipMemcpy(ctx->taps64.p, f64.data(), f64.size() * sizeof(Tap64), hipMemcpyHostToDevice));
       ctx->op_ntaps = (int)fwd.size();
       ctx->op_R = R;
       ctx->op_kind = kind;
@@ -955,6 +967,125 @@ int pnp_op_ssim(pnp_ctx* ctx, const float* x_true, const float* x, int B, int C,
     HIPCHK(ctx, hipMemcpyAsync(h.data(), m, h.size() * sizeof(double), hipMemcpyDeviceToHost, st));
     HIPCHK(ctx, hipStreamSynchronize(st));
     for (int b = 0; b < B; ++b) ssim_out[b] = h[(size_t)b * kMetrics + 2];
+  });
+}
+
+// main.py:49-64 on the device; see degrade.hip for the numpy-stream restatement.
+int pnp_degrade(pnp_ctx* ctx, const pnp_degrade_params* p, int B, int C, int H, int W, const float* d_xtrue,
+                float* d_xobs, float* d_x0, double* d_xobs64, void* stream) {
+  if (!ctx) return PNP_E_ARG;
+  return guarded(ctx, [&] {
+    if (!p || !d_xtrue || (!d_xobs && !d_x0 && !d_xobs64)) fail(ctx, PNP_E_ARG, "bad arguments");
+    if (B < 1 || H < 1 || W < 1 || (C != 1 && C != 3))
+      fail(ctx, PNP_E_ARG, "bad shape B=%d C=%d H=%d W=%d (utils_noise.py handles (H,W) and (3,H,W))", B, C, H, W);
+    if (p->poisson_noise && !(p->poisson_alpha > 0.0)) fail(ctx, PNP_E_ARG, "poisson_alpha must be > 0");
+    check_operator_shape(ctx, H, W);
+    hipStream_t st = pick_stream(ctx, stream);
+    const size_t n = (size_t)C * H * W, N = (size_t)B * n;
+    const int noise_cnt = (int)((double)H * W * p->sp_nl / 2.0);      // utils_noise.py:4
+    const size_t npairs = noise_cnt > 0 ? 2 * (size_t)noise_cnt : 0;  // utils_noise.py:11
+    const size_t ndraw = 2 * npairs;
+    const size_t half = (n + 1) / 2, ncand = half + half / 2 + 4096;  // legacy_gauss acceptance pi/4
+    const uint32_t rng = (uint32_t)(H - 1);                           // randint(0, img.shape[-2])
+    uint32_t mask = rng;
+    for (int sh = 1; sh < 32; sh <<= 1) mask |= mask >> sh;
+    size_t want = 0;
+    if (p->gaussian_nl != 0.0) want = std::max(want, 4 * ncand);
+    if (npairs && rng) want = std::max(want, 3 * ndraw + 4096);
+    if (p->poisson_noise) want = std::max(want, 6 * n + 65536);
+    const size_t scan_n = std::max({ncand, want, npairs, (size_t)1});
+    ensure(ctx, ctx->dg_flag, scan_n * 4);
+    ensure(ctx, ctx->dg_rank, scan_n * 4);
+    ensure(ctx, ctx->dg_scan, scan_scratch_words(scan_n) * 4);
+    ensure(ctx, ctx->dg_noise, n * sizeof(double));
+    ensure(ctx, ctx->dg_img, N * sizeof(double));
+    ensure(ctx, ctx->dg_status, 2 * sizeof(unsigned long long));
+    auto stream_words = [&](size_t nw) {       // the tempered MT19937 stream of np.random.seed(seed)
+      nw = (nw + kMtBlock - 1) / kMtBlock * kMtBlock;
+      if (ctx->dg_nwords >= nw && ctx->dg_seed == p->seed) return;
+      ensure(ctx, ctx->dg_words, nw * 4);
+      launch_mt_stream(p->seed, P<uint32_t>(ctx->dg_words), nw, st);
+      check_launch(ctx, "mt_stream");
+      ctx->dg_nwords = nw;
+      ctx->dg_seed = p->seed;
+    };
+    auto read_status = [&](unsigned long long* h) {
+      HIPCHK(ctx, hipMemcpyAsync(h, ctx->dg_status.p, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+      HIPCHK(ctx, hipStreamSynchronize(st));
+    };
+    stream_words(std::max(want, (size_t)kMtBlock));
+    // 1) x_obs = Phi(x_true) + M(sigma randn)        utils_noise.py:35-38
+    const double* noise = nullptr;
+    if (p->gaussian_nl != 0.0) {
+      launch_gauss(P<uint32_t>(ctx->dg_words), ncand, P<uint32_t>(ctx->dg_flag), P<uint32_t>(ctx->dg_rank),
+                   P<uint32_t>(ctx->dg_scan), P<double>(ctx->dg_noise), n, st);
+      check_launch(ctx, "gauss");
+      uint32_t acc = 0;
+      HIPCHK(ctx, hipMemcpyAsync(&acc, ctx->dg_scan.p, 4, hipMemcpyDeviceToHost, st));
+      HIPCHK(ctx, hipStreamSynchronize(st));
+      if (acc < half) fail(ctx, PNP_E_INTERNAL, "gaussian stream too short (%u of %zu pairs)", acc, half);
+      noise = P<double>(ctx->dg_noise);
+    }
+    const OpDesc od = op_desc(ctx);
+    for (int attempt = 0;; ++attempt) {
+      launch_observe(d_xtrue, noise, P<Tap64>(ctx->taps64), ctx->op_ntaps, od.mask, ctx->op_kind, p->gaussian_nl,
+                     P<double>(ctx->dg_img), B, C, H, W, st);
+      check_launch(ctx, "observe");
+      if (!p->poisson_noise) break;
+      // 2) x_obs = poisson(alpha x_obs)              utils_noise.py:40-43
+      HIPCHK(ctx, hipMemsetAsync(ctx->dg_status.p, 0, 2 * sizeof(unsigned long long), st));
+      launch_poisson(P<uint32_t>(ctx->dg_words), ctx->dg_nwords, P<double>(ctx->dg_img), B, n, p->poisson_alpha,
+                     P<unsigned long long>(ctx->dg_status), st);
+      check_launch(ctx, "poisson");
+      unsigned long long hs[2];
+      read_status(hs);
+      if (hs[0] == 1) fail(ctx, PNP_E_ARG, "poisson: lam < 0 or NaN (numpy raises ValueError)");
+      if (hs[0] == 2) fail(ctx, PNP_E_ARG, "poisson: lam value too large");
+      if (hs[0] != 3) break;
+      if (attempt >= 6) fail(ctx, PNP_E_INTERNAL, "poisson stream exhausted");
+      stream_words(2 * ctx->dg_nwords);            // deterministic: a longer prefix of the same stream
+    }
+    // 3) salt & pepper                               utils_noise.py:3-33
+    if (npairs) {
+      const uint8_t* tgt = ctx->op_kind == PNP_OP_RANDOM_SAMPLING ? od.mask : nullptr;
+      const size_t side = (size_t)H * std::max(H, W);
+      ensure(ctx, ctx->dg_draws, ndraw * 4);
+      ensure(ctx, ctx->dg_first, side * 4);
+      HIPCHK(ctx, hipMemsetAsync(ctx->dg_first.p, 0xff, side * 4, st));
+      HIPCHK(ctx, hipMemsetAsync(ctx->dg_status.p, 0, 2 * sizeof(unsigned long long), st));
+      if (rng == 0) {
+        HIPCHK(ctx, hipMemsetAsync(ctx->dg_draws.p, 0, ndraw * 4, st));   // randint(0, 1) draws nothing
+      } else {
+        size_t nw = std::min(ctx->dg_nwords, 3 * ndraw + 4096);   // words scanned for the draws
+        for (int attempt = 0;; ++attempt) {
+          ensure(ctx, ctx->dg_flag, nw * 4);
+          ensure(ctx, ctx->dg_rank, nw * 4);
+          ensure(ctx, ctx->dg_scan, scan_scratch_words(nw) * 4);
+          launch_sp_draws(P<uint32_t>(ctx->dg_words), nw, mask, rng, P<uint32_t>(ctx->dg_flag),
+                          P<uint32_t>(ctx->dg_rank), P<uint32_t>(ctx->dg_scan), P<uint32_t>(ctx->dg_draws), ndraw, st);
+          check_launch(ctx, "sp_draws");
+          uint32_t valid = 0;
+          HIPCHK(ctx, hipMemcpyAsync(&valid, ctx->dg_scan.p, 4, hipMemcpyDeviceToHost, st));
+          HIPCHK(ctx, hipStreamSynchronize(st));
+          if (valid >= ndraw) break;
+          if (attempt >= 6) fail(ctx, PNP_E_INTERNAL, "salt-and-pepper stream exhausted");
+          nw *= 2;
+          stream_words(nw);
+        }
+      }
+      launch_sp_apply(P<uint32_t>(ctx->dg_draws), (int)npairs, tgt, H, W, P<uint32_t>(ctx->dg_first),
+                      P<uint32_t>(ctx->dg_flag), P<uint32_t>(ctx->dg_rank), P<uint32_t>(ctx->dg_scan), noise_cnt,
+                      P<double>(ctx->dg_img), B, C, P<unsigned long long>(ctx->dg_status), st);
+      check_launch(ctx, "sp_apply");
+      unsigned long long hs[2];
+      read_status(hs);
+      if (hs[0] == 4) fail(ctx, PNP_E_ARG, "salt-and-pepper: column index out of range (the reference draws "
+                                           "columns in [0, H) and raises IndexError when H > W)");
+    }
+    // 4) x_obs (float32 state of the solver), x_0 = x_obs (/ alpha)   main.py:62-64
+    launch_degrade_finalize(P<double>(ctx->dg_img), N, p->poisson_alpha, p->poisson_noise, d_xobs, d_x0, d_xobs64, st);
+    check_launch(ctx, "degrade_finalize");
+    HIPCHK(ctx, hipStreamSynchronize(st));
   });
 }
 

@@ -76,6 +76,30 @@ void launch_sqdiff(const float* a, const float* c, double* partials, int B, size
 void launch_shrink(const float* v, float* out, const float* theta, int B, size_t n, hipStream_t st);
 void launch_gkl(const float* x, const float* x0, float* out, size_t count, double gamma, double alpha,
                 hipStream_t st);
+// ---- observation pipeline (degrade.hip, main.py:49-64 + utils_noise.py) ----
+struct Tap64 {   // blur tap in float64: y[i,j] += v * x[(i+dy) mod H, (j+dx) mod W]
+  int dy, dx;
+  double v;
+};
+constexpr size_t kMtBlock = 624;   // MT19937 words per twist
+void launch_mt_stream(uint32_t seed, uint32_t* out, size_t nwords, hipStream_t st);
+size_t scan_scratch_words(size_t n);
+// exclusive prefix sum of n u32 flags; scratch[0] receives the total
+void launch_scan(const uint32_t* f, size_t n, uint32_t* out, uint32_t* scratch, hipStream_t st);
+void launch_gauss(const uint32_t* w, size_t ncand, uint32_t* flag, uint32_t* rank, uint32_t* scan_scr, double* noise,
+                  size_t n, hipStream_t st);
+void launch_observe(const float* xt, const double* noise, const Tap64* taps, int ntaps, const uint8_t* mask, int kind,
+                    double sigma, double* img, int B, int C, int H, int W, hipStream_t st);
+void launch_poisson(const uint32_t* w, size_t nwords, double* img, int B, size_t n, double alpha,
+                    unsigned long long* status, hipStream_t st);
+void launch_sp_draws(const uint32_t* w, size_t nw, uint32_t mask, uint32_t rng, uint32_t* flag, uint32_t* rank,
+                     uint32_t* scan_scr, uint32_t* draws, size_t ndraw, hipStream_t st);
+void launch_sp_apply(const uint32_t* draws, int npairs, const uint8_t* tgt, int H, int W, uint32_t* first,
+                     uint32_t* acc, uint32_t* rank, uint32_t* scan_scr, int noise_cnt, double* img, int B, int C,
+                     unsigned long long* status, hipStream_t st);
+void launch_degrade_finalize(const double* img, size_t N, double alpha, int poisson, float* xobs, float* x0,
+                             double* xobs64, hipStream_t st);
+
 // per-iteration metrics: metrics[b][it][kMetrics] = {c_n, PSNR, SSIM}
 constexpr int kMetrics = 3;
 // SSIM of x against xt (utils_eval.py:9-12) into metrics[b][it][2]; scratch >= ssim_scratch_bytes

@@ -16,7 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libpnppds.so")
 
 PNP_OK = 0
-ERRORS = {-1: "PNP_E_ARG", -2: "PNP_E_UNSUPPORTED", -3: "PNP_E_HIP", -4: "PNP_E_OOM", -5: "PNP_E_STATE"}
+ERRORS = {-1: "PNP_E_ARG", -2: "PNP_E_UNSUPPORTED", -3: "PNP_E_HIP", -4: "PNP_E_OOM", -5: "PNP_E_STATE", -6: "PNP_E_INTERNAL"}
 
 METHOD_A, METHOD_B, METHOD_C, METHOD_ADMM_B2 = 0, 1, 2, 3
 OP_ID, OP_BLUR, OP_RANDOM_SAMPLING = 0, 1, 2
@@ -40,6 +40,11 @@ class pnp_params(C.Structure):
 
 
 ABI_VERSION = 2   # include/pnppds.h PNP_ABI_VERSION
+class pnp_degrade_params(C.Structure):
+    _fields_ = [("gaussian_nl", C.c_double), ("sp_nl", C.c_double), ("poisson_alpha", C.c_double),
+                ("poisson_noise", C.c_int32), ("seed", C.c_uint32)]
+
+
 _lib = None
 _lock = threading.Lock()
 
@@ -78,6 +83,8 @@ _SIGS = {
     "pnp_op_prox_gkl": ([_P, _P, _P, _P, C.c_int64, C.c_double, C.c_double, _P], C.c_int),
     "pnp_op_denoise": ([_P, _P, _P, C.c_int, C.c_int, C.c_int, C.c_int, _P], C.c_int),
     "pnp_op_psnr": ([_P, _P, _P, C.c_int, C.c_int64, _D, _P], C.c_int),
+    "pnp_degrade": ([_P, C.POINTER(pnp_degrade_params), C.c_int, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P, _P],
+                    C.c_int),
     "pnp_op_ssim": ([_P, _P, _P, C.c_int, C.c_int, C.c_int, C.c_int, _D, _P], C.c_int),
 }
 
@@ -271,6 +278,13 @@ class Context:
         out = np.empty(B, np.float64)
         self._check(self.lib.pnp_op_psnr(self.h, _P(xt), _P(x), B, n, _dptr(out), _P(stream) if stream else None))
         return out
+
+    def degrade(self, params: "pnp_degrade_params", xt, B, Cc, H, W, xobs=None, x0=None, xobs64=None,
+                stream=None):
+        """main.py:49-64 on device pointers (ints); synchronous."""
+        self._check(self.lib.pnp_degrade(self.h, C.byref(params), B, Cc, H, W, _P(xt), _P(xobs) if xobs else None,
+                                         _P(x0) if x0 else None, _P(xobs64) if xobs64 else None,
+                                         _P(stream) if stream else None))
 
     def op_ssim(self, xt, x, B, Cc, H, W, stream=None):
         """utils_eval.eval_ssim per image (Cc == 1: the reference's (H, W) grayscale arrays)."""
