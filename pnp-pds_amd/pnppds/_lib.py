@@ -97,6 +97,10 @@ def load_library(path: str = LIB_PATH):
             if not os.path.exists(path):
                 raise RuntimeError(f"libpnppds.so not found at {path}; run `make -C pnp-pds_amd` "
                                    "(or __graft_entry__.build())")
+            try:   # torch ships its own HIP runtime under the same soname: load it first so the
+                import torch  # noqa: F401  process has one runtime (ours would shadow torch's)
+            except ImportError:
+                pass
             lib = C.CDLL(path)
             for name, (args, res) in _SIGS.items():
                 fn = getattr(lib, name)

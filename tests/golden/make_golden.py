@@ -189,5 +189,40 @@ def main(ref_root="/root/reference"):
     print(f"long_A_blur_256.npz psnr {res[3][0]:.3f} -> {res[3][-1]:.3f} ({time.perf_counter()-t:.1f}s)")
 
 
+def make_driver_golden(ref_root="/root/reference"):
+    """utils_textfile.py / utils_parse_args.py / utils_method_master.py outputs for fixed inputs
+    (tests/golden/driver.json): the CSV text of a synthetic ``datas`` dict and the argument
+    defaults, produced by the reference's own functions."""
+    import json
+    sys.path.insert(0, ref_root)
+    from utils import utils_textfile as tf
+    from utils import utils_parse_args as pa
+    from utils.utils_method_master import get_algorithm_denoiser
+    results = {i: {"filename": f"{i:02d}.png", "PSNR": 20.0 + i / 3, "SSIM": 0.5 + i / 7,
+                   "PSNR_observation": 15.0 + i / 9, "SSIM_observation": 0.25 + i / 11} for i in range(3)}
+    datas = {"experimental_settings": pa.parse_args_exp({"gaussian_nl": 0.01, "deg_op": "random_sampling"}),
+             "method": pa.parse_args_method({"method": "A-Proposed", "gamma1": 0.99, "alpha_n": 0.94}),
+             "configs": pa.parse_args_configs({}), "results": results}
+    from utils.utils_unparse_args import unparse_args_configs, unparse_args_exp, unparse_args_method
+    datas["experimental_settings"] = unparse_args_exp(*datas["experimental_settings"])
+    datas["method"] = unparse_args_method(*datas["method"])
+    datas["configs"] = unparse_args_configs(*datas["configs"])
+    alg, den = get_algorithm_denoiser("A-Proposed")
+    datas["summary"] = {"algorithm": alg, "denoiser": den, "Average_PSNR": 21.0, "Average_SSIM": 0.6}
+    out = {"datas": {k: v for k, v in datas.items() if k != "results"},
+           "results": [results[i] for i in range(3)],
+           "header": tf.get_csv_header(), "data": tf.get_csv_data(datas), "footer": tf.get_csv_footer(datas),
+           "defaults": {"exp": list(pa.parse_args_exp({})), "method": list(pa.parse_args_method({})),
+                        "configs": list(pa.parse_args_configs({}))},
+           "methods": {m: list(get_algorithm_denoiser(m)) for m in
+                       ("A-Proposed", "A-PDS-TV", "C-RED-DnCNN", "comparisonB-2", "nope")}}
+    with open(os.path.join(HERE, "driver.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    print("driver.json")
+
+
 if __name__ == "__main__":
-    main(*sys.argv[1:])
+    if len(sys.argv) > 1 and sys.argv[1] == "--driver":
+        make_driver_golden(*sys.argv[2:])
+    else:
+        main(*sys.argv[1:])
