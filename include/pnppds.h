@@ -55,7 +55,19 @@ enum pnp_method {
   PNP_METHOD_A = 0,       /* Gaussian noise, l2-ball data constraint                  */
   PNP_METHOD_B = 1,       /* Gaussian + sparse noise, l2 ball + l1 ball on s           */
   PNP_METHOD_C = 2,       /* Poisson noise, generalised-KL prox                       */
-  PNP_METHOD_ADMM_B2 = 3  /* comparisonB-2                                            */
+  PNP_METHOD_ADMM_B2 = 3, /* comparisonB-2: ADMM, denoiser x-step (admm.py:30-44)    */
+  /* comparison methods (iteration.py:71-180; the BM3D ones are not available)       */
+  PNP_METHOD_A_PNPFBS = 4,  /* A-PnPFBS-DnCNN:  x = D(x - g1 lam Phi^T(Phi x - x_obs))    */
+  PNP_METHOD_A_PDS_TV = 5,  /* A-PDS-TV:  PDS with TV (D, D^T, prox_l12) + l2 ball        */
+  PNP_METHOD_A_FBS_TV = 6,  /* A-FBS-TV:  additive data term + TV dual                    */
+  PNP_METHOD_A_RED = 7,     /* A-RED-DnCNN: RED steepest descent                          */
+  PNP_METHOD_B_HTV = 8,     /* comparisonB-3: TV + l1 ball on s + l2 ball                 */
+  PNP_METHOD_B_RED = 9,     /* comparisonB-4: RED with the sparse component               */
+  PNP_METHOD_B_PNPFBS = 10, /* comparisonB-5: PnP-FBS with the sparse component           */
+  PNP_METHOD_C_PNPADMM = 11,/* C-PnPADMM-DnCNN: Poisson ADMM, denoiser z-step             */
+  PNP_METHOD_C_RED = 12     /* C-RED-DnCNN: Poisson ADMM, RED z-step                      */
+  /* A-PnPPDS-unstable-DnCNN / C-PnP-unstable-DnCNN are METHOD_A / METHOD_C with the
+   * KAIR DnCNN set as the denoiser (residual_sign -1, ReLU, clamp_io 0).             */
 };
 
 /* operators.py:60-79 */

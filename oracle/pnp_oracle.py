@@ -64,7 +64,7 @@ def sampling_mask(H: int, W: int, r: float) -> np.ndarray:
 def random_sampling(x: np.ndarray, r: float) -> np.ndarray:
     """operators.py:40-58 (self-adjoint); returns float64 like the reference."""
     m = sampling_mask(x.shape[-2], x.shape[-1], r)
-    return np.asarray(x, np.float64) * m
+    return np.where(m.astype(bool), np.asarray(x, np.float64), 0.0)   # t[q] = 0: NaN-safe like the shipped code
 
 
 def observation_operators(kind: str, h: np.ndarray | None = None, r: float = 0.8):
@@ -268,6 +268,53 @@ class OracleDenoiser:
 METHOD_ALIASES = {"ours-A": "A-Proposed", "ours-B": "B-Proposed", "ours-C": "C-Proposed"}
 
 
+# ---------------------------------------------------------------------------
+# TV operators (operators.py:110-137) — restated with the shipped boundary handling
+# ---------------------------------------------------------------------------
+def D(x):
+    """operators.py:120-126: forward differences along rows then columns, zero last row /
+    column; (C,H,W) -> (2C,H,W)."""
+    xv = np.zeros(x.shape)
+    xh = np.zeros(x.shape)
+    xv[:, :-1, :] = x[:, 1:, :] - x[:, :-1, :]
+    xh[:, :, :-1] = x[:, :, 1:] - x[:, :, :-1]
+    return np.concatenate([xv, xh], 0)
+
+
+def D_T(y):
+    """operators.py:128-137 as shipped: first row -y[0], inner rows y[i-1] - y[i], last row
+    +y[H-1] (not y[H-2]); likewise for columns."""
+    C = y.shape[0] // 2
+    yv, yh = y[:C], y[C:]
+    ov = np.empty(yv.shape)
+    ov[:, 0] = -yv[:, 0]
+    ov[:, 1:-1] = -yv[:, 1:-1] + yv[:, :-2]
+    ov[:, -1] = yv[:, -1]
+    oh = np.empty(yh.shape)
+    oh[:, :, 0] = -yh[:, :, 0]
+    oh[:, :, 1:-1] = -yh[:, :, 1:-1] + yh[:, :, :-2]
+    oh[:, :, -1] = yh[:, :, -1]
+    return ov + oh
+
+
+def prox_l12(x, gamma):
+    """operators.py:110-112: per-pixel group soft threshold over axis 0."""
+    with np.errstate(divide="ignore"):
+        val = gamma / np.sqrt(np.sum(x * x, 0))
+    return np.fmax(1 - val, 0) * x
+
+
+def _admm_poisson_x(u, v, y, phi, adj_phi, alpha, lam, m, gamma):
+    """algorithm/admm.py:4-16 (step1ofADMMforPoisson)."""
+    x = np.ones(u.shape)
+    for _ in range(m):
+        with np.errstate(divide="ignore", invalid="ignore"):
+            ratio = y / (alpha * phi(x))
+        grad = -adj_phi(ratio) / alpha + adj_phi(np.ones(x.shape)) / alpha + lam * (x - v + u)
+        x = x - gamma * grad
+    return x
+
+
 def test_iter(x_0, x_obsrv, x_true, phi, adj_phi, gamma1, gamma2, alpha_s, alpha_n, myLambda,
               m1, m2, gammaInADMMStep1, gaussian_nl, sp_nl, poisson_alpha, denoiser, max_iter,
               method="A-Proposed", ch=3, r=1, ssim_fn=None):
@@ -276,8 +323,11 @@ def test_iter(x_0, x_obsrv, x_true, phi, adj_phi, gamma1, gamma2, alpha_s, alpha
     method = METHOD_ALIASES.get(method, method)
     x_n = x_0
     y_n = np.zeros(x_0.shape)
+    y1_n = np.zeros((2 * x_0.shape[0],) + x_0.shape[1:]) if x_0.ndim == 3 else None
+    y2_n = np.zeros(x_0.shape)
     s_n = np.zeros(x_0.shape)
     z_n = np.zeros(x_0.shape)
+    d_n = np.zeros(x_0.shape)
     c = np.zeros(max_iter)
     psnr_data = np.zeros(max_iter)
     ssim_data = np.zeros(max_iter)
@@ -309,6 +359,52 @@ def test_iter(x_0, x_obsrv, x_true, phi, adj_phi, gamma1, gamma2, alpha_s, alpha
                 s_n = proj_l1_ball(s_n, alpha_s, sp_nl)
             z_n = proj_l2_ball(phi(x_n) + s_n + y_n, alpha_n, gaussian_nl, sp_nl, x_obsrv)
             y_n = y_n + phi(x_n) + s_n - z_n
+        elif method == "A-PnPFBS-DnCNN":                                  # iteration.py:71-73
+            x_n = denoiser.denoise(x_n - gamma1 * myLambda * 0.5 * (2 * adj_phi(phi(x_n) - x_obsrv)))
+        elif method == "A-PDS-TV":                                        # iteration.py:86-91
+            x_n = x_n - gamma1 * (D_T(y1_n) + adj_phi(y2_n))
+            y1_n = y1_n + gamma2 * D(2 * x_n - x_prev)
+            y1_n = y1_n - gamma2 * prox_l12(y1_n / gamma2, 1 / gamma2)
+            y2_n = y2_n + gamma2 * (phi(2 * x_n - x_prev))
+            y2_n = y2_n - gamma2 * proj_l2_ball(y2_n / gamma2, alpha_n, gaussian_nl, sp_nl, x_obsrv)
+        elif method == "A-FBS-TV":                                        # iteration.py:92-96
+            x_n = x_n - gamma1 * (adj_phi(phi(x_n) - x_obsrv) + D_T(y1_n))
+            y1_n = y1_n + gamma2 * D(2 * x_n - x_prev)
+            y1_n = y1_n - gamma2 * prox_l12(y1_n / gamma2, 1 / gamma2)
+        elif method == "A-RED-DnCNN":                                     # iteration.py:97-103
+            x_n = denoiser.denoise(x_n)
+            mu = 2 / (1 / gamma1 ** 2 + myLambda)
+            x_n = x_prev - mu * ((1 / gamma1 ** 2) * adj_phi(phi(x_prev) - x_obsrv) + myLambda * (x_prev - x_n))
+        elif method in ("A-PnPPDS-unstable-DnCNN", "C-PnP-unstable-DnCNN"):   # iteration.py:104-110,174-180
+            x_n = denoiser.denoise(x_n - gamma1 * adj_phi(y_n))          # denoiser = the KAIR DnCNN here
+            y_n = y_n + gamma2 * phi(2 * x_n - x_prev)
+            if method.startswith("A"):
+                y_n = y_n - gamma2 * proj_l2_ball(y_n / gamma2, alpha_n, gaussian_nl, sp_nl, x_obsrv)
+            else:
+                y_n = y_n - gamma2 * prox_gkl(y_n / gamma2, myLambda / gamma2, poisson_alpha, x_obsrv)
+        elif method == "comparisonB-3":                                   # iteration.py:139-145
+            x_n = x_n - gamma1 * (D_T(y1_n) + adj_phi(y2_n))
+            s_n = proj_l1_ball(s_n - gamma1 * y2_n, alpha_s, sp_nl)
+            y1_n = y1_n + gamma2 * D(2 * x_n - x_prev)
+            y1_n = y1_n - gamma2 * prox_l12(y1_n / gamma2, 1 / gamma2)
+            y2_n = y2_n + gamma2 * (phi(2 * x_n - x_prev) + 2 * s_n - s_prev)
+            y2_n = y2_n - gamma2 * proj_l2_ball(y2_n / gamma2, alpha_n, gaussian_nl, sp_nl, x_obsrv)
+        elif method == "comparisonB-4":                                   # iteration.py:146-151
+            x_n = x_prev - gamma1 * (myLambda * adj_phi(phi(x_prev) + s_n - x_obsrv) + (x_prev - denoiser.denoise(x_n)))
+            s_n = proj_l1_ball(s_n - gamma1 * (phi(x_n) + s_n - x_obsrv), alpha_s, sp_nl)
+        elif method == "comparisonB-5":                                   # iteration.py:152-155
+            x_n = denoiser.denoise(x_n - gamma1 * (2 * adj_phi(phi(x_n) + s_n - x_obsrv)))
+            s_n = proj_l1_ball(s_n - gamma1 * (phi(x_n) + s_n - x_obsrv), alpha_s, sp_nl)
+        elif method in ("C-PnPADMM-DnCNN", "C-RED-DnCNN"):                # iteration.py:163-173
+            x_n = _admm_poisson_x(d_n, z_n, x_obsrv, phi, adj_phi, poisson_alpha, myLambda, m1, gammaInADMMStep1)
+            if method == "C-PnPADMM-DnCNN":
+                z_n = denoiser.denoise(x_n + d_n)
+            else:                                                         # admm.py:18-27 (beta=myLambda, lam=gamma1)
+                z_str = x_n + d_n
+                for _ in range(m2):
+                    z_n = denoiser.denoise(z_n)
+                    z_n = 1 / (myLambda + gamma1) * (gamma1 * z_n + myLambda * z_str)
+            d_n = d_n + x_n - z_n
         else:
             raise ValueError(f"Unknown method: {method}")
         c[i] = np.linalg.norm((x_n - x_prev).flatten(), 2) / np.linalg.norm(x_prev.flatten(), 2)

@@ -65,7 +65,8 @@ struct pnp_ctx {
   pnp_params prm{};
   int cur = 0;
   DevBuf x[2], y, s, w, xobs, xtrue, u32, u16, act[2], partials, metrics, theta;
-  DevBuf z, p, t;   // comparisonB-2 only
+  DevBuf z, p, t;   // comparisonB-2 and the other comparison methods
+  DevBuf y1, d, c1; // TV dual [B][2C][H][W]; Poisson-ADMM d and Phi^T 1
   DevBuf ssim_scr;  // SSIM partials (record_ssim)
 
   // observation pipeline (pnp_degrade)
@@ -411,20 +412,172 @@ void solver_iteration_admm(pnp_ctx* ctx) {
   ctx->it += 1;
 }
 
+bool is_tv(int m) { return m == PNP_METHOD_A_PDS_TV || m == PNP_METHOD_A_FBS_TV || m == PNP_METHOD_B_HTV; }
+bool is_poisson_admm(int m) { return m == PNP_METHOD_C_PNPADMM || m == PNP_METHOD_C_RED; }
+
+// The comparison methods of iteration.py:71-180 (BM3D excluded), composed from the PDS
+// path's kernels plus methods.hip.  x_o = x_n of the reference on entry, x_n on exit.
+void solver_iteration_cmp(pnp_ctx* ctx) {
+  hipStream_t st = ctx->stream;
+  const pnp_params& p = ctx->prm;
+  const int B = ctx->B, C = ctx->C, H = ctx->H, W = ctx->W, m = ctx->method;
+  const size_t n = (size_t)C * H * W, N = (size_t)B * n;
+  const OpDesc od = op_desc(ctx);
+  float* xo = P<float>(ctx->x[ctx->cur]);
+  float* xn = P<float>(ctx->x[ctx->cur ^ 1]);
+  float *y = P<float>(ctx->y), *sv = P<float>(ctx->s), *xobs = P<float>(ctx->xobs);
+  float *t = P<float>(ctx->t), *pp = P<float>(ctx->p), *w = P<float>(ctx->w), *z = P<float>(ctx->z);
+  const float* xt = ctx->has_true ? P<float>(ctx->xtrue) : nullptr;
+  const int record = p.record_metrics && ctx->it < ctx->cap;
+  auto phi = [&](const float* in, float* out, const float* add = nullptr) {
+    launch_op_phi(od.kind, 0, in, out, od, B * C, H, W, st, add);
+  };
+  auto adj = [&](const float* in, float* out) { launch_op_phi(od.kind, 1, in, out, od, B * C, H, W, st); };
+  auto lin = [&](float* out, double k, const float* a, double ca, const float* b = nullptr, double cb = 0.0,
+                 const float* c = nullptr, double cc = 0.0, const float* d = nullptr, double cd = 0.0) {
+    launch_lincomb(out, k, a, ca, b, cb, c, cc, d, cd, N, st);
+  };
+  auto denoise = [&](const float* in, float* out) {          // Denoiser_J.denoise / KAIR forward
+    launch_pack_input(in, P<float>(ctx->u32), P<half_t>(ctx->u16), B, C, H, W, ctx->den_clamp, st);
+    run_denoiser(ctx, P<half_t>(ctx->u16), P<float>(ctx->u32), out, ctx->act, B, H, W, st);
+  };
+  const double eta = p.alpha_s * (double)n * p.sp_nl * 0.5;                         // proj_l1_ball, r = 1
+  const double eps = std::sqrt((double)n * (1.0 - p.sp_nl)) * p.alpha_n * p.gaussian_nl;  // proj_l2_ball, r = 1
+  auto l1proj = [&](const float* in, float* out) {
+    launch_l1_select(in, P<float>(ctx->theta), B, n, eta, st);
+    launch_shrink(in, out, P<float>(ctx->theta), B, n, st);
+  };
+  auto metrics = [&] {
+    if (record)
+      launch_metrics(xn, xo, xt, P<double>(ctx->partials), P<double>(ctx->metrics), B, n, ctx->it, ctx->cap, st);
+  };
+  // Phi x + s - x_obs  (grad_s_l2, operators.py:91-92), into out
+  auto residual = [&](const float* x, const float* s, float* out) {
+    phi(x, out, s);
+    lin(out, 0.0, out, 1.0, xobs, -1.0);
+  };
+  ProfScope ps(ctx, "cmp_iteration", st);
+  switch (m) {
+    case PNP_METHOD_A_PNPFBS: {      // iteration.py:71-73
+      residual(xo, nullptr, t);
+      adj(t, pp);
+      lin(pp, 0.0, xo, 1.0, pp, -(p.gamma1 * p.my_lambda * 0.5) * 2.0);
+      denoise(pp, xn);
+      metrics();
+      break;
+    }
+    case PNP_METHOD_A_RED: {         // iteration.py:98-103
+      denoise(xo, xn);
+      residual(xo, nullptr, t);
+      adj(t, pp);
+      const double ig = 1.0 / (p.gamma1 * p.gamma1), mu = 2.0 / (ig + p.my_lambda);
+      lin(xn, 0.0, xo, 1.0 - mu * p.my_lambda, pp, -mu * ig, xn, mu * p.my_lambda);
+      metrics();
+      break;
+    }
+    case PNP_METHOD_B_RED: {         // iteration.py:146-151
+      denoise(xo, xn);
+      residual(xo, sv, t);
+      adj(t, pp);
+      lin(xn, 0.0, xo, 1.0 - p.gamma1, pp, -p.gamma1 * p.my_lambda, xn, p.gamma1);
+      residual(xn, sv, t);
+      lin(w, 0.0, sv, 1.0, t, -p.gamma1);
+      l1proj(w, sv);
+      metrics();
+      break;
+    }
+    case PNP_METHOD_B_PNPFBS: {      // iteration.py:152-155
+      residual(xo, sv, t);
+      adj(t, pp);
+      lin(pp, 0.0, xo, 1.0, pp, -p.gamma1 * 2.0);
+      denoise(pp, xn);
+      residual(xn, sv, t);
+      lin(w, 0.0, sv, 1.0, t, -p.gamma1);
+      l1proj(w, sv);
+      metrics();
+      break;
+    }
+    case PNP_METHOD_A_PDS_TV:        // iteration.py:86-91
+    case PNP_METHOD_B_HTV: {         // iteration.py:139-145
+      float* y1 = P<float>(ctx->y1);
+      adj(y, pp);
+      launch_tv_primal(xo, y1, pp, p.gamma1, xn, B, C, H, W, st);
+      const int mb = m == PNP_METHOD_B_HTV;
+      if (mb) {
+        lin(w, 0.0, sv, 1.0, y, -p.gamma1);
+        launch_l1_select(w, P<float>(ctx->theta), B, n, eta, st);
+      }
+      launch_tv_dual(xn, xo, y1, p.gamma2, B, C, H, W, st);
+      launch_k2(od.kind, mb ? PNP_METHOD_B : PNP_METHOD_A, xn, xo, y, xobs, xt, sv, w, P<float>(ctx->theta),
+                P<double>(ctx->partials), od, B, C, H, W, p.gamma2, 0.0, p.poisson_alpha, record, st);
+      launch_k3(mb ? PNP_METHOD_B : PNP_METHOD_A, y, xobs, P<double>(ctx->partials), od, B, C, H, W, p.gamma2, eps,
+                P<double>(ctx->metrics), ctx->it, ctx->cap, record, ctx->has_true, st);
+      break;
+    }
+    case PNP_METHOD_A_FBS_TV: {      // iteration.py:92-96
+      residual(xo, nullptr, t);
+      adj(t, pp);
+      launch_tv_primal(xo, P<float>(ctx->y1), pp, p.gamma1, xn, B, C, H, W, st);
+      launch_tv_dual(xn, xo, P<float>(ctx->y1), p.gamma2, B, C, H, W, st);
+      metrics();
+      break;
+    }
+    case PNP_METHOD_C_PNPADMM:       // iteration.py:163-166
+    case PNP_METHOD_C_RED: {         // iteration.py:167-173
+      float* d = P<float>(ctx->d);
+      lin(xn, 1.0, nullptr, 0.0);                                       // admm.py:9 x_n = ones
+      for (int i = 0; i < p.m1; ++i) {                                  // admm.py:10-12
+        phi(xn, t);
+        launch_poisson_ratio(xobs, t, p.poisson_alpha, t, N, st);
+        adj(t, pp);
+        launch_admm_poisson_step(xn, pp, P<float>(ctx->c1), z, d, p.gamma_in_admm_step1, p.poisson_alpha,
+                                 p.my_lambda, N, st);
+      }
+      if (m == PNP_METHOD_C_PNPADMM) {
+        lin(pp, 0.0, xn, 1.0, d, 1.0);
+        denoise(pp, z);                                                 // z = D(x + d)
+      } else {                                                          // admm.py:18-27
+        const double beta = p.my_lambda, lam2 = p.gamma1;
+        lin(pp, 0.0, xn, 1.0, d, 1.0);                                  // z_str
+        for (int i = 0; i < p.m2; ++i) {
+          denoise(z, z);
+          lin(z, 0.0, z, (1.0 / (beta + lam2)) * lam2, pp, (1.0 / (beta + lam2)) * beta);
+        }
+      }
+      lin(d, 0.0, d, 1.0, xn, 1.0, z, -1.0);                            // d = d + x - z
+      metrics();
+      break;
+    }
+    default:
+      fail(ctx, PNP_E_UNSUPPORTED, "method %d", m);
+  }
+  check_launch(ctx, "cmp_iteration");
+  record_ssim(ctx, xn, st);
+  ctx->cur ^= 1;
+  ctx->it += 1;
+}
+
 void solver_step(pnp_ctx* ctx) {
   if (ctx->method == PNP_METHOD_ADMM_B2) solver_iteration_admm(ctx);
-  else solver_iteration(ctx);
+  else if (ctx->method <= PNP_METHOD_C) solver_iteration(ctx);
+  else solver_iteration_cmp(ctx);
 }
 
 void solver_setup(pnp_ctx* ctx, int method, const pnp_params* params, int B, int C, int H, int W, int cap) {
   if (!params) fail(ctx, PNP_E_ARG, "params is NULL");
-  if (method < PNP_METHOD_A || method > PNP_METHOD_ADMM_B2)
+  if (method < PNP_METHOD_A || method > PNP_METHOD_C_RED)
     fail(ctx, PNP_E_UNSUPPORTED, "method %d not supported on device", method);
   if (method == PNP_METHOD_ADMM_B2 && (params->m1 < 0 || params->m2 < 0 || params->gamma1 == 0.0))
     fail(ctx, PNP_E_ARG, "comparisonB-2 needs m1, m2 >= 0 and gamma1 != 0");
+  if (is_poisson_admm(method) && (params->m1 < 0 || params->m2 < 0 || params->poisson_alpha == 0.0))
+    fail(ctx, PNP_E_ARG, "Poisson ADMM needs m1, m2 >= 0 and poisson_alpha != 0");
+  if (is_tv(method) && (H < 3 || W < 3 || C > kMaxC))
+    fail(ctx, PNP_E_ARG, "TV methods need H, W >= 3 (operators.py:128-137)");
   if (B < 1 || C < 1 || C > kMaxC || H < 1 || W < 1) fail(ctx, PNP_E_ARG, "bad shape B=%d C=%d H=%d W=%d", B, C, H, W);
-  if (!ctx->den_ready) fail(ctx, PNP_E_STATE, "denoiser not set");
-  if (ctx->den_C != C) fail(ctx, PNP_E_ARG, "denoiser has %d channels, images have %d", ctx->den_C, C);
+  if (!is_tv(method)) {   // the TV methods use no denoiser
+    if (!ctx->den_ready) fail(ctx, PNP_E_STATE, "denoiser not set");
+    if (ctx->den_C != C) fail(ctx, PNP_E_ARG, "denoiser has %d channels, images have %d", ctx->den_C, C);
+  }
   check_operator_shape(ctx, H, W);
   if (ctx->op_kind == PNP_OP_BLUR && (ctx->op_R > H || ctx->op_R > W))
     fail(ctx, PNP_E_ARG, "blur kernel radius %d larger than the image", ctx->op_R);
@@ -440,11 +593,16 @@ void solver_setup(pnp_ctx* ctx, int method, const pnp_params* params, int B, int
   ensure(ctx, ctx->xobs, fb);
   ensure(ctx, ctx->xtrue, fb);
   ensure(ctx, ctx->u32, fb);
-  if (method == PNP_METHOD_B || method == PNP_METHOD_ADMM_B2) ensure(ctx, ctx->w, fb);
-  if (method == PNP_METHOD_ADMM_B2) {
+  if (method != PNP_METHOD_A && method != PNP_METHOD_C) ensure(ctx, ctx->w, fb);
+  if (method >= PNP_METHOD_ADMM_B2) {
     ensure(ctx, ctx->z, fb);
     ensure(ctx, ctx->p, fb);
     ensure(ctx, ctx->t, fb);
+  }
+  if (is_tv(method)) ensure(ctx, ctx->y1, 2 * fb);
+  if (is_poisson_admm(method)) {
+    ensure(ctx, ctx->d, fb);
+    ensure(ctx, ctx->c1, fb);
   }
   ensure_padded(ctx, ctx->u16, B, H, W, 4, 1, ctx->stream);
   ensure(ctx, ctx->partials,
@@ -460,7 +618,15 @@ void solver_reset_state(pnp_ctx* ctx) {
   const size_t fb = (size_t)ctx->B * ctx->C * ctx->H * ctx->W * sizeof(float);
   HIPCHK(ctx, hipMemsetAsync(ctx->y.p, 0, fb, ctx->stream));          // iteration.py:24
   HIPCHK(ctx, hipMemsetAsync(ctx->s.p, 0, fb, ctx->stream));          // iteration.py:27
-  if (ctx->method == PNP_METHOD_ADMM_B2) HIPCHK(ctx, hipMemsetAsync(ctx->z.p, 0, fb, ctx->stream));
+  if (ctx->method >= PNP_METHOD_ADMM_B2) HIPCHK(ctx, hipMemsetAsync(ctx->z.p, 0, fb, ctx->stream));
+  if (is_tv(ctx->method)) HIPCHK(ctx, hipMemsetAsync(ctx->y1.p, 0, 2 * fb, ctx->stream));   // iteration.py:25
+  if (is_poisson_admm(ctx->method)) {
+    HIPCHK(ctx, hipMemsetAsync(ctx->d.p, 0, fb, ctx->stream));                            // iteration.py:29
+    const OpDesc od = op_desc(ctx);                                                     // c1 = Phi^T 1 (admm.py:11)
+    launch_lincomb(P<float>(ctx->t), 1.0, nullptr, 0.0, nullptr, 0.0, nullptr, 0.0, nullptr, 0.0, fb / 4,
+                   ctx->stream);
+    launch_op_phi(od.kind, 1, P<float>(ctx->t), P<float>(ctx->c1), od, ctx->B * ctx->C, ctx->H, ctx->W, ctx->stream);
+  }
   if (ctx->cap) {
     std::vector<double> nanbuf((size_t)ctx->B * ctx->cap * kMetrics, std::nan(""));
     HIPCHK(ctx, hipMemcpyAsync(ctx->metrics.p, nanbuf.data(), nanbuf.size() * sizeof(double), hipMemcpyHostToDevice,
@@ -551,7 +717,7 @@ int pnp_destroy(pnp_ctx* ctx) {
                     &ctx->partials, &ctx->metrics, &ctx->theta, &ctx->scr_u32, &ctx->scr_u16,
                     &ctx->scr_act[0], &ctx->scr_act[1], &ctx->scr_part, &ctx->scr_theta,
                     &ctx->z, &ctx->p, &ctx->t, &ctx->dense_fwd, &ctx->dense_adj, &ctx->ssim_scr,
-                    &ctx->taps64, &ctx->dg_words, &ctx->dg_flag, &ctx->dg_rank, &ctx->dg_scan, &ctx->dg_noise,
+                    &ctx->taps64, &ctx->y1, &ctx->d, &ctx->c1, &ctx->dg_words, &ctx->dg_flag, &ctx->dg_rank, &ctx->dg_scan, &ctx->dg_noise,
                     &ctx->dg_img, &ctx->dg_draws, &ctx->dg_first, &ctx->dg_status};
   for (DevBuf* b : bufs) release(*b);
   for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);

@@ -100,6 +100,17 @@ void launch_sp_apply(const uint32_t* draws, int npairs, const uint8_t* tgt, int 
 void launch_degrade_finalize(const double* img, size_t N, double alpha, int poisson, float* xobs, float* x0,
                              double* xobs64, hipStream_t st);
 
+// ---- comparison methods (methods.hip) ----
+// out = x - gamma1 (D^T y1 + g); y1 is [B][2C][H][W]; g may be null
+void launch_tv_primal(const float* x, const float* y1, const float* g, double gamma1, float* out, int B, int C, int H,
+                      int W, hipStream_t st);
+// y1 <- y1 + g2 D(2 xn - xo); y1 <- y1 - g2 prox_l12(y1 / g2, 1 / g2)
+void launch_tv_dual(const float* xn, const float* xo, float* y1, double gamma2, int B, int C, int H, int W,
+                    hipStream_t st);
+void launch_poisson_ratio(const float* y, const float* t, double alpha, float* out, size_t N, hipStream_t st);
+void launch_admm_poisson_step(float* x, const float* g, const float* c1, const float* v, const float* u,
+                              double gamma, double alpha, double lam, size_t N, hipStream_t st);
+
 // per-iteration metrics: metrics[b][it][kMetrics] = {c_n, PSNR, SSIM}
 constexpr int kMetrics = 3;
 // SSIM of x against xt (utils_eval.py:9-12) into metrics[b][it][2]; scratch >= ssim_scratch_bytes

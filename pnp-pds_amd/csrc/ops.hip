@@ -409,7 +409,7 @@ __global__ __launch_bounds__(256) void op_phi_kernel(const float* __restrict__ x
     const size_t k = (size_t)i * W + j;
     float v;
     if (KIND == OP_BLUR) v = acc[r];
-    else if (KIND == OP_MASK) v = xp[k] * (float)op.mask[k];
+    else if (KIND == OP_MASK) v = op.mask[k] ? xp[k] : 0.f;   // t[q] = 0 (operators.py:49-57), NaN-safe
     else v = xp[k];
     if (add) v += add[(size_t)bc * plane + k];
     out[(size_t)bc * plane + k] = v;

@@ -19,6 +19,9 @@ PNP_OK = 0
 ERRORS = {-1: "PNP_E_ARG", -2: "PNP_E_UNSUPPORTED", -3: "PNP_E_HIP", -4: "PNP_E_OOM", -5: "PNP_E_STATE", -6: "PNP_E_INTERNAL"}
 
 METHOD_A, METHOD_B, METHOD_C, METHOD_ADMM_B2 = 0, 1, 2, 3
+(METHOD_A_PNPFBS, METHOD_A_PDS_TV, METHOD_A_FBS_TV, METHOD_A_RED, METHOD_B_HTV, METHOD_B_RED, METHOD_B_PNPFBS,
+ METHOD_C_PNPADMM, METHOD_C_RED) = range(4, 13)
+TV_METHODS = (METHOD_A_PDS_TV, METHOD_A_FBS_TV, METHOD_B_HTV)   # no denoiser
 OP_ID, OP_BLUR, OP_RANDOM_SAMPLING = 0, 1, 2
 TUNE_DENOISE_CHUNK = 1
 TUNE_BODY_VARIANT = 2

@@ -14,8 +14,13 @@ Differences from the reference, by design:
     Python closures cannot run on the device; there is no host fallback).
   * state is fp32 on the device (the reference mixes fp32 x and fp64 y); denoiser
     operands are fp16 with fp32 accumulation.  Tolerances: DESIGN.md §Parity.
-  * ``ssim`` is not computed on the device yet (utils_eval.eval_ssim needs skimage,
-    which is absent here, so it is also unpinned); it is returned as NaN.
+  * ``ssim`` is computed on the device every iteration (utils_eval.eval_ssim restated;
+    skimage is absent here, so its parity is unpinned).
+  * comparisonB-4 / comparisonB-5 run with the DnCNN denoiser their text uses; the
+    reference raises UnboundLocalError for them (denoiser_J is only built for names
+    containing 'Proposed' or 'DnCNN', iteration.py:40-41).
+  * the BM3D methods (A-PnPPDS-BM3D, A-PnPFBS-BM3D, comparisonB-1, C-PnPPDS-BM3D) need the
+    bm3d package and are not available: they raise ValueError.
   * ``average_time`` is wall-clock seconds per iteration (the reference reports
     process_time, iteration.py:43,193-194).
 """
@@ -34,6 +39,13 @@ METHODS = {
     "B-Proposed": _lib.METHOD_B, "ours-B": _lib.METHOD_B,
     "C-Proposed": _lib.METHOD_C, "ours-C": _lib.METHOD_C,
     "comparisonB-2": _lib.METHOD_ADMM_B2,
+    # comparison methods (iteration.py:71-180)
+    "A-PnPFBS-DnCNN": _lib.METHOD_A_PNPFBS, "A-PDS-TV": _lib.METHOD_A_PDS_TV, "A-FBS-TV": _lib.METHOD_A_FBS_TV,
+    "A-RED-DnCNN": _lib.METHOD_A_RED, "comparisonB-3": _lib.METHOD_B_HTV, "comparisonB-4": _lib.METHOD_B_RED,
+    "comparisonB-5": _lib.METHOD_B_PNPFBS, "C-PnPADMM-DnCNN": _lib.METHOD_C_PNPADMM,
+    "C-RED-DnCNN": _lib.METHOD_C_RED,
+    # the KAIR DnCNN (path_prox = dncnn_color_blind / dncnn_15) in the A / C loops (iteration.py:104-110,174-180)
+    "A-PnPPDS-unstable-DnCNN": _lib.METHOD_A, "C-PnP-unstable-DnCNN": _lib.METHOD_C,
 }
 
 
@@ -45,7 +57,12 @@ def make_params(gamma1, gamma2, alpha_s, alpha_n, myLambda, m1, m2, gammaInADMMS
                            1 if (record_metrics and record_ssim) else 0)
 
 
+BM3D_METHODS = ("A-PnPPDS-BM3D", "A-PnPFBS-BM3D", "comparisonB-1", "C-PnPPDS-BM3D")
+
+
 def resolve_method(method: str) -> int:
+    if method in BM3D_METHODS:
+        raise ValueError(f"{method} needs the bm3d package (iteration.py:74-85,119-126,158-162); not available")
     if method not in METHODS:
         raise ValueError(f"Unknown method: {method!r} (device path supports {sorted(METHODS)})")
     return METHODS[method]
@@ -83,8 +100,9 @@ def test_iter_batch(x_0, x_obsrv, x_true, phi, adj_phi, gamma1, gamma2, alpha_s,
     if Cc != ch:
         raise ValueError(f"ch={ch} but images have {Cc} channels")
     ctx = ctx or get_ctx()
-    den = _resolve_denoiser(path_prox, ch)
-    den.configure(ctx)
+    if m not in _lib.TV_METHODS:                       # the TV methods use no denoiser
+        den = _resolve_denoiser(path_prox, ch)
+        den.configure(ctx)
     phi.configure(ctx, H, W)
     prm = make_params(gamma1, gamma2, alpha_s, alpha_n, myLambda, m1, m2, gammaInADMMStep1, gaussian_nl, sp_nl,
                       poisson_alpha, r, record_metrics, record_ssim)

@@ -221,7 +221,55 @@ def make_driver_golden(ref_root="/root/reference"):
     print("driver.json")
 
 
+CMP_CASES = [
+    # name,        method,                   deg_op, ch, sigma, sp,  pois,  g1,      g2,          a_n,  a_s,  lam, r,   iters, m1, m2, arch
+    ("A_pnpfbs",  "A-PnPFBS-DnCNN",          "blur", 3, 0.01, 0.0, False, 1.0,     0.99,        0.95, 0.95, 1.99, 1.0, 4, 15, 15, None),
+    ("A_pdstv",   "A-PDS-TV",                "blur", 3, 0.01, 0.0, False, 0.125,   0.99,        0.9,  0.95, 1.0, 1.0, 6, 15, 15, None),
+    ("A_fbstv",   "A-FBS-TV",                "random_sampling", 3, 0.01, 0.0, False, 0.1, 0.99,  0.9,  0.95, 1.0, 0.8, 6, 15, 15, None),
+    ("A_red",     "A-RED-DnCNN",             "blur", 3, 0.01, 0.0, False, 1.0,     0.99,        0.95, 0.95, 0.4, 1.0, 4, 15, 15, None),
+    ("A_unstable", "A-PnPPDS-unstable-DnCNN", "blur", 3, 0.01, 0.0, False, 0.99,   0.99,        0.95, 0.95, 1.0, 1.0, 4, 15, 15,
+     "dncnn_color_blind"),
+    ("B3_htv",    "comparisonB-3",           "blur", 3, 0.01, 0.1, False, 0.1,     0.99,        0.95, 0.95, 1.0, 1.0, 6, 15, 15, None),
+    ("C_admm",    "C-PnPADMM-DnCNN",         "blur", 3, 0.0,  0.0, True,  0.99,    0.99,        0.95, 0.95, 1.0, 1.0, 3, 5, 3, None),
+    ("C_red",     "C-RED-DnCNN",             "random_sampling", 3, 0.0, 0.0, True, 1.0, 0.99,    0.95, 0.95, 0.5, 0.5, 3, 5, 2, None),
+    ("C_unstable", "C-PnP-unstable-DnCNN",   "random_sampling", 1, 0.0, 0.0, True, 0.00035, 1 / 0.00035, 1.0, 1.0, 1.0, 0.5, 4, 15, 15,
+     "dncnn_15"),
+]
+
+
+def make_cmp_golden(ref_root="/root/reference"):
+    """Trajectories of the comparison methods (iteration.py:71-180, BM3D excluded).
+    comparisonB-4 / -5 are absent: the reference raises UnboundLocalError for them
+    (denoiser_J is only built for names containing 'Proposed' or 'DnCNN', iteration.py:40-41)."""
+    install_shims(ref_root)
+    import operators as op
+    import iteration
+    path_kernel = os.path.join(ref_root, "blur_models", "blur_1.mat")
+    nn_dir = os.path.join(ref_root, "nn")
+    for (name, method, deg, ch, sig, sp, pois, g1, g2, an, as_, lam, r, iters, m1, m2, arch) in CMP_CASES:
+        phi, adj = op.get_observation_operators(deg, path_kernel, r)
+        Id, _ = op.get_observation_operators("Id", path_kernel, r)
+        xt = synthetic_image(ch, 64, 64, seed=300 + len(name))
+        if ch == 1:
+            xt = xt[0]
+        obs, x0 = degrade(xt, phi, Id, deg, sig, sp, pois, 300)
+        arch = arch or f"DnCNN_nobn_nch_{ch}_nlev_0.01"
+        gad = 0.1
+        t = time.perf_counter()
+        res = iteration.test_iter(x0, obs, xt, phi, adj, g1, g2, as_, an, lam, m1, m2, gad, sig, sp, 300,
+                                  os.path.join(nn_dir, arch + ".pth"), iters, method, ch, r)
+        xs, ss, c, ps, _ssim, _t = res
+        np.savez_compressed(os.path.join(HERE, f"iter_cmp_{name}.npz"), x_true=xt, x_obs=obs, x_0=x0,
+                            x_out=np.asarray(xs), s_out=ss, c=c, psnr=ps,
+                            params=np.array([g1, g2, as_, an, lam, m1, m2, gad, sig, sp, 300, iters, ch, r]),
+                            method=np.array(method), deg_op=np.array(deg), arch=np.array(arch))
+        print(f"iter_cmp_{name}.npz  psnr {ps[0]:.3f} -> {ps[-1]:.3f}  ({time.perf_counter()-t:.1f}s)")
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "--cmp":
+        make_cmp_golden(*sys.argv[2:])
+        sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "--driver":
         make_driver_golden(*sys.argv[2:])
     else:

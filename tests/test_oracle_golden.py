@@ -80,6 +80,26 @@ def test_test_iter_trajectory(case):
     np.testing.assert_allclose(ps, g["psnr"], atol=1e-4)
 
 
+CMP_CASES = ["A_pnpfbs", "A_pdstv", "A_fbstv", "A_red", "A_unstable", "B3_htv", "C_admm", "C_red", "C_unstable"]
+
+
+@pytest.mark.parametrize("case", CMP_CASES)
+def test_comparison_method_trajectory(case):
+    """Comparison methods (iteration.py:71-180) restated vs the reference's own trajectories."""
+    g = load_golden(f"iter_cmp_{case}.npz")
+    g1, g2, as_, an, lam, m1, m2, gadmm, sig, sp, palpha, iters, ch, r = g["params"]
+    w = DenoiserWeights.load_npz(os.path.join(WEIGHTS_DIR, str(g["arch"]) + ".npz"))
+    h = load_golden("ops.npz")["h"]
+    phi, adj = O.observation_operators(str(g["deg_op"]), h, r)
+    x, s, c, ps, _ss, _t = O.test_iter(g["x_0"], g["x_obs"], g["x_true"], phi, adj, g1, g2, as_, an, lam,
+                                       int(m1), int(m2), gadmm, sig, sp, palpha, O.OracleDenoiser(w),
+                                       int(iters), str(g["method"]), int(ch), r)
+    np.testing.assert_allclose(x, g["x_out"], atol=2e-5)
+    np.testing.assert_allclose(s, g["s_out"], atol=2e-5)
+    np.testing.assert_allclose(c, g["c"], rtol=1e-4, atol=1e-7)
+    np.testing.assert_allclose(ps, g["psnr"], atol=1e-4)
+
+
 def test_method_alias_and_unknown():
     x = np.zeros((1, 8, 8))
     phi, adj = O.observation_operators("Id")
