@@ -76,7 +76,7 @@ def test_unknown_method_and_closure_rejected():
     phi, adj = ops.get_observation_operators("Id", "blur_1", 0.8)
     with pytest.raises(ValueError):
         test_iter(x, x, x, phi, adj, 1, 1, 1, 1, 1, 1, 1, 0.1, 0.01, 0, 300, "DnCNN_nobn_nch_3_nlev_0.01", 1,
-                  "A-PDS-TV", 3, 1)
+                  "A-Nonexistent", 3, 1)
     with pytest.raises(TypeError):
         test_iter(x, x, x, lambda v: v, lambda v: v, 1, 1, 1, 1, 1, 1, 1, 0.1, 0.01, 0, 300,
                   "DnCNN_nobn_nch_3_nlev_0.01", 1, "A-Proposed", 3, 1)
