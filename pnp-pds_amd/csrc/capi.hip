@@ -49,6 +49,7 @@ struct pnp_ctx {
   int den_C = 0, den_depth = 0, den_act = 0, den_residual = 1, den_clamp = 1;
   int den_chunk = 0;   // images per denoiser pass; 0 = auto
   int body_fused = 0;     // 1: body layers two per launch (conv_body2), 0: one per launch (conv_body_v3)
+  int body_stagger = 0;   // PNP_TUNE_BODY_VARIANT 2: staggered epilogue in conv_body_v3
   int ablate = 0;         // profiling only (PNP_TUNE_ABLATE): parts of conv_body_v3 skipped, results wrong
   bool den_ready = false;
   DevBuf head_w, head_b, body_w, body_b, tail_w, tail_b;
@@ -261,7 +262,7 @@ void run_denoiser(pnp_ctx* ctx, const half_t* u16, const float* u32, float* xout
     {
       ProfScope ps(ctx, "conv_head", st);
       launch_conv_head(in4, P<half_t>(act[0]), ctx->head_w.p, P<float>(ctx->head_b), s, ctx->den_act,
-                       ctx->num_cus, st);
+                       ctx->num_cus, ctx->ablate >= 100 ? ctx->ablate - 100 : 4, st);
       check_launch(ctx, "conv_head");
     }
     int cur = 0;
@@ -278,7 +279,7 @@ void run_denoiser(pnp_ctx* ctx, const half_t* u16, const float* u32, float* xout
       } else {
         ProfScope ps(ctx, "conv_body", st);
         launch_conv_body(P<half_t>(act[cur]), P<half_t>(act[cur ^ 1]), wl, bl, s, ctx->den_act, ctx->num_cus,
-                         ctx->ablate, st);
+                         ctx->ablate ? ctx->ablate : (ctx->body_stagger ? 8 : 0), st);
         check_launch(ctx, "conv_body");
         l += 1;
       }
@@ -742,8 +743,10 @@ int pnp_set_tuning(pnp_ctx* ctx, int key, int value) {
       return;
     }
     if (key == PNP_TUNE_BODY_VARIANT) {
-      if (value < 0 || value > 1) fail(ctx, PNP_E_ARG, "body variant must be 0 (one layer/launch) or 1 (two)");
-      ctx->body_fused = value;
+      if (value < 0 || value > 2)
+        fail(ctx, PNP_E_ARG, "body variant must be 0 (one layer/launch), 1 (two) or 2 (one, staggered)");
+      ctx->body_fused = value == 1;
+      ctx->body_stagger = value == 2;
       return;
     }
     if (key == PNP_TUNE_ABLATE) {          // profiling only

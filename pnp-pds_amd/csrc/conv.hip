@@ -145,7 +145,11 @@ constexpr int kV3Stage = 3 * kV3Halo;
 constexpr int kV3Bias = kV3Stage + 8 * 4096;
 constexpr int kV3Lds = kV3Bias + 256;                           // 163584 B
 
-// ABL: profiling ablation (PNP_TUNE_ABLATE), compile-time; ABL = 0 is the product kernel.
+// ABL: bits 1/2/4 = profiling ablation (PNP_TUNE_ABLATE, results wrong), compile-time;
+//      bit 8 = stagger: waves 4-7 (the SIMD partners of waves 0-3) run each tile's epilogue
+//      at the start of the next tile, after the barrier, so on every SIMD one wave's
+//      bias/activation/staging work overlaps its partner's MFMAs (MI355X_MICROARCH.md, "two
+//      waves per SIMD", item 9).  Results are bit-identical.
 // ACT: 0 = LeakyReLU(0.01) (simple_CNN), 1 = ReLU (KAIR DnCNN).
 template <int ABL, int ACT>
 __global__ __launch_bounds__(512, 2) void conv_body_v3_kernel(const half_t* __restrict__ in,
@@ -195,10 +199,37 @@ __global__ __launch_bounds__(512, 2) void conv_body_v3_kernel(const half_t* __re
     const int pix = 16 * j + (lane >> 2), c = lane & 3;
     if constexpr ((ABL & 2) == 0) __builtin_amdgcn_raw_buffer_store_b128(v, rs[j >> 1], (pix & 31) * 128 + 64 * m + 16 * c, 0, 0);
   };
+  constexpr bool kStagger = (ABL & 8) != 0;
+  const bool late = kStagger && wave >= 4;
+  if constexpr ((ABL & 16) != 0) {            // static priority for the second-dispatched half
+    if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+  }
+  floatx16 acc0 = {}, acc1 = {};
+  int pb = 0, pty0 = 0, ptx0 = 0;             // previous tile (late waves' deferred epilogue)
+  bool have_prev = false;
+  auto epilogue = [&](int eb, int ety0, int etx0) {   // bias + activation -> fp16 -> staging (wave-private)
+    const float* bl = bias_l + 32 * m + 16 * h;
+    const int sw = (col >> 1) & 3;    // ds_write_b128 banks repeat every 128 B: 8 lanes distinct
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+      const int pix = n * 32 + col;
+      const floatx16& a = n == 0 ? acc0 : acc1;
+      *reinterpret_cast<half8_t*>(stg + pix * 64 + 16 * ((2 * h) ^ sw)) = bias_act8<ACT>(a, 0, bl);
+      *reinterpret_cast<half8_t*>(stg + pix * 64 + 16 * ((2 * h + 1) ^ sw)) = bias_act8<ACT>(a, 8, bl + 8);
+    }
+    const int ncols = min(kTileW, s.W - etx0);
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+      const int y = ety0 + 2 * rp + n;
+      half_t* row = out + (((size_t)eb * s.Hp + y + s.pad) * s.Wp + etx0 + s.pad) * kWidth;
+      rs[n] = __builtin_amdgcn_make_buffer_rsrc(row, (short)0, y < s.H ? ncols * 128 : 0, 0x00020000);
+    }
+  };
   int cur = 0;
   for (; t < s.tiles; t += gridDim.x) {
     int b, ty0, tx0;
     decode_tile(t, s, b, ty0, tx0);
+    if (late && have_prev) epilogue(pb, pty0, ptx0);
     const int nxt2 = cur >= 1 ? cur - 1 : 2;  // (cur + 2) % 3
     if constexpr ((ABL & 1) == 0) issue_dma(t + 2 * gridDim.x, nxt2);
     const unsigned char* hl = buf(cur);
@@ -207,7 +238,8 @@ __global__ __launch_bounds__(512, 2) void conv_body_v3_kernel(const half_t* __re
       return *reinterpret_cast<const half8_t*>(
           hl + halo_off(2 * rp + n + tap / 3, col + tap % 3, 2 * sub + h));
     };
-    floatx16 acc0 = {}, acc1 = {};
+    acc0 = floatx16{};
+    acc1 = floatx16{};
     half8_t fb[2][2];
     v4i_t sv;
 #pragma unroll
@@ -236,30 +268,16 @@ __global__ __launch_bounds__(512, 2) void conv_body_v3_kernel(const half_t* __re
         __builtin_amdgcn_sched_barrier(0);
       }
     }
-    {                                         // bias + activation -> fp16 -> staging (wave-private)
-      const float* bl = bias_l + 32 * m + 16 * h;
-      const int sw = (col >> 1) & 3;    // ds_write_b128 banks repeat every 128 B: 8 lanes distinct
-#pragma unroll
-      for (int n = 0; n < 2; ++n) {
-        const int pix = n * 32 + col;
-        const floatx16& a = n == 0 ? acc0 : acc1;
-        *reinterpret_cast<half8_t*>(stg + pix * 64 + 16 * ((2 * h) ^ sw)) = bias_act8<ACT>(a, 0, bl);
-        *reinterpret_cast<half8_t*>(stg + pix * 64 + 16 * ((2 * h + 1) ^ sw)) = bias_act8<ACT>(a, 8, bl + 8);
-      }
-      const int ncols = min(kTileW, s.W - tx0);
-#pragma unroll
-      for (int n = 0; n < 2; ++n) {
-        const int y = ty0 + 2 * rp + n;
-        half_t* row = out + (((size_t)b * s.Hp + y + s.pad) * s.Wp + tx0 + s.pad) * kWidth;
-        rs[n] = __builtin_amdgcn_make_buffer_rsrc(row, (short)0, y < s.H ? ncols * 128 : 0, 0x00020000);
-      }
-    }
+    if (!late) epilogue(b, ty0, tx0);
+    pb = b; pty0 = ty0; ptx0 = tx0;
+    have_prev = true;
     // tile t+1 landed: only the DMA of t+2 (ndma ops) and this tile's 4 stores are younger
     if (ndma == 6) asm volatile("s_waitcnt vmcnt(10) lgkmcnt(0)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(9) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     cur = cur == 2 ? 0 : cur + 1;
   }
+  if (late && have_prev) epilogue(pb, pty0, ptx0);
 #pragma unroll
   for (int j = 0; j < 4; ++j) stage_store(j, stage_read(j));
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA may land after the workgroup ends
@@ -272,6 +290,10 @@ __global__ __launch_bounds__(512, 2) void conv_body_v3_kernel(const half_t* __re
                                                      ConvShape);
 PNP_V3_INST(0, 0)
 PNP_V3_INST(0, 1)
+PNP_V3_INST(8, 0)
+PNP_V3_INST(8, 1)
+PNP_V3_INST(16, 0)
+PNP_V3_INST(24, 0)
 PNP_V3_INST(1, 0)
 PNP_V3_INST(2, 0)
 PNP_V3_INST(3, 0)
@@ -523,7 +545,9 @@ __global__ __launch_bounds__(256) void conv_head_kernel(const half_t* __restrict
                                                          ConvShape s, int act) {
   __shared__ __attribute__((aligned(16))) unsigned char wl[kHeadWBytes];
   __shared__ __attribute__((aligned(16))) uint2 hl[kHaloPix];
+  __shared__ __attribute__((aligned(16))) unsigned char stg_all[4 * 8192];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  unsigned char* stg = stg_all + wave * 8192;
   const int h = lane >> 5, col = lane & 31;
   for (int i = tid; i < kHeadWBytes / 16; i += 256) reinterpret_cast<uint4*>(wl)[i] = wpk[i];
   float bias_r[2][16];
@@ -532,17 +556,31 @@ __global__ __launch_bounds__(256) void conv_head_kernel(const half_t* __restrict
 #pragma unroll
     for (int r = 0; r < 16; ++r) bias_r[m][r] = bias[32 * m + 16 * h + r];
 
+  // the next tile's halo is loaded into registers while this tile computes (2 pixels per thread)
+  const int Wp4 = s.W + 2;                    // u16: NHWC4 with a one-pixel zero border
+  uint2 pre[2];
+  auto load_halo = [&](int tt) {
+    int pb_, pty, ptx;
+    decode_tile(tt < s.tiles ? tt : s.tiles - 1, s, pb_, pty, ptx);
+    const uint2* base = reinterpret_cast<const uint2*>(in4) + ((size_t)pb_ * (s.H + 2) + pty) * Wp4 + ptx;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int p = tid + 256 * k;
+      const int pl = p < kHaloPix ? p : kHaloPix - 1;
+      const int pr = pl / kHaloW, pc = pl - pr * kHaloW;
+      pre[k] = base[(size_t)pr * Wp4 + pc];
+    }
+  };
+  if (blockIdx.x < s.tiles) load_halo(blockIdx.x);
   for (int t = blockIdx.x; t < s.tiles; t += gridDim.x) {
     int b, ty0, tx0;
     decode_tile(t, s, b, ty0, tx0);
     __syncthreads();
-    const int Wp4 = s.W + 2;                  // u16: NHWC4 with a one-pixel zero border
-    const uint2* base = reinterpret_cast<const uint2*>(in4) + ((size_t)b * (s.H + 2) + ty0) * Wp4 + tx0;
-    for (int p = tid; p < kHaloPix; p += 256) {
-      const int pr = p / kHaloW, pc = p - pr * kHaloW;
-      hl[p] = base[(size_t)pr * Wp4 + pc];
-    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+      if (tid + 256 * k < kHaloPix) hl[tid + 256 * k] = pre[k];
     __syncthreads();
+    load_halo(t + gridDim.x);
     floatx16 acc00 = {}, acc01 = {}, acc10 = {}, acc11 = {};
 #pragma unroll
     for (int ks = 0; ks < kHeadKSteps; ++ks) {
@@ -565,8 +603,36 @@ __global__ __launch_bounds__(256) void conv_head_kernel(const half_t* __restrict
         }
       }
     }
-    store_act64(out, s, b, ty0 + 2 * wave, tx0 + col, h, acc00, acc10, bias_r, act);
-    store_act64(out, s, b, ty0 + 2 * wave + 1, tx0 + col, h, acc01, acc11, bias_r, act);
+    // epilogue through wave-private LDS staging: 2 rows x 32 pixels x 128 B, 16-B chunks
+    // XOR-swizzled by pixel (conflict-free writes), stored back as full 128-B pixel lines
+    // (1 KiB contiguous per instruction) instead of 16-B pieces at a 128-B stride.
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+      const floatx16& a0 = n == 0 ? acc00 : acc01;
+      const floatx16& a1 = n == 0 ? acc10 : acc11;
+      unsigned char* px = stg + (n * 32 + col) * 128;
+      const int sw = col & 7;
+      half8_t v[4];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        v[0][r] = (half_t)act_fn(a0[r] + bias_r[0][r], act);
+        v[1][r] = (half_t)act_fn(a0[r + 8] + bias_r[0][r + 8], act);
+        v[2][r] = (half_t)act_fn(a1[r] + bias_r[1][r], act);
+        v[3][r] = (half_t)act_fn(a1[r + 8] + bias_r[1][r + 8], act);
+      }
+      *reinterpret_cast<half8_t*>(px + 16 * ((2 * h) ^ sw)) = v[0];          // channels 16h .. +7
+      *reinterpret_cast<half8_t*>(px + 16 * ((2 * h + 1) ^ sw)) = v[1];      // 16h+8 .. +15
+      *reinterpret_cast<half8_t*>(px + 16 * ((4 + 2 * h) ^ sw)) = v[2];      // 32+16h .. +7
+      *reinterpret_cast<half8_t*>(px + 16 * ((5 + 2 * h) ^ sw)) = v[3];      // 32+16h+8 .. +15
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {             // 8 pixels x 8 chunks per instruction
+      const int n = j >> 2, p = 8 * (j & 3) + (lane >> 3), c = lane & 7;
+      const uint4 q = *reinterpret_cast<const uint4*>(stg + (n * 32 + p) * 128 + 16 * (c ^ (p & 7)));
+      const int y = ty0 + 2 * wave + n, x = tx0 + p;
+      if (y < s.H && x < s.W)
+        *reinterpret_cast<uint4*>(out + (((size_t)b * s.Hp + y + s.pad) * s.Wp + x + s.pad) * kWidth + 8 * c) = q;
+    }
   }
 }
 
@@ -766,6 +832,8 @@ ConvShape make_conv_shape(int B, int H, int W) {
 hipError_t conv_kernels_init() {
   hipError_t e = hipSuccess;
   for (const void* k : {(const void*)conv_body_v3_kernel<0, 0>, (const void*)conv_body_v3_kernel<0, 1>,
+                        (const void*)conv_body_v3_kernel<8, 0>, (const void*)conv_body_v3_kernel<8, 1>,
+                        (const void*)conv_body_v3_kernel<16, 0>, (const void*)conv_body_v3_kernel<24, 0>,
                         (const void*)conv_body_v3_kernel<1, 0>, (const void*)conv_body_v3_kernel<2, 0>,
                         (const void*)conv_body_v3_kernel<3, 0>, (const void*)conv_body_v3_kernel<4, 0>,
                         (const void*)conv_body_v3_kernel<6, 0>}) {
@@ -780,8 +848,8 @@ hipError_t conv_kernels_init() {
 }
 
 void launch_conv_head(const half_t* in4, half_t* out, const void* w, const float* bias, const ConvShape& s,
-                      int act, int num_cus, hipStream_t st) {
-  const int grid = s.tiles < num_cus * 4 ? s.tiles : num_cus * 4;
+                      int act, int num_cus, int blocks_per_cu, hipStream_t st) {
+  const int grid = s.tiles < num_cus * blocks_per_cu ? s.tiles : num_cus * blocks_per_cu;
   hipLaunchKernelGGL(conv_head_kernel, dim3(grid), dim3(256), 0, st, in4, out, (const uint4*)w, bias, s, act);
 }
 
@@ -790,11 +858,18 @@ void launch_conv_body(const half_t* in, half_t* out, const void* w, const float*
   const int grid = s.tiles < num_cus ? s.tiles : num_cus;
 #define V3(A, F) hipLaunchKernelGGL((conv_body_v3_kernel<A, F>), dim3(grid), dim3(512), kV3Lds, st, in, out, \
                                     (const uint4*)w, bias, s)
+  if (ablate == 8) {                          // staggered epilogue (PNP_TUNE_BODY_VARIANT 2)
+    if (act != 0) V3(8, 1);
+    else V3(8, 0);
+    return;
+  }
   if (act != 0) {
     V3(0, 1);
     return;
   }
   switch (ablate) {
+    case 16: V3(16, 0); break;
+    case 24: V3(24, 0); break;
     case 1: V3(1, 0); break;
     case 2: V3(2, 0); break;
     case 3: V3(3, 0); break;

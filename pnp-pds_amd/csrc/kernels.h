@@ -19,7 +19,7 @@ void pack_body_weights(const float* W, uint16_t* out);
 void pack_head_weights(const float* W, int C, uint16_t* out);
 void pack_tail_weights(const float* W, int C, uint16_t* out);
 void launch_conv_head(const half_t* in4, half_t* out, const void* w, const float* bias, const ConvShape& s,
-                      int act, int num_cus, hipStream_t st);
+                      int act, int num_cus, int blocks_per_cu, hipStream_t st);
 // one 64 -> 64 layer (variant kept for the tuning ABI; one kernel)
 void launch_conv_body(const half_t* in, half_t* out, const void* w, const float* bias, const ConvShape& s,
                       int act, int num_cus, int variant, hipStream_t st);

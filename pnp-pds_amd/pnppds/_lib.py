@@ -190,8 +190,8 @@ class Context:
         self._check(self.lib.pnp_set_tuning(self.h, TUNE_ABLATE, int(bits)))
 
     def set_body_variant(self, variant: int):
-        """Body layers per launch: 1 = two fused layers (default), 0 = one.  Performance only
-        (bit-identical results)."""
+        """Body layers per launch: 0 = one (default), 1 = two fused layers, 2 = one with the
+        staggered epilogue.  Performance only (bit-identical results)."""
         self._check(self.lib.pnp_set_tuning(self.h, TUNE_BODY_VARIANT, int(variant)))
 
     def set_operator(self, kind: int, h=None, mask=None, key=None):

@@ -58,17 +58,19 @@ def test_denoiser_ragged_batched(gpu_ctx, B, C, H, W):
 
 @pytest.mark.parametrize("B,C,H,W", [(3, 3, 50, 70), (2, 3, 256, 256)])
 def test_body_variants_bit_identical(gpu_ctx, B, C, H, W):
-    """One layer per launch and two fused layers per launch run the same MFMA K-sequence
-    per output (and the fused intermediate is the same fp16 image): same bits."""
+    """One layer per launch (plain and staggered epilogue) and two fused layers per launch run
+    the same MFMA K-sequence per output (and the fused intermediate is the same fp16 image):
+    same bits."""
     rng = np.random.default_rng(11)
     w = DenoiserWeights.load_npz(os.path.join(WEIGHTS_DIR, "DnCNN_nobn_nch_3_nlev_0.01.npz"))
     x = rng.uniform(0, 1, (B, C, H, W)).astype(np.float32)
     outs = []
-    for v in (0, 1):
+    for v in (0, 1, 2):
         gpu_ctx.set_body_variant(v)
         outs.append(run_denoise(gpu_ctx, w, x))
-    gpu_ctx.set_body_variant(1)
+    gpu_ctx.set_body_variant(0)
     np.testing.assert_array_equal(outs[0], outs[1])
+    np.testing.assert_array_equal(outs[0], outs[2])
 
 
 def test_denoiser_full_size_rgb(gpu_ctx):
