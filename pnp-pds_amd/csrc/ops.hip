@@ -489,56 +489,21 @@ __global__ __launch_bounds__(256) void pack_input_kernel(const float* __restrict
 
 // =====================================================================================
 // Register-blocked blur passes (operators.py:7-38 inside iteration.py:50/51).  The stencil
-// over a 19x19 (R = 9) or 5x5 (R = 2) kernel runs on a 64 x 128 block tile staged in LDS
-// with its periodic halo; thread (tx, ty) owns columns 2tx, 2tx+1 and rows 16ty .. +15.
-// For each of the 2R+2 LDS columns it touches, the thread loads the (16 + 2R)-row column
-// segment once into registers and applies every non-zero tap of the two kernel columns
-// that use it to its 16 x 2 accumulators: 0.2 LDS reads per FMA instead of 1 in stencil4.
-// Taps come from a dense (2R+1)^2 column-major table ([ox + R][oy + R]), one batch of
-// scalar loads per kernel column, zeros skipped by a uniform branch.
-// Per-tile partial sums are written per 32 x 32 cell (the k3 reduction grid).
+// over the kernel's non-zero taps runs on a 64 x 64 output tile of one channel plane,
+// staged in LDS with its periodic halo; thread (tx, ty) owns columns 2tx, 2tx+1 and rows
+// 8ty .. 8ty+7.  For each LDS column pair it touches, the thread loads the (8 + 2R)-row
+// column segment once into registers and applies every non-zero tap of the kernel columns
+// that use it to its 8 x 2 accumulators.  One block per (plane, tile), 6 blocks per CU.
+// (Measured slower and removed: persistent blocks that prefetch the next tile's halo into
+// registers while the current tile computes: 3 blocks per CU at 168 VGPRs, K1 0.26 vs
+// 0.22 ms, K2 0.56 vs 0.40 ms - the stencil needs the wave count more than the prefetch.)
+// The LDS halo is only as wide as the taps' non-zero columns need (blur_1: columns -4..+4
+// of 19; rows -8..+8): 72 x 80 floats instead of 80 x 80.
 // =====================================================================================
-constexpr int kRbW = 64, kRbH = 64, kRbRows = 8;   // 8 waves x 2 thread rows x 8 rows
-
-// Periodic ('wrap') halo fill of the (128+2R) x (64+2R) tile.  The loads of a batch of
-// kRbFill elements per thread are issued before any LDS store (all addresses clamped in
-// range, so the loads are unconditional and stay in flight together).
-constexpr int kRbFill = 8;
-template <int R, class F>
-__device__ __forceinline__ void rb_fill(float* lds, int i0, int j0, int H, int W, F val) {
-  constexpr int LW = kRbW + 2 * R, LH = kRbH + 2 * R, N = LW * LH;
-  for (int q0 = threadIdx.x; q0 < N; q0 += 256 * kRbFill) {
-    float v[kRbFill];
-#pragma unroll
-    for (int k = 0; k < kRbFill; ++k) {
-      const int q = min(q0 + 256 * k, N - 1);
-      const int ly = q / LW, lx = q - ly * LW;
-      int gi = i0 - R + ly, gj = j0 - R + lx;        // R <= H, W: one wrap covers the rows read
-      gi += gi < 0 ? H : 0;
-      gi -= gi >= H ? H : 0;
-      gj += gj < 0 ? W : 0;
-      gj -= gj >= W ? W : 0;
-      gi = gi < 0 ? 0 : (gi >= H ? H - 1 : gi);      // beyond: rows/cols only zero taps touch
-      gj = gj < 0 ? 0 : (gj >= W ? W - 1 : gj);
-      v[k] = val((size_t)gi * W + gj);
-    }
-#pragma unroll
-    for (int k = 0; k < kRbFill; ++k)
-      if (q0 + 256 * k < N) lds[q0 + 256 * k] = v[k];
-  }
-}
+constexpr int kRbW = 64, kRbH = 64, kRbRows = 8;   // 8 thread rows x 8 rows; 32 threads x 2 columns
 
 typedef float f2_t __attribute__((ext_vector_type(2)));
 
-// Thread (tx, ty) accumulates rows 16ty..+15 of output columns 2tx, 2tx+1 as float2
-// pairs (v_pk_fma_f32).  LDS columns are read in pairs (A = 2tx+2p, B = A+1) by one
-// ds_read_b64 per row: 32 lanes x 8 B contiguous, conflict-free.  Column A feeds output
-// column 0 with kernel column 2p and output column 1 with kernel column 2p-1; column B
-// feeds them with kernel columns 2p+1 and 2p.  Each pair of taps is one packed FMA with
-// the column value broadcast.  The loop is fully unrolled over the compile-time non-zero
-// pattern TAPS (taps_gen.h; DenseTaps<R> for any other kernel): no per-tap branches (a
-// branch per tap made hipcc copy the 32 accumulators at every join) and no loads of
-// LDS columns or weights that only zero taps touch.  Tap values are runtime data.
 template <int R>
 struct DenseTaps {
   static constexpr int kR = R;
@@ -546,21 +511,54 @@ struct DenseTaps {
   __host__ __device__ static constexpr uint32_t col(int) { return (1u << (2 * R + 1)) - 1u; }
 };
 
+// Geometry of the LDS halo for a tap pattern T.  Column pair P (LDS columns 2tx+2P-kOff and
+// +1) is active when kernel column 2P-1, 2P or 2P+1 has a non-zero tap; only pairs
+// kPmin..kPmax are read, so the LDS image starts at global column j0 - R + kOff.
+template <class T>
+struct TapGeom {
+  static constexpr int R = T::kR, D = 2 * R + 1;
+  static constexpr uint32_t colm(int k) { return k < 0 || k >= D ? 0u : T::col(k); }
+  static constexpr bool active(int P) { return (colm(2 * P - 1) | colm(2 * P) | colm(2 * P + 1)) != 0u; }
+  static constexpr int pmin() {
+    for (int P = 0; P <= R; ++P)
+      if (active(P)) return P;
+    return 0;
+  }
+  static constexpr int pmax() {
+    for (int P = R; P >= 0; --P)
+      if (active(P)) return P;
+    return 0;
+  }
+  static constexpr int kPmin = pmin(), kPmax = pmax();
+  static constexpr int kOff = 2 * kPmin;
+  static constexpr int LW = kRbW + 2 * (kPmax - kPmin), LH = kRbH + 2 * R;
+  static constexpr int N = LW * LH, NF = (N + 255) / 256;
+};
+
+// Thread (tx, ty) accumulates rows 8ty..+7 of output columns 2tx, 2tx+1 as float2 pairs
+// (v_pk_fma_f32).  LDS columns are read in pairs (A, B = A+1) by ds_read_b64: 32 lanes x
+// 8 B contiguous, conflict-free.  Column A feeds output column 0 with kernel column 2P and
+// output column 1 with kernel column 2P-1; column B feeds them with kernel columns 2P+1 and
+// 2P.  Each pair of taps is one packed FMA with the column value broadcast.  The loop is
+// fully unrolled over the compile-time non-zero pattern TAPS (taps_gen.h; DenseTaps<R> for
+// any other kernel): no per-tap branches and no loads of LDS columns or weights that only
+// zero taps touch.  Tap values are runtime data.  (Measured: one scalar v_fma_f32 per
+// non-zero tap instead - 13 % fewer FMAs, 76 % more instructions - is slower, K1 0.27 vs
+// 0.22 ms: the packed form issues at the scalar rate.)
 // wp: packed tap pairs [p][dyi][2] (float2): [.][.][0] = (W[2p][dyi], W[2p-1][dyi]) for
 // LDS column A, [.][.][1] = (W[2p+1][dyi], W[2p][dyi]) for column B (W = column-major
 // dense table, out-of-range columns 0), built on the host (pnp_set_operator) so each
 // packed FMA takes its weight pair straight from one s_load_dwordx2.
 template <class T, int P>
 __device__ __forceinline__ void rb_pair(const f2_t* base, const f2_t* __restrict__ wp, f2_t (&acc)[kRbRows]) {
-  constexpr int R = T::kR, LW = kRbW + 2 * R, D = 2 * R + 1;
-  constexpr uint32_t m0 = T::col(2 * P);
-  constexpr uint32_t mm1 = 2 * P >= 1 ? T::col(2 * P - 1) : 0u;
-  constexpr uint32_t m1 = 2 * P + 1 < D ? T::col(2 * P + 1) : 0u;
+  using G = TapGeom<T>;
+  constexpr int R = T::kR, D = G::D;
+  constexpr uint32_t m0 = G::colm(2 * P), mm1 = G::colm(2 * P - 1), m1 = G::colm(2 * P + 1);
   constexpr uint32_t mA = m0 | mm1, mB = m1 | m0;
   if constexpr ((mA | mB) != 0u) {
     f2_t cv[kRbRows + 2 * R];
 #pragma unroll
-    for (int k = 0; k < kRbRows + 2 * R; ++k) cv[k] = base[k * (LW / 2) + P];   // unused rows: dead loads
+    for (int k = 0; k < kRbRows + 2 * R; ++k) cv[k] = base[k * (G::LW / 2) + P - G::kPmin];   // unused rows: dead
 #pragma unroll
     for (int dyi = 0; dyi < D; ++dyi) {
       if ((mA >> dyi) & 1u) {
@@ -585,44 +583,98 @@ __device__ __forceinline__ void rb_pair_dispatch(int p, const f2_t* base, const 
   (void)((p == Ps ? (rb_pair<T, Ps>(base, wp, acc), true) : false) || ...);
 }
 
-// wp: packed tap pairs [p][dyi][2] (float2): [.][.][0] = (W[2p][dyi], W[2p-1][dyi]) for
-// LDS column A, [.][.][1] = (W[2p+1][dyi], W[2p][dyi]) for column B (W = column-major
-// dense table, out-of-range columns 0), built on the host (pnp_set_operator) so each
-// packed FMA takes its weight pair straight from one s_load_dwordx2.  The pair loop
-// stays a runtime loop (one straight-line, compile-time-masked body per pair), so the
-// weights and the column values of only one pair are live at a time.
+// The pair loop stays a runtime loop (one straight-line, compile-time-masked body per pair),
+// so the weights and the column values of only one pair are live at a time.
 template <class T>
 __device__ __forceinline__ void rb_stencil(const float* lds, const f2_t* __restrict__ wp, f2_t (&acc)[kRbRows]) {
-  constexpr int R = T::kR, LW = kRbW + 2 * R;
+  using G = TapGeom<T>;
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
 #pragma unroll
   for (int r = 0; r < kRbRows; ++r) acc[r] = f2_t{0.f, 0.f};
-  const f2_t* base = reinterpret_cast<const f2_t*>(lds + ty * kRbRows * LW + 2 * tx);
+  const f2_t* base = reinterpret_cast<const f2_t*>(lds + ty * kRbRows * G::LW + 2 * tx);
 #pragma unroll 1
-  for (int p = 0; p <= R; ++p) rb_pair_dispatch<T>(p, base, wp, acc, std::make_integer_sequence<int, R + 1>{});
+  for (int p = G::kPmin; p <= G::kPmax; ++p)
+    rb_pair_dispatch<T>(p, base, wp, acc, std::make_integer_sequence<int, T::kR + 1>{});
 }
 
-// One block = one 64 x 128 tile of ONE channel plane (grid (tiles, B*C)), so the halo
-// fill of one block overlaps the stencil of the others.  K1 writes its channel of the
-// NHWC4 fp16 denoiser input with 2-byte stores.
+// Periodic ('wrap') halo gather of one plane's LH x LW tile: element q = tid + 256k of the
+// LDS image comes from global (i0 - R + q / LW, j0 - R + kOff + q % LW) wrapped once (R <= H,
+// W), then clamped (rows/columns past one wrap are only read by zero taps).  The (row,
+// column) of each k is stepped from the thread's first one by compile-time increments.
+// load(k, idx) issues the loads of element k (plane-relative index idx); all NF loads of
+// a thread are independent, so they are in flight together.
+template <class G, int K0 = 0, int K1 = G::NF, class F>
+__device__ __forceinline__ void rb_gather(int i0, int j0, int H, int W, F&& load) {
+  const int tid = threadIdx.x;
+  const int ly0 = tid / G::LW, lx0 = tid - ly0 * G::LW;
+  const int ci = i0 - G::R, cj = j0 - G::R + G::kOff;
+#pragma unroll
+  for (int k = K0; k < K1; ++k) {
+    const int dy = (256 * k) / G::LW, dx = (256 * k) % G::LW;
+    int lx = lx0 + dx, ly = ly0 + dy;
+    const bool carry = lx >= G::LW;
+    lx = carry ? lx - G::LW : lx;
+    ly = carry ? ly + 1 : ly;
+    ly = min(ly, G::LH - 1);                       // q >= N: any in-range element, never stored
+    int gi = ci + ly, gj = cj + lx;
+    gi += gi < 0 ? H : 0;
+    gi -= gi >= H ? H : 0;
+    gj += gj < 0 ? W : 0;
+    gj -= gj >= W ? W : 0;
+    gi = min(max(gi, 0), H - 1);
+    gj = min(max(gj, 0), W - 1);
+    load(k - K0, gi * W + gj);
+  }
+}
+
+// Halo fill: batches of kRbFill elements per thread (the loads of a batch in flight
+// together, then their LDS stores), so few registers are live and 6 blocks fit per CU.  val(a, b) combines the values of the two source
+// planes (b is unused for one-plane fills).
+constexpr int kRbFill = 8;
+template <class G, int K0, class FA, class FB, class FV>
+__device__ __forceinline__ void rb_fill_batch(float* lds, int i0, int j0, int H, int W, FA&& la, FB&& lb, FV&& val) {
+  constexpr int K1 = K0 + kRbFill < G::NF ? K0 + kRbFill : G::NF;
+  float a[kRbFill], b[kRbFill];
+  rb_gather<G, K0, K1>(i0, j0, H, W, [&](int k, int idx) {
+    a[k] = la(idx);
+    b[k] = lb(idx);
+  });
+#pragma unroll
+  for (int k = K0; k < K1; ++k) {
+    const int q = threadIdx.x + 256 * k;
+    if (G::N % 256 == 0 || q < G::N) lds[q] = val(a[k - K0], b[k - K0]);
+  }
+  if constexpr (K1 < G::NF) rb_fill_batch<G, K1>(lds, i0, j0, H, W, la, lb, val);
+}
+
+__device__ __forceinline__ void rb_tile_origin(int tile, int tiles_x, int& i0, int& j0) {
+  const int ty = tile / tiles_x;
+  i0 = ty * kRbH;
+  j0 = (tile - ty * tiles_x) * kRbW;
+}
+
+// K1: u = [clamp](x - g1 Phi^T y) -> u32 and its channel of the NHWC4 fp16 denoiser input
+// u16 (2-byte stores); B: w = s - g1 y.  Block = one (plane, 64 x 64 tile).
 template <class T>
 __global__ __launch_bounds__(256) void k1_blur_rb(const float* __restrict__ x, const float* __restrict__ y,
                                                    const float* __restrict__ s, float* __restrict__ u32,
                                                    half_t* __restrict__ u16, float* __restrict__ w,
-                                                   const f2_t* __restrict__ wd_adj, int C, int H, int W,
-                                                   int tiles_x, float gamma1, int clamp_in, int method_b) {
-  constexpr int R = T::kR;
-  __shared__ float lds[(kRbW + 2 * R) * (kRbH + 2 * R)];
-  const int tile = blockIdx.x, bc = blockIdx.y, b = bc / C, c = bc - b * C;
-  const int i0 = (tile / tiles_x) * kRbH, j0 = (tile % tiles_x) * kRbW;
+                                                   const f2_t* __restrict__ wd_adj, int C, int H, int W, int tiles_x,
+                                                   int tiles, float gamma1, int clamp_in, int method_b) {
+  using G = TapGeom<T>;
+  __shared__ float lds[G::N];
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
-  const size_t plane = (size_t)H * W;
-  const float* yp = y + (size_t)bc * plane;
-  rb_fill<R>(lds, i0, j0, H, W, [&](size_t k) { return yp[k]; });
+  const int bc = blockIdx.x / tiles, b = bc / C, c = bc - b * C;
+  int i0, j0;
+  rb_tile_origin(blockIdx.x - bc * tiles, tiles_x, i0, j0);
+  const int j = j0 + 2 * tx;
+  const size_t pb = (size_t)bc * H * W;
+  const float* yp = y + pb;
+  rb_fill_batch<G, 0>(lds, i0, j0, H, W, [&](int k) { return yp[k]; }, [](int) { return 0.f; },
+                      [](float a, float) { return a; });
   __syncthreads();
   f2_t g[kRbRows];
   rb_stencil<T>(lds, wd_adj, g);
-  const int j = j0 + 2 * tx;
 #pragma unroll
   for (int r = 0; r < kRbRows; ++r) {
     const int i = i0 + ty * kRbRows + r;
@@ -630,104 +682,112 @@ __global__ __launch_bounds__(256) void k1_blur_rb(const float* __restrict__ x, c
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       if (j + q >= W) break;
-      const size_t idx = (size_t)bc * plane + (size_t)i * W + j + q;
-      float u = x[idx] - gamma1 * g[r][q];
-      if (clamp_in) u = fminf(fmaxf(u, 0.f), 1.f);
-      u32[idx] = u;
-      u16[(((size_t)b * (H + 2) + i + 1) * (W + 2) + j + q + 1) * 4 + c] = (half_t)u;
+      const size_t idx = pb + (size_t)i * W + j + q;
+      float uu = x[idx] - gamma1 * g[r][q];
+      if (clamp_in) uu = fminf(fmaxf(uu, 0.f), 1.f);
+      u32[idx] = uu;
+      u16[(((size_t)b * (H + 2) + i + 1) * (W + 2) + j + q + 1) * 4 + c] = (half_t)uu;
       if (method_b) w[idx] = s[idx] - gamma1 * y[idx];
     }
   }
 }
 
-// partials: [B][cells][C][4] (per 32 x 32 cell and channel), reduced by k3 in that order.
+// K2: v = y + g2 (Phi(2x+ - x) [+ 2 s+ - s]), s+ = shrink(w, theta) (B), the GKL prox (C),
+// per-cell partial sums.  Block = one (plane, 64 x 64 tile).  partials: [B][cells][C][4]
+// (per 32 x 32 cell and channel), reduced by k3 in that order.
 template <class T, int METHOD>
 __global__ __launch_bounds__(256) void k2_blur_rb(const float* __restrict__ xn, const float* __restrict__ xo,
                                                    float* __restrict__ y, const float* __restrict__ xobs,
                                                    const float* __restrict__ xtrue, float* __restrict__ s,
                                                    const float* __restrict__ w, const float* __restrict__ theta,
                                                    double* __restrict__ partials, const f2_t* __restrict__ wd_fwd,
-                                                   int C, int H, int W, int tiles_x, int cells_x, int cells,
-                                                   double gamma2, double gkl_gamma, double gkl_alpha, int record) {
-  constexpr int R = T::kR;
-  __shared__ float lds[(kRbW + 2 * R) * (kRbH + 2 * R)];
-  const int tile = blockIdx.x, bc = blockIdx.y, b = bc / C, c = bc - b * C;
-  const int i0 = (tile / tiles_x) * kRbH, j0 = (tile % tiles_x) * kRbW;
+                                                   int C, int H, int W, int tiles_x, int tiles, int cells_x, int cells,
+                                                   double gamma2, double inv_g2, double gkl_gamma, double gkl_alpha,
+                                                   int record) {
+  using G = TapGeom<T>;
+  __shared__ float lds[G::N];
+  __shared__ double red[8][2][4];
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int bc = blockIdx.x / tiles, b = bc / C, c = bc - b * C;
+  int i0, j0;
+  rb_tile_origin(blockIdx.x - bc * tiles, tiles_x, i0, j0);
   const size_t plane = (size_t)H * W;
-  const float* xnp = xn + (size_t)bc * plane;
-  const float* xop = xo + (size_t)bc * plane;
-  rb_fill<R>(lds, i0, j0, H, W, [&](size_t k) { return 2.f * xnp[k] - xop[k]; });
+  {
+    const float* xnp = xn + (size_t)bc * plane;
+    const float* xop = xo + (size_t)bc * plane;
+    rb_fill_batch<G, 0>(lds, i0, j0, H, W, [&](int k) { return xnp[k]; }, [&](int k) { return xop[k]; },
+                        [](float a, float b) { return 2.f * a - b; });   // Phi(2x+ - x)'s argument
+  }
   __syncthreads();
   f2_t g[kRbRows];
   rb_stencil<T>(lds, wd_fwd, g);
-  double d2 = 0, e2 = 0, n2 = 0, t2 = 0;
-  const float th = METHOD == M_B ? theta[b] : 0.f;
-  const int j = j0 + 2 * tx;
+  {
+    double d2 = 0, e2 = 0, n2 = 0, t2 = 0;
+    const float th = METHOD == M_B ? theta[b] : 0.f;
+    const int j = j0 + 2 * tx;
 #pragma unroll
-  for (int r = 0; r < kRbRows; ++r) {
-    const int i = i0 + ty * kRbRows + r;
-    if (i >= H) break;
+    for (int r = 0; r < kRbRows; ++r) {
+      const int i = i0 + ty * kRbRows + r;
+      if (i >= H) break;
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      if (j + q >= W) break;
-      const size_t idx = (size_t)bc * plane + (size_t)i * W + j + q;
-      double gv = g[r][q];
-      if (METHOD == M_B) {
-        const float wv = w[idx];
-        const float sp = copysignf(fmaxf(fabsf(wv) - th, 0.f), wv);   // operators.py:98
-        gv += 2.0 * (double)sp - (double)s[idx];
-        s[idx] = sp;
-      }
-      const double v = (double)y[idx] + gamma2 * gv;
-      const double ob = xobs[idx];
-      if (METHOD == M_C) {
-        const double vv = v / gamma2;
-        const double tt = vv - gkl_gamma * gkl_alpha;
-        const double p = 0.5 * (tt + sqrt(tt * tt + 4.0 * gkl_gamma * ob));
-        y[idx] = (float)(v - gamma2 * p);
-      } else {
-        y[idx] = (float)v;
-        const double dd = v / gamma2 - ob;
-        d2 += dd * dd;
-      }
-      if (record) {
-        const double a = xn[idx], o = xo[idx];
-        e2 += (a - o) * (a - o);
-        n2 += o * o;
-        if (xtrue) {
-          const double qv = (double)xtrue[idx] - a;
-          t2 += qv * qv;
+      for (int q = 0; q < 2; ++q) {
+        if (j + q >= W) break;
+        const size_t idx = (size_t)bc * plane + (size_t)i * W + j + q;
+        double gv = g[r][q];
+        if (METHOD == M_B) {
+          const float wv = w[idx];
+          const float sp = copysignf(fmaxf(fabsf(wv) - th, 0.f), wv);   // operators.py:98
+          gv += 2.0 * (double)sp - (double)s[idx];
+          s[idx] = sp;
+        }
+        const double v = (double)y[idx] + gamma2 * gv;
+        const double ob = xobs[idx];
+        if (METHOD == M_C) {
+          const double tt = v * inv_g2 - gkl_gamma * gkl_alpha;
+          const double p = 0.5 * (tt + sqrt(tt * tt + 4.0 * gkl_gamma * ob));
+          y[idx] = (float)(v - gamma2 * p);
+        } else {
+          y[idx] = (float)v;
+          const double dd = v * inv_g2 - ob;
+          d2 += dd * dd;
+        }
+        if (record) {
+          const double a = xn[idx], o = xo[idx];
+          e2 += (a - o) * (a - o);
+          n2 += o * o;
+          if (xtrue) {
+            const double qv = (double)xtrue[idx] - a;
+            t2 += qv * qv;
+          }
         }
       }
     }
-  }
-  // 32 x 32 cell = 16 threads (tx) x 4 thread rows (ty) = two half-cells of two waves:
-  // reduce each half in its wave (lanes {c, c+32}: xor 32, then xor 8..1), then combine
-  // the two waves' halves through LDS in a fixed order.
-  auto half_sum = [](double v) {
-    v += __shfl_xor(v, 32, 64);
+    // 32 x 32 cell = 16 threads (tx) x 4 thread rows (ty) = two half-cells of two waves:
+    // reduce each half in its wave (lanes {c, c+32}: xor 32, then xor 8..1), then combine
+    // the two waves' halves through LDS in a fixed order.
+    auto half_sum = [](double v) {
+      v += __shfl_xor(v, 32, 64);
 #pragma unroll
-    for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-  };
-  __shared__ double red[8][2][4];
-  d2 = half_sum(d2);
-  e2 = half_sum(e2);
-  n2 = half_sum(n2);
-  t2 = half_sum(t2);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if ((lane & 47) == 0) {                              // lanes 0 and 16: the wave's two half-cells
-    double* q = red[wave][lane >> 4];
-    q[0] = d2; q[1] = e2; q[2] = n2; q[3] = t2;
-  }
-  __syncthreads();
-  if (threadIdx.x < 16) {                              // 2 x 2 cells x 4 sums
-    const int cell = threadIdx.x >> 2, k = threadIdx.x & 3, cy = cell >> 1, cx = cell & 1;
-    const int gy = i0 / 32 + cy, gx = j0 / 32 + cx;
-    if (gy * 32 < H && gx < cells_x)
-      partials[(((size_t)b * cells + (size_t)gy * cells_x + gx) * C + c) * 4 + k] =
-          red[2 * cy][cx][k] + red[2 * cy + 1][cx][k];
+      for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+      return v;
+    };
+    d2 = half_sum(d2);
+    e2 = half_sum(e2);
+    n2 = half_sum(n2);
+    t2 = half_sum(t2);
+    if ((lane & 47) == 0) {                              // lanes 0 and 16: the wave's two half-cells
+      double* q = red[wave][lane >> 4];
+      q[0] = d2; q[1] = e2; q[2] = n2; q[3] = t2;
+    }
+    __syncthreads();
+    if (threadIdx.x < 16) {                              // 2 x 2 cells x 4 sums
+      const int cell = threadIdx.x >> 2, k = threadIdx.x & 3, cy = cell >> 1, cx = cell & 1;
+      const int gy = i0 / 32 + cy, gx = j0 / 32 + cx;
+      if (gy * 32 < H && gx < cells_x)
+        partials[(((size_t)b * cells + (size_t)gy * cells_x + gx) * C + c) * 4 + k] =
+            red[2 * cy][cx][k] + red[2 * cy + 1][cx][k];
+    }
   }
 }
 
@@ -1000,20 +1060,19 @@ inline TileGrid tile_grid(int H, int W) {
 static bool rb_ok(const OpDesc& op, int C) { return op.kind == OP_BLUR && op.dense_fwd && op.Rd > 0 && C >= 1; }
 
 template <class T>
-static void launch_k1_rb(dim3 grid, hipStream_t st, const float* x, const float* y, const float* s, float* u32,
-                         half_t* u16, float* w, const OpDesc& op, int C, int H, int W, int tiles_x, float gamma1,
-                         int clamp_in, int method_b) {
-  hipLaunchKernelGGL((k1_blur_rb<T>), grid, dim3(256), 0, st, x, y, s, u32, u16, w, reinterpret_cast<const f2_t*>(op.dense_adj), C, H, W, tiles_x,
-                     gamma1, clamp_in, method_b);
+static void launch_k1_rb(hipStream_t st, const float* x, const float* y, const float* s, float* u32, half_t* u16,
+                         float* w, const OpDesc& op, int B, int C, int H, int W, float gamma1, int clamp_in,
+                         int method_b) {
+  const int tx = (W + kRbW - 1) / kRbW, tiles = tx * ((H + kRbH - 1) / kRbH);
+  hipLaunchKernelGGL((k1_blur_rb<T>), dim3(B * C * tiles), dim3(256), 0, st, x, y, s, u32, u16, w,
+                     reinterpret_cast<const f2_t*>(op.dense_adj), C, H, W, tx, tiles, gamma1, clamp_in, method_b);
 }
 
 void launch_k1(int kind, const float* x, const float* y, const float* s, float* u32, half_t* u16, float* w,
                const OpDesc& op, int B, int C, int H, int W, float gamma1, int clamp_in, int method_b,
                hipStream_t st) {
   if (kind == OP_BLUR && rb_ok(op, C)) {
-    const int tx = (W + kRbW - 1) / kRbW, ty = (H + kRbH - 1) / kRbH;
-    const dim3 grid(tx * ty, B * C);
-#define K1RB(TT) launch_k1_rb<TT>(grid, st, x, y, s, u32, u16, w, op, C, H, W, tx, gamma1, clamp_in, method_b)
+#define K1RB(TT) launch_k1_rb<TT>(st, x, y, s, u32, u16, w, op, B, C, H, W, gamma1, clamp_in, method_b)
     switch (op.taps_id) {
       case TAPS_BLUR_1: K1RB(Taps_blur_1_Adj); break;
       case TAPS_SQUARE_MINI: K1RB(Taps_square_mini_Adj); break;
@@ -1046,12 +1105,14 @@ static void launch_k2_kind(int method, dim3 grid, hipStream_t st, const float* x
 }
 
 template <class T>
-static void launch_k2_rb(int method, dim3 grid, hipStream_t st, const float* xn, const float* xo, float* y,
-                         const float* xobs, const float* xtrue, float* s, const float* w, const float* theta,
-                         double* partials, const OpDesc& op, int C, int H, int W, int tiles_x, int cells_x, int cells,
-                         double gamma2, double gkl_gamma, double gkl_alpha, int record) {
-#define K2RB_ARGS xn, xo, y, xobs, xtrue, s, w, theta, partials, reinterpret_cast<const f2_t*>(op.dense_fwd), C, H, W, tiles_x, cells_x, cells, gamma2, \
-                  gkl_gamma, gkl_alpha, record
+static void launch_k2_rb(int method, hipStream_t st, const float* xn, const float* xo, float* y, const float* xobs,
+                         const float* xtrue, float* s, const float* w, const float* theta, double* partials,
+                         const OpDesc& op, int B, int C, int H, int W, int cells_x, int cells, double gamma2,
+                         double gkl_gamma, double gkl_alpha, int record) {
+  const int tx = (W + kRbW - 1) / kRbW, tiles = tx * ((H + kRbH - 1) / kRbH);
+  const dim3 grid(B * C * tiles);
+#define K2RB_ARGS xn, xo, y, xobs, xtrue, s, w, theta, partials, reinterpret_cast<const f2_t*>(op.dense_fwd), C, H, W, \
+                  tx, tiles, cells_x, cells, gamma2, 1.0 / gamma2, gkl_gamma, gkl_alpha, record
   if (method == M_A) hipLaunchKernelGGL((k2_blur_rb<T, M_A>), grid, dim3(256), 0, st, K2RB_ARGS);
   else if (method == M_B) hipLaunchKernelGGL((k2_blur_rb<T, M_B>), grid, dim3(256), 0, st, K2RB_ARGS);
   else hipLaunchKernelGGL((k2_blur_rb<T, M_C>), grid, dim3(256), 0, st, K2RB_ARGS);
@@ -1064,9 +1125,7 @@ void launch_k2(int kind, int method, const float* xn, const float* xo, float* y,
                int record, hipStream_t st) {
   const TileGrid g = tile_grid(H, W);
   if (kind == OP_BLUR && rb_ok(op, C)) {
-    const int tx = (W + kRbW - 1) / kRbW, ty = (H + kRbH - 1) / kRbH;
-    const dim3 grid(tx * ty, B * C);
-#define K2RB(TT) launch_k2_rb<TT>(method, grid, st, xn, xo, y, xobs, xtrue, s, w, theta, partials, op, C, H, W, tx, \
+#define K2RB(TT) launch_k2_rb<TT>(method, st, xn, xo, y, xobs, xtrue, s, w, theta, partials, op, B, C, H, W, \
                                   g.tiles_x, g.tiles, gamma2, gkl_gamma, gkl_alpha, record)
     switch (op.taps_id) {
       case TAPS_BLUR_1: K2RB(Taps_blur_1_Fwd); break;
