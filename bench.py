@@ -150,9 +150,15 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     import torch.distributed as dist
+    # Rehearsal of the N-rank path on fewer GPUs (never used by the driver): PNP_BENCH_REHEARSAL=1
+    # maps ranks onto the visible devices round-robin and does the barrier / max over gloo.
+    rehearsal = os.environ.get("PNP_BENCH_REHEARSAL") == "1"
+    if rehearsal:
+        local %= torch.cuda.device_count()
+    backend = "gloo" if rehearsal else "nccl"
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", init_method="env://")
+        dist.init_process_group(backend, init_method="env://")
     from pnppds import _lib
     from pnppds.iteration import make_params
     from pnppds.operators import load_blur_kernel
@@ -228,7 +234,7 @@ def main():
     t_el = time.perf_counter() - t_start
     if world > 1:
         dist.barrier()
-        t_el = max_over_ranks(t_el, device=f"cuda:{local}")   # job time = slowest rank
+        t_el = max_over_ranks(t_el, device=None if rehearsal else f"cuda:{local}")   # job time = slowest rank
     prof = ctx.profile_read() if args.profile else {}
     x_out, s_out, c_hist, psnr_hist, ssim_hist = ctx.solver_fetch()
 
