@@ -861,8 +861,11 @@ __device__ __forceinline__ float ssim_s(float ux, float uy, float uxx, float uyy
 // magnitudes in play, so running sums give scipy's axis-by-axis means bit for bit after the
 // float32 rounding; the mean is sum * (1/7) (within an ulp of float64 of scipy's division).
 constexpr double kInv7 = 1.0 / 7.0;
-constexpr int kSsTW = 64, kSsTH = 32;             // output tile; vertical sums for 70 columns
-constexpr int kSsVW = kSsTW + 6, kSsVS = 71;      // LDS row stride 71: conflict-free row segments
+// Output tile 56 x 32: the vertical sums of its 62 columns take one pass of a 64-lane wave,
+// the horizontal pass 7 segments of 8 columns per row, and the LDS (40 KiB) fits 4 blocks
+// per CU.  (64 x 32 with 70 columns: two vertical passes, 45 KiB, 3 blocks: 0.30 ms.)
+constexpr int kSsTW = 56, kSsTH = 32;
+constexpr int kSsVW = kSsTW + 6, kSsVS = 63;      // odd LDS row stride
 
 // grid (tiles, B*C), block 256 = 4 waves.  Vertical pass: thread (column, 8-row segment) with
 // running sums straight from HBM/L2; horizontal pass: thread (row, 8-column segment) with
@@ -917,12 +920,12 @@ __global__ __launch_bounds__(256) void ssim_rgb_kernel(const float* __restrict__
     }
   }
   __syncthreads();
-  // ---- horizontal + SSIM map: row r = t / 8, columns 8*(t % 8) .. +8 ----
+  // ---- horizontal + SSIM map: row r = t / 8, columns 8*(t % 8) .. +8 (segments 0..6) ----
   const int r = threadIdx.x >> 3, c0 = (threadIdx.x & 7) * 8;
   const int i = i0 + r;
   const float C1 = cst[0], C2 = cst[1];
   double acc = 0;
-  if (i >= 3 && i < H - 3) {
+  if (c0 < kSsTW && i >= 3 && i < H - 3) {
     double h[5];
 #pragma unroll
     for (int u = 0; u < 5; ++u) {
