@@ -142,6 +142,8 @@ def main():
     ap.add_argument("--chunk-sweep", type=str, default="", help="e.g. 4,8,16,256: time each (stderr)")
     ap.add_argument("--variant", type=int, default=0, help="body layers per launch: 0 = one (default), 1 = two fused")
     ap.add_argument("--variant-sweep", type=str, default="", help="e.g. 0,1: interleaved A/B (stderr)")
+    ap.add_argument("--op", default="blur", choices=["blur", "Id", "random_sampling"],
+                    help="degradation operator (the metric's is blur; the others time the elementwise K1/K2)")
     ap.add_argument("--ablate", type=int, default=0, help="profiling only (results wrong): 1 DMA, 2 stores, 4 MFMA")
     args = ap.parse_args()
 
@@ -170,7 +172,13 @@ def main():
     ctx = _lib.Context(local)
     ctx.set_denoiser(resolve_weights(ARCH, 3))
     h = load_blur_kernel("blur_1")
-    ctx.set_operator(_lib.OP_BLUR, h=h)
+    if args.op == "blur":
+        ctx.set_operator(_lib.OP_BLUR, h=h)
+    elif args.op == "Id":
+        ctx.set_operator(_lib.OP_ID)
+    else:
+        from pnppds.operators import sampling_keep_mask
+        ctx.set_operator(_lib.OP_RANDOM_SAMPLING, mask=sampling_keep_mask(H, W, 0.8))
 
     # ---- synthetic inputs, degraded on the device exactly as main.py:49-64 does ---------------
     t0 = time.perf_counter()
@@ -249,7 +257,8 @@ def main():
                     "(main.py:49-64, generated on device); real "
                     "DnCNN_nobn_nch_3_nlev_0.01 weights",
             "config": {"workload": f"ours-A (A-Proposed) blur, batch={B}/GPU RGB {H}x{W}", "global_batch": B * world,
-                       "image": f"{C}x{H}x{W}", "deg_op": "blur_1", "method": "ours-A",
+                       "image": f"{C}x{H}x{W}", "deg_op": "blur_1" if args.op == "blur" else args.op,
+                       "method": "ours-A",
                        "parallelism": f"dp{world} (independent image shards, no collective)"},
             "batch_iters_per_s": round(K / t_el, 3),
         }
@@ -287,7 +296,7 @@ def main():
                                 for k in pb if k in prof}
         line["psnr_img0_db"] = [round(float(psnr_hist[0, 0]), 4), round(float(psnr_hist[0, cap - 1]), 4)]
         line["ssim_img0"] = [round(float(ssim_hist[0, 0]), 5), round(float(ssim_hist[0, cap - 1]), 5)]
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and args.op == "blur":
             rate, n_cpu, ps_cpu, thr = cpu_baseline(x_true[0], d_obs[0].cpu().numpy(), h, args.cpu_budget, cap)
             line["cpu_baseline"] = {"value": round(rate, 3), "unit": "image-iterations/s", "cores": thr,
                                     "kind": "port",

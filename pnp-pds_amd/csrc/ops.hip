@@ -214,6 +214,174 @@ __global__ __launch_bounds__(256) void k2_dual(const float* __restrict__ xn, con
   }
 }
 
+// =====================================================================================
+// K1 / K2 for the pointwise operators ('Id' and 'random_sampling', operators.py:40-79):
+// pure streaming passes.  Block = one 32 x 32 tile of an image (all C channels), thread =
+// 4 consecutive pixels of one row: 16-B loads and stores where the row allows (W % 4 == 0),
+// scalar otherwise.  K2's four partial sums are reduced once per block (wave shuffles, then
+// the 4 waves in a fixed order): partials [B][tiles][4], the layout k3 re-reduces.
+// =====================================================================================
+template <int KIND>
+__device__ __forceinline__ float4 op_apply4(float4 v, const uint8_t* __restrict__ mask, size_t pix, bool vec, int nv) {
+  if (KIND == OP_MASK) {                 // select (t[q] = 0), so a NaN/inf at a dropped pixel cannot leak
+    uchar4 m = {0, 0, 0, 0};
+    if (vec) {
+      m = *reinterpret_cast<const uchar4*>(mask + pix);
+    } else {
+      if (nv > 0) m.x = mask[pix];
+      if (nv > 1) m.y = mask[pix + 1];
+      if (nv > 2) m.z = mask[pix + 2];
+      if (nv > 3) m.w = mask[pix + 3];
+    }
+    v.x = m.x ? v.x : 0.f; v.y = m.y ? v.y : 0.f; v.z = m.z ? v.z : 0.f; v.w = m.w ? v.w : 0.f;
+  }
+  return v;
+}
+
+__device__ __forceinline__ float4 ld4(const float* __restrict__ p, bool vec, int nv) {
+  if (vec) return *reinterpret_cast<const float4*>(p);
+  float4 v = {0.f, 0.f, 0.f, 0.f};
+  if (nv > 0) v.x = p[0];
+  if (nv > 1) v.y = p[1];
+  if (nv > 2) v.z = p[2];
+  if (nv > 3) v.w = p[3];
+  return v;
+}
+__device__ __forceinline__ void st4(float* __restrict__ p, float4 v, bool vec, int nv) {
+  if (vec) { *reinterpret_cast<float4*>(p) = v; return; }
+  if (nv > 0) p[0] = v.x;
+  if (nv > 1) p[1] = v.y;
+  if (nv > 2) p[2] = v.z;
+  if (nv > 3) p[3] = v.w;
+}
+__device__ __forceinline__ float f4get(const float4& v, int k) { return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w; }
+
+// K1: thread = one pixel column of 4 rows (consecutive lanes on consecutive pixels, so each
+// 8-B NHWC4 store of u16 is part of one contiguous 512-B wave store).  NC = C when it is a
+// compile-time 1 or 3 (all channels' loads in flight together), 0 = runtime C <= 4.
+template <int KIND, int NC>
+__global__ __launch_bounds__(256) void k1_elem(const float* __restrict__ x, const float* __restrict__ y,
+                                                const float* __restrict__ s, float* __restrict__ u32,
+                                                half_t* __restrict__ u16, float* __restrict__ w,
+                                                const uint8_t* __restrict__ mask, int Crt, int H, int W, int tiles_x,
+                                                float gamma1, int clamp_in, int method_b) {
+  constexpr int CM = NC ? NC : kMaxC;
+  const int C = NC ? NC : Crt;
+  const int tile = blockIdx.x, b = blockIdx.y;
+  const int ty = tile / tiles_x;
+  const int i0 = ty * kST + 4 * (threadIdx.x >> 5), j = (tile - ty * tiles_x) * kST + (threadIdx.x & 31);
+  if (j >= W) return;
+  const size_t plane = (size_t)H * W;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = i0 + r;
+    if (i >= H) break;
+    const size_t pix = (size_t)i * W + j;
+    const bool keep = KIND != OP_MASK || mask[pix] != 0;
+    float xv[CM], yv[CM];
+#pragma unroll
+    for (int c = 0; c < CM; ++c) {
+      if (c >= C) break;
+      const size_t o = ((size_t)b * C + c) * plane + pix;
+      xv[c] = x[o];
+      yv[c] = y[o];
+    }
+    half4_t h4 = {0, 0, 0, 0};
+#pragma unroll
+    for (int c = 0; c < CM; ++c) {
+      if (c >= C) break;
+      const size_t o = ((size_t)b * C + c) * plane + pix;
+      const float g = keep ? yv[c] : 0.f;    // random_sampling: t[q] = 0 (a NaN cannot leak)
+      float u = xv[c] - gamma1 * g;
+      if (clamp_in) u = fminf(fmaxf(u, 0.f), 1.f);
+      u32[o] = u;
+      h4[c] = (half_t)u;
+      if (method_b) w[o] = s[o] - gamma1 * yv[c];
+    }
+    *reinterpret_cast<half4_t*>(u16 + (((size_t)b * (H + 2) + i + 1) * (W + 2) + j + 1) * 4) = h4;
+  }
+}
+
+template <int KIND, int METHOD, int NC>
+__global__ __launch_bounds__(256) void k2_elem(const float* __restrict__ xn, const float* __restrict__ xo,
+                                                float* __restrict__ y, const float* __restrict__ xobs,
+                                                const float* __restrict__ xtrue, float* __restrict__ s,
+                                                const float* __restrict__ w, const float* __restrict__ theta,
+                                                double* __restrict__ partials, const uint8_t* __restrict__ mask,
+                                                int Crt, int H, int W, int tiles_x, int tiles, double gamma2,
+                                                double inv_g2, double gkl_gamma, double gkl_alpha, int record) {
+  constexpr int CM = NC ? NC : kMaxC;
+  const int C = NC ? NC : Crt;
+  __shared__ double red[4][4];
+  const int tile = blockIdx.x, b = blockIdx.y;
+  const int ty = tile / tiles_x;
+  const int i = ty * kST + (threadIdx.x >> 3), j = (tile - ty * tiles_x) * kST + 4 * (threadIdx.x & 7);
+  double d2 = 0, e2 = 0, n2 = 0, t2 = 0;
+  if (i < H && j < W) {
+    const int nv = min(4, W - j);
+    const bool vec = (W & 3) == 0 && nv == 4;
+    const size_t plane = (size_t)H * W, pix = (size_t)i * W + j;
+    const float th = METHOD == M_B ? theta[b] : 0.f;
+#pragma unroll
+    for (int c = 0; c < CM; ++c) {
+      if (c >= C) break;
+      const size_t o = ((size_t)b * C + c) * plane + pix;
+      const float4 a4 = ld4(xn + o, vec, nv), o4 = ld4(xo + o, vec, nv);
+      float4 g4;
+      g4.x = 2.f * a4.x - o4.x; g4.y = 2.f * a4.y - o4.y; g4.z = 2.f * a4.z - o4.z; g4.w = 2.f * a4.w - o4.w;
+      g4 = op_apply4<KIND>(g4, mask, pix, vec, nv);
+      const float4 y4 = ld4(y + o, vec, nv), b4 = ld4(xobs + o, vec, nv);
+      float4 s4 = {}, w4 = {}, sp4 = {}, t4 = {}, yo;
+      if (METHOD == M_B) { s4 = ld4(s + o, vec, nv); w4 = ld4(w + o, vec, nv); }
+      if (record && xtrue) t4 = ld4(xtrue + o, vec, nv);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        double gv = f4get(g4, k);
+        if (METHOD == M_B) {
+          const float wv = f4get(w4, k);
+          const float sp = copysignf(fmaxf(fabsf(wv) - th, 0.f), wv);   // operators.py:98
+          gv += 2.0 * (double)sp - (double)f4get(s4, k);
+          (k == 0 ? sp4.x : k == 1 ? sp4.y : k == 2 ? sp4.z : sp4.w) = sp;
+        }
+        const double v = (double)f4get(y4, k) + gamma2 * gv;
+        const double ob = f4get(b4, k);
+        float yk;
+        if (METHOD == M_C) {
+          const double tt = v * inv_g2 - gkl_gamma * gkl_alpha;
+          const double p = 0.5 * (tt + sqrt(tt * tt + 4.0 * gkl_gamma * ob));
+          yk = (float)(v - gamma2 * p);
+        } else {
+          yk = (float)v;
+          const double dd = v * inv_g2 - ob;
+          if (k < nv) d2 += dd * dd;
+        }
+        (k == 0 ? yo.x : k == 1 ? yo.y : k == 2 ? yo.z : yo.w) = yk;
+        if (record && k < nv) {
+          const double a = f4get(a4, k), oo = f4get(o4, k);
+          e2 += (a - oo) * (a - oo);
+          n2 += oo * oo;
+          if (xtrue) {
+            const double q = (double)f4get(t4, k) - a;
+            t2 += q * q;
+          }
+        }
+      }
+      st4(y + o, yo, vec, nv);
+      if (METHOD == M_B) st4(s + o, sp4, vec, nv);
+    }
+  }
+  d2 = wave_sum(d2);
+  e2 = wave_sum(e2);
+  n2 = wave_sum(n2);
+  t2 = wave_sum(t2);
+  const int wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { red[wv][0] = d2; red[wv][1] = e2; red[wv][2] = n2; red[wv][3] = t2; }
+  __syncthreads();
+  if (threadIdx.x < 4)
+    partials[((size_t)b * tiles + tile) * 4 + threadIdx.x] =
+        ((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x];
+}
+
 // Deterministic reduction of one image's tile partials (fixed order) in a 256-block.
 __device__ __forceinline__ void reduce_partials(const double* __restrict__ partials, int b, int tiles,
                                                 double (&out)[4], double* red) {
@@ -1088,9 +1256,16 @@ void launch_k1(int kind, const float* x, const float* y, const float* s, float* 
   const TileGrid g = tile_grid(H, W);
   dim3 grid(g.tiles, B);
 #define K1_ARGS x, y, s, u32, u16, w, op, C, H, W, g.tiles_x, gamma1, clamp_in, method_b
+#define K1E_ARGS x, y, s, u32, u16, w, op.mask, C, H, W, g.tiles_x, gamma1, clamp_in, method_b
+#define K1E(KD)                                                                              \
+  if (C == 3) hipLaunchKernelGGL((k1_elem<KD, 3>), grid, dim3(256), 0, st, K1E_ARGS);        \
+  else if (C == 1) hipLaunchKernelGGL((k1_elem<KD, 1>), grid, dim3(256), 0, st, K1E_ARGS);   \
+  else hipLaunchKernelGGL((k1_elem<KD, 0>), grid, dim3(256), 0, st, K1E_ARGS);
   if (kind == OP_BLUR) hipLaunchKernelGGL(k1_primal_pre<OP_BLUR>, grid, dim3(256), 0, st, K1_ARGS);
-  else if (kind == OP_MASK) hipLaunchKernelGGL(k1_primal_pre<OP_MASK>, grid, dim3(256), 0, st, K1_ARGS);
-  else hipLaunchKernelGGL(k1_primal_pre<OP_ID>, grid, dim3(256), 0, st, K1_ARGS);
+  else if (kind == OP_MASK) { K1E(OP_MASK) }
+  else { K1E(OP_ID) }
+#undef K1E
+#undef K1E_ARGS
 #undef K1_ARGS
 }
 
@@ -1101,9 +1276,23 @@ static void launch_k2_kind(int method, dim3 grid, hipStream_t st, const float* x
                            double gamma2, double gkl_gamma, double gkl_alpha, int record) {
 #define K2_ARGS xn, xo, y, xobs, xtrue, s, w, theta, partials, op, C, H, W, tiles_x, tiles, gamma2, gkl_gamma, \
                 gkl_alpha, record
-  if (method == M_A) hipLaunchKernelGGL((k2_dual<KIND, M_A>), grid, dim3(256), 0, st, K2_ARGS);
-  else if (method == M_B) hipLaunchKernelGGL((k2_dual<KIND, M_B>), grid, dim3(256), 0, st, K2_ARGS);
-  else hipLaunchKernelGGL((k2_dual<KIND, M_C>), grid, dim3(256), 0, st, K2_ARGS);
+#define K2E_ARGS xn, xo, y, xobs, xtrue, s, w, theta, partials, op.mask, C, H, W, tiles_x, tiles, gamma2, \
+                 1.0 / gamma2, gkl_gamma, gkl_alpha, record
+  if constexpr (KIND == OP_BLUR) {
+    if (method == M_A) hipLaunchKernelGGL((k2_dual<KIND, M_A>), grid, dim3(256), 0, st, K2_ARGS);
+    else if (method == M_B) hipLaunchKernelGGL((k2_dual<KIND, M_B>), grid, dim3(256), 0, st, K2_ARGS);
+    else hipLaunchKernelGGL((k2_dual<KIND, M_C>), grid, dim3(256), 0, st, K2_ARGS);
+  } else {
+#define K2E(M)                                                                                        \
+    if (C == 3) hipLaunchKernelGGL((k2_elem<KIND, M, 3>), grid, dim3(256), 0, st, K2E_ARGS);          \
+    else if (C == 1) hipLaunchKernelGGL((k2_elem<KIND, M, 1>), grid, dim3(256), 0, st, K2E_ARGS);     \
+    else hipLaunchKernelGGL((k2_elem<KIND, M, 0>), grid, dim3(256), 0, st, K2E_ARGS);
+    if (method == M_A) { K2E(M_A) }
+    else if (method == M_B) { K2E(M_B) }
+    else { K2E(M_C) }
+#undef K2E
+  }
+#undef K2E_ARGS
 #undef K2_ARGS
 }
 
