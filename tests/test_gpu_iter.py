@@ -92,3 +92,41 @@ def test_numpy_api_mirrors_reference(golden_ops):
     v, x0 = g["prox_v"], g["prox_x0"]
     np.testing.assert_allclose(ops.proj_l2_ball(x0 + v, 0.95, 0.01, 0.1, x0, 0.8), g["l2_0.01_0.95"], atol=2e-7)
     np.testing.assert_allclose(ops.proj_l1_ball(v, 0.95, 0.1, 0.8), g["l1_0.1"], atol=1e-6)
+
+
+@pytest.mark.parametrize("deg_op,method,C,H,W", [("Id", "A-Proposed", 3, 37, 53), ("random_sampling", "C-Proposed", 3, 30, 45),
+                                                 ("random_sampling", "B-Proposed", 1, 34, 41),
+                                                 ("blur", "B-Proposed", 3, 50, 70)])
+def test_ragged_shapes_vs_oracle(deg_op, method, C, H, W):
+    """Widths that are not multiples of 4 (the scalar edge paths of the pointwise K1/K2) or of
+    the 64-pixel blur tile, every operator, against the oracle on the same observation."""
+    from pnppds import operators as ops
+    from pnppds.iteration import test_iter
+    from pnppds.noise import make_observation
+    from pnppds.weights import resolve_weights
+    rng = np.random.default_rng(H * W)
+    yy, xx = np.meshgrid(np.linspace(0, 1, H), np.linspace(0, 1, W), indexing="ij")
+    xt = np.stack([0.5 + 0.3 * np.sin(5 * xx + c) * np.cos(3 * yy) for c in range(C)]).astype(np.float32)
+    xt = np.clip(xt + 0.02 * rng.standard_normal(xt.shape), 0, 1).astype(np.float32)
+    if C == 1:
+        xt = xt[0]
+    poisson = method == "C-Proposed"
+    sp = 0.1 if method == "B-Proposed" else 0.0
+    sig = 0.0 if poisson else 0.01
+    xobs, x0 = make_observation(xt, deg_op, "blur_1", 0.8, sig, sp, poisson, 300.0)
+    if method == "C-Proposed":
+        g1, g2 = 0.00035, 1 / 0.00035
+    elif method == "B-Proposed":
+        g1, g2 = 1.0, 0.49
+    else:
+        g1, g2 = 0.99, 0.99
+    arch = "DnCNN_nobn_nch_3_nlev_0.01" if C == 3 else "DnCNN_nobn_nch_1_nlev_0.01"
+    args = (g1, g2, 0.95, 0.95, 1.0, 15, 15, 0.1, sig, sp, 300.0)
+    phi, adj = ops.get_observation_operators(deg_op, "blur_1", 0.8)
+    x, s, c, psnr, _, _ = test_iter(x0, xobs, xt, phi, adj, *args, arch + ".pth", 4, method, C, 0.8)
+    p_ref, p_adj = O.observation_operators(deg_op, ops.load_blur_kernel("blur_1"), 0.8)
+    xo, so, co, po, _, _ = O.test_iter(np.asarray(x0, np.float64), np.asarray(xobs, np.float64), xt, p_ref, p_adj,
+                                       *args, O.OracleDenoiser(resolve_weights(arch, C)), 4, method, C, 0.8)
+    np.testing.assert_allclose(psnr, po, atol=0.01)
+    np.testing.assert_allclose(x, xo, atol=5e-3)
+    np.testing.assert_allclose(s, so, atol=5e-3)
