@@ -92,7 +92,7 @@ __device__ __forceinline__ int dma_count(int wave) {           // slots issued b
 // UNIFORM: every wave issues kSlots (the extra slots re-read pixel 339 into padding past
 // the halo), so the issue has no control flow and the compiler's own vmcnt accounting for
 // loads issued before it stays exact; the buffer must then hold NW * kSlots KiB.
-template <int NW, bool UNIFORM = false>
+template <int NW, bool UNIFORM = false, int SWZ = 0>
 struct RingDma {                                               // one wave's share of a halo DMA
   static constexpr int kSlots = (kDmaSlots + NW - 1) / NW;     // NW=8: 6 (waves >= 3: 5); NW=4: 11 (wave 3: 10)
   unsigned off[kSlots];
@@ -103,7 +103,7 @@ struct RingDma {                                               // one wave's sha
       const int p = 8 * (NW * j + wave) + (lane >> 3);
       const int pl = min(p, kHaloPix - 1);
       const int pr = pl / kHaloW, pc = pl - pr * kHaloW;
-      const int c = (lane & 7) ^ ((pc >> 1) & 7);
+      const int c = (lane & 7) ^ (SWZ ? (pc & 6) : ((pc >> 1) & 7));
       off[j] = (unsigned)(((pr * s.Wp + pc) * kWidth + c * 8) * 2);
     }
   }
@@ -139,9 +139,9 @@ struct RingDma {                                               // one wave's sha
 // LDS: 3 x 42.5 KiB halo + 8 x 4 KiB staging + bias = 163584 B.
 // (Round-1 alternatives measured slower and removed: weights in LDS with 4 or 8 waves,
 // warp-specialised DMA waves, one wave per SIMD holding the whole layer, a channel-plane
-// halo, v_mfma_f32_16x16x32_f16 with 32 channels per wave (1.98 ms: twice the B-fragment
-// LDS reads per FLOP), the head computed into the first layer's LDS halo instead of HBM
-// (1.82 ms vs 0.51 + 1.22 ms: the head phase serialises behind the K-loop); DESIGN.md.)
+// halo, the head computed into the first layer's LDS halo (1.82 ms vs 0.51 + 1.22 ms),
+// DMA slots spread over the K-loop, full 128-B line stores through a shared staging tile,
+// non-temporal stores; the 16x16x32 form is kept below as variant 3; DESIGN.md.)
 // ------------------------------------------------------------------------------------
 constexpr int kV3Stage = 3 * kV3Halo;
 constexpr int kV3Bias = kV3Stage + 8 * 4096;
@@ -302,6 +302,171 @@ PNP_V3_INST(3, 0)
 PNP_V3_INST(4, 0)
 PNP_V3_INST(6, 0)
 #undef PNP_V3_INST
+
+// ------------------------------------------------------------------------------------
+// Body layer on v_mfma_f32_16x16x32_f16 (PNP_TUNE_BODY_VARIANT 3).  Same tile, 3-deep
+// LDS-DMA ring and resident weights as conv_body_v3; the 16x16x32 form issues in half the
+// cycles of 32x32x16 for half the FLOPs and the chip holds a higher clock on it
+// (MI355X_MICROARCH.md, DVFS give-back item 7).  Wave w owns channels 32m..32m+31 (m = w&1)
+// as two 16-row M-tiles and its two tile rows as four 16-pixel N-tiles; one K-step is one
+// tap x 32 input channels (18 steps, 8 MFMAs each, 4 activation fragments from LDS): the
+// same LDS bytes per MFMA FLOP as v3.
+// Planar halo: 16-B chunk c (channels 8c..8c+7) of halo pixel p at c * 5632 + 16 p (planes
+// of 352 pixels, a multiple of 16, so the q = 0..3 lane groups of a ds_read_b128 over 16
+// consecutive pixels hit 16 distinct bank slots).  Every B-fragment address is then ONE
+// per-lane register (16 col + 5632 q) plus an immediate: no per-tap address registers, no
+// spills - a spilled register reloaded inside the K-loop waits on vmcnt(0), i.e. on the
+// in-flight halo DMA, and serialises the ring.
+// A row R of M-tile i is channel 8(R>>2) + 4i + (R&3) of the wave's 32, so lane group
+// q = lane>>4 owns channels 8q..8q+7 of its pixel: the epilogue stores 16 B per lane and
+// N-tile straight from registers (16 pixels x 64 B per instruction), no staging.
+// LDS: 3 x 45056 B halo + bias = 135424 B.
+// Measured (B = 256): 1.28 ms vs 1.21-1.24 for conv_body_v3; PMC at B = 64: clock 1.78 vs
+// 1.60 GHz, MFMA busy 48 vs 56 %.  The planar halo took it from 1.94 ms (14 spilled address
+// registers reloaded inside the K-loop).  Not kept: B double-buffered (same), stores
+// deferred into the next K-loop from registers (1.36 ms), one wave per SIMD holding all
+// 64 channels (4 MFMAs per B fragment, 450 registers: 1.45 ms).
+// ------------------------------------------------------------------------------------
+constexpr int kBody16KSteps = 18;
+constexpr int kPlanePix = 352;                                  // >= 340, multiple of 16
+constexpr int kPlaneBytes = kPlanePix * 16;                     // 5632
+constexpr int kV5Halo = 8 * kPlaneBytes;                        // 45056
+constexpr int kV5Slots = kV5Halo / 1024;                        // 44 DMA pieces of 64 x 16 B
+constexpr int kV5Bias = 3 * kV5Halo;
+constexpr int kV5Lds = kV5Bias + 256;                           // 135424
+
+template <int ACT>
+__global__ __launch_bounds__(512, 2) void conv_body_v4_kernel(const half_t* __restrict__ in,
+                                                               half_t* __restrict__ out,
+                                                               const uint4* __restrict__ wpk,
+                                                               const float* __restrict__ bias,
+                                                               ConvShape s) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float* bias_l = reinterpret_cast<float*>(smem + kV5Bias);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int m = wave & 1, rp = wave >> 1;    // channel half, row pair
+  const int q = lane >> 4, col = lane & 15;
+  if (tid < kWidth) bias_l[tid] = bias[tid];
+
+  half8_t wA[kBody16KSteps][2];               // [k-step][M-tile], resident for the launch
+#pragma unroll
+  for (int ks = 0; ks < kBody16KSteps; ++ks)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      wA[ks][i] = *reinterpret_cast<const half8_t*>(reinterpret_cast<const unsigned char*>(wpk) +
+                                                    (((ks * 2 + m) * 2 + i) * 64 + lane) * 16);
+
+  // DMA: piece g (64 lanes x 16 B) of the planar image; wave w issues g = w, w + 8, ...
+  constexpr int kSlotsPerWave = (kV5Slots + 7) / 8;             // 6 (waves >= 4: 5)
+  const int ndma = (kV5Slots - wave + 7) / 8;
+  unsigned doff[kSlotsPerWave];
+#pragma unroll
+  for (int j = 0; j < kSlotsPerWave; ++j) {
+    const int k = 64 * (8 * j + wave) + lane;                   // 16-B unit of the planar image
+    const int c = k / kPlanePix, p = min(k - c * kPlanePix, kHaloPix - 1);
+    const int pr = p / kHaloW, pc = p - pr * kHaloW;
+    doff[j] = (unsigned)(((pr * s.Wp + pc) * kWidth + 8 * min(c, 7)) * 2);
+  }
+  auto buf = [&](int i) { return smem + i * kV5Halo; };
+  auto issue_dma = [&](int tt, int bi) {
+    int b, ty0, tx0;
+    decode_tile(tt < s.tiles ? tt : s.tiles - 1, s, b, ty0, tx0);
+    const half_t* base = in + (((size_t)b * s.Hp + ty0 + s.pad - 1) * s.Wp + tx0 + s.pad - 1) * kWidth;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, 0x7fffffff, 0x00020000);
+#pragma unroll
+    for (int j = 0; j < kSlotsPerWave; ++j)
+      if (j < ndma)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(buf(bi) + (8 * j + wave) * 1024),
+                                                 16, doff[j], 0, 0, 0);
+  };
+
+  int t = blockIdx.x;
+  if (t < s.tiles) {
+    issue_dma(t, 0);
+    issue_dma(t + gridDim.x, 1);
+    if (ndma == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");   // tile t landed
+    else asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+  }
+  __syncthreads();
+  const int lane_off = q * kPlaneBytes + col * 16 + rp * 2 * kHaloW * 16;
+  floatx4 acc[4][2];
+  int cur = 0;
+  for (; t < s.tiles; t += gridDim.x) {
+    int b, ty0, tx0;
+    decode_tile(t, s, b, ty0, tx0);
+    const int nxt2 = cur >= 1 ? cur - 1 : 2;  // (cur + 2) % 3
+    issue_dma(t + 2 * gridDim.x, nxt2);
+    const unsigned char* hl = buf(cur) + lane_off;
+    auto ldB = [&](int ks, int n) {           // everything but lane_off is an immediate
+      const int tap = ks >> 1, sub = ks & 1;
+      const int pr = (n >> 1) + tap / 3, pc = 16 * (n & 1) + tap % 3;
+      return *reinterpret_cast<const half8_t*>(hl + 4 * sub * kPlaneBytes + (pr * kHaloW + pc) * 16);
+    };
+#pragma unroll
+    for (int n = 0; n < 4; ++n) acc[n][0] = acc[n][1] = floatx4{};
+    // rolling ring: fragment n of step ks+1 is read right after the two MFMAs of step ks
+    // that use fragment n (sched barriers pin the order, so it reuses n's registers)
+    half8_t fb[4];
+#pragma unroll
+    for (int n = 0; n < 4; ++n) fb[n] = ldB(0, n);
+#pragma unroll
+    for (int ks = 0; ks < kBody16KSteps; ++ks) {
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        acc[n][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wA[ks][0], fb[n], acc[n][0], 0, 0, 0);
+        acc[n][1] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wA[ks][1], fb[n], acc[n][1], 0, 0, 0);
+        if (ks + 1 < kBody16KSteps) {
+          __builtin_amdgcn_sched_barrier(0);
+          fb[n] = ldB(ks + 1, n);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    }
+    {                                          // bias + activation -> fp16 -> 16 B per lane and N-tile
+      const float* bl = bias_l + 32 * m + 8 * q;
+      const int ncols = min(kTileW, s.W - tx0);
+#pragma unroll
+      for (int rr = 0; rr < 2; ++rr) {
+        const int y = ty0 + 2 * rp + rr;
+        half_t* row = out + (((size_t)b * s.Hp + y + s.pad) * s.Wp + tx0 + s.pad) * kWidth;
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc(row, (short)0, y < s.H ? ncols * 128 : 0, 0x00020000);
+#pragma unroll
+        for (int nh = 0; nh < 2; ++nh) {
+          const int n = 2 * rr + nh;
+          half8_t o;
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int r2 = 0; r2 < 4; r2 += 2) {
+              f2v_t v = f2v_t{acc[n][i][r2], acc[n][i][r2 + 1]} + f2v_t{bl[4 * i + r2], bl[4 * i + r2 + 1]};
+              if (ACT == 0) {
+                const f2v_t tt = v * 0.01f;
+                v = f2v_t{fmaxf(v.x, tt.x), fmaxf(v.y, tt.y)};
+              } else {
+                v = f2v_t{fmaxf(v.x, 0.f), fmaxf(v.y, 0.f)};
+              }
+              o[4 * i + r2] = (half_t)v.x;
+              o[4 * i + r2 + 1] = (half_t)v.y;
+            }
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i_t, o), rs,
+                                                 (16 * nh + col) * 128 + 64 * m + 16 * q, 0, 0);
+        }
+      }
+    }
+    // tile t+1 landed: only the DMA of t+2 (ndma ops) and this tile's 4 stores are younger
+    if (ndma == 6) asm volatile("s_waitcnt vmcnt(10) lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(9) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    cur = cur == 2 ? 0 : cur + 1;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA may land after the workgroup ends
+}
+template __global__ void conv_body_v4_kernel<0>(const half_t* __restrict__, half_t* __restrict__,
+                                                const uint4* __restrict__, const float* __restrict__, ConvShape);
+template __global__ void conv_body_v4_kernel<1>(const half_t* __restrict__, half_t* __restrict__,
+                                                const uint4* __restrict__, const float* __restrict__, ConvShape);
 
 // ------------------------------------------------------------------------------------
 // Two body layers per launch (l+1 and l+2 of basic_models.py:29-33): the intermediate
@@ -801,6 +966,23 @@ void pack_head_weights(const float* W, int C, uint16_t* out) {
         }
 }
 
+// conv_body_v4 (16x16x32): [ks 18][m 2][i 2][lane 64][8 x f16]; k-step ks = tap ks/2, input
+// channels 32(ks&1) + 8(l>>4) + j; A row R = l&15 of M-tile i = channel 32m + 8(R>>2) + 4i + (R&3).
+void pack_body_weights16(const float* W, uint16_t* out) {
+  for (int ks = 0; ks < kBody16KSteps; ++ks) {
+    const int tap = ks / 2, sub = ks % 2, ky = tap / 3, kx = tap % 3;
+    for (int m = 0; m < 2; ++m)
+      for (int i = 0; i < 2; ++i)
+        for (int l = 0; l < 64; ++l)
+          for (int j = 0; j < 8; ++j) {
+            const int R = l & 15;
+            const int co = 32 * m + 8 * (R >> 2) + 4 * i + (R & 3);
+            const int ci = 32 * sub + 8 * (l >> 4) + j;
+            out[((((ks * 2 + m) * 2 + i) * 64 + l) * 8) + j] = f32_to_f16_bits(W[((co * 64 + ci) * 3 + ky) * 3 + kx]);
+          }
+  }
+}
+
 // W: [C][64][3][3].  16x16x32: lane l holds A[row l&15][k = 8(l>>4)+j]; k-step ks covers
 // tap ks/2, input channels 32*(ks&1) .. +31.
 void pack_tail_weights(const float* W, int C, uint16_t* out) {
@@ -842,6 +1024,10 @@ hipError_t conv_kernels_init() {
     e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kV3Lds);
     if (e != hipSuccess) return e;
   }
+  for (const void* k : {(const void*)conv_body_v4_kernel<0>, (const void*)conv_body_v4_kernel<1>}) {
+    e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kV5Lds);
+    if (e != hipSuccess) return e;
+  }
   for (const void* k : {(const void*)conv_body2_kernel<0>, (const void*)conv_body2_kernel<1>}) {
     e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kB2Lds);
     if (e != hipSuccess) return e;
@@ -880,6 +1066,15 @@ void launch_conv_body(const half_t* in, half_t* out, const void* w, const float*
     default: V3(0, 0);
   }
 #undef V3
+}
+
+void launch_conv_body16(const half_t* in, half_t* out, const void* w16, const float* bias, const ConvShape& s,
+                        int act, int num_cus, hipStream_t st) {
+  const int grid = s.tiles < num_cus ? s.tiles : num_cus;
+  if (act == 0)
+    hipLaunchKernelGGL((conv_body_v4_kernel<0>), dim3(grid), dim3(512), kV5Lds, st, in, out, (const uint4*)w16, bias, s);
+  else
+    hipLaunchKernelGGL((conv_body_v4_kernel<1>), dim3(grid), dim3(512), kV5Lds, st, in, out, (const uint4*)w16, bias, s);
 }
 
 void launch_conv_body2(const half_t* in, half_t* out, const void* w1, const float* b1, const void* w2,

@@ -16,6 +16,7 @@ struct ConvShape {
 ConvShape make_conv_shape(int B, int H, int W);
 hipError_t conv_kernels_init();
 void pack_body_weights(const float* W, uint16_t* out);
+void pack_body_weights16(const float* W, uint16_t* out);   // conv_body_v4 (16x16x32) order, same size
 void pack_head_weights(const float* W, int C, uint16_t* out);
 void pack_tail_weights(const float* W, int C, uint16_t* out);
 void launch_conv_head(const half_t* in4, half_t* out, const void* w, const float* bias, const ConvShape& s,
@@ -23,6 +24,9 @@ void launch_conv_head(const half_t* in4, half_t* out, const void* w, const float
 // one 64 -> 64 layer (variant kept for the tuning ABI; one kernel)
 void launch_conv_body(const half_t* in, half_t* out, const void* w, const float* bias, const ConvShape& s,
                       int act, int num_cus, int variant, hipStream_t st);
+// one 64 -> 64 layer on 16x16x32 MFMAs (weights packed by pack_body_weights16)
+void launch_conv_body16(const half_t* in, half_t* out, const void* w16, const float* bias, const ConvShape& s,
+                        int act, int num_cus, hipStream_t st);
 // two 64 -> 64 layers in one launch (the intermediate stays in LDS); in needs pad >= 2
 void launch_conv_body2(const half_t* in, half_t* out, const void* w1, const float* b1, const void* w2,
                        const float* b2, const ConvShape& s, int act, int num_cus, hipStream_t st);

@@ -191,7 +191,8 @@ class Context:
 
     def set_body_variant(self, variant: int):
         """Body layers per launch: 0 = one (default), 1 = two fused layers, 2 = one with the
-        staggered epilogue.  Performance only (bit-identical results)."""
+        staggered epilogue, 3 = one on 16x16x32 MFMAs (not bit-identical: another summation
+        order).  Performance only."""
         self._check(self.lib.pnp_set_tuning(self.h, TUNE_BODY_VARIANT, int(variant)))
 
     def set_operator(self, kind: int, h=None, mask=None, key=None):

@@ -75,6 +75,30 @@ def test_body_variants_bit_identical(gpu_ctx, name, B, C, H, W):
         np.testing.assert_array_equal(outs[0], o)
 
 
+@pytest.mark.parametrize("variant", [3])
+@pytest.mark.parametrize("name,B,C,H,W", [("DnCNN_nobn_nch_3_nlev_0.01", 3, 3, 50, 70),
+                                          ("DnCNN_nobn_nch_3_nlev_0.01", 2, 3, 256, 256),
+                                          ("dncnn_15", 2, 1, 37, 45)])
+def test_body_variant_mfma16(gpu_ctx, variant, name, B, C, H, W):
+    """Variant 3 (16x16x32 MFMAs, planar halo) sums each output's 576 products in another
+    order than the 32x32x16 kernels, so it matches the fp16-emulating oracle to the same
+    tolerance rather than variant 0 bit for bit."""
+    rng = np.random.default_rng(12)
+    w = DenoiserWeights.load_npz(os.path.join(WEIGHTS_DIR, name + ".npz"))
+    x = rng.uniform(0, 1, (B, C, H, W)).astype(np.float32)
+    gpu_ctx.set_body_variant(variant)
+    try:
+        out = run_denoise(gpu_ctx, w, x)
+        one = run_denoise(gpu_ctx, w, x[B - 1:B])
+    finally:
+        gpu_ctx.set_body_variant(0)
+    emu = O.OracleDenoiser(w, emulate_fp16=True).forward_batch(x[:1])
+    np.testing.assert_allclose(out[:1], emu, atol=TOL_VS_FP16_EMU)
+    base = run_denoise(gpu_ctx, w, x)
+    assert np.abs(out - base).max() <= TOL_VS_FP16_EMU
+    np.testing.assert_array_equal(one[0], out[B - 1])        # images independent: same bits alone
+
+
 def test_denoiser_full_size_rgb(gpu_ctx):
     """256x256 RGB, real weights, batch 2 — the metric's image shape."""
     w = DenoiserWeights.load_npz(os.path.join(WEIGHTS_DIR, "DnCNN_nobn_nch_3_nlev_0.01.npz"))
