@@ -122,7 +122,9 @@ enum pnp_tuning_key {
   PNP_TUNE_DENOISE_CHUNK = 1,
   PNP_TUNE_BODY_VARIANT = 2,  /* 64->64 body layers: 1 = two layers per launch, the intermediate
                                  kept in LDS; 0 = one layer per launch (default); 2 = one
-                                 layer, staggered epilogue; 3 = one layer on 16x16x32 MFMAs */
+                                 layer, staggered epilogue; 3 = one layer on 16x16x32 MFMAs;
+                                 4 = one layer as a row-wise Winograd F(2,3) (3 and 4 round
+                                 differently, within the fp16 tolerance) */
   PNP_TUNE_ABLATE = 3         /* profiling only, results are wrong: one-layer body kernel with parts
                                  skipped (1 = halo DMA, 2 = output stores, 4 = MFMA K-loop) */
 };

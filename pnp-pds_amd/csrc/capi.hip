@@ -51,9 +51,10 @@ struct pnp_ctx {
   int body_fused = 0;     // 1: body layers two per launch (conv_body2), 0: one per launch (conv_body_v3)
   int body_stagger = 0;   // PNP_TUNE_BODY_VARIANT 2: staggered epilogue in conv_body_v3
   int body_mf16 = 0;      // PNP_TUNE_BODY_VARIANT 3: conv_body_v4 (16x16x32 MFMAs)
+  int body_wg = 0;        // PNP_TUNE_BODY_VARIANT 4: conv_body_wg (row Winograd F(2,3))
   int ablate = 0;         // profiling only (PNP_TUNE_ABLATE): parts of conv_body_v3 skipped, results wrong
   bool den_ready = false;
-  DevBuf head_w, head_b, body_w, body_w16, body_b, tail_w, tail_b;
+  DevBuf head_w, head_b, body_w, body_w16, body_wwg, body_b, tail_w, tail_b;
 
   // operator
   int op_kind = PNP_OP_ID;
@@ -277,6 +278,12 @@ void run_denoiser(pnp_ctx* ctx, const half_t* u16, const float* u32, float* xout
                           ctx->den_act, ctx->num_cus, st);
         check_launch(ctx, "conv_body2");
         l += 2;
+      } else if (ctx->body_wg && !ctx->ablate) {
+        ProfScope ps(ctx, "conv_body", st);
+        launch_conv_body_wg(P<half_t>(act[cur]), P<half_t>(act[cur ^ 1]),
+                            (const char*)ctx->body_wwg.p + (size_t)l * kBodyWgBytes, bl, s, ctx->den_act, ctx->num_cus, st);
+        check_launch(ctx, "conv_body");
+        l += 1;
       } else if (ctx->body_mf16 && !ctx->ablate) {
         ProfScope ps(ctx, "conv_body", st);
         launch_conv_body16(P<half_t>(act[cur]), P<half_t>(act[cur ^ 1]),
@@ -719,7 +726,7 @@ int pnp_destroy(pnp_ctx* ctx) {
   if (!ctx) return PNP_OK;
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-  DevBuf* bufs[] = {&ctx->head_w, &ctx->head_b, &ctx->body_w, &ctx->body_w16, &ctx->body_b, &ctx->tail_w, &ctx->tail_b,
+  DevBuf* bufs[] = {&ctx->head_w, &ctx->head_b, &ctx->body_w, &ctx->body_w16, &ctx->body_wwg, &ctx->body_b, &ctx->tail_w, &ctx->tail_b,
                     &ctx->taps_fwd, &ctx->taps_adj, &ctx->mask, &ctx->x[0], &ctx->x[1], &ctx->y, &ctx->s,
                     &ctx->w, &ctx->xobs, &ctx->xtrue, &ctx->u32, &ctx->u16, &ctx->act[0], &ctx->act[1],
                     &ctx->partials, &ctx->metrics, &ctx->theta, &ctx->scr_u32, &ctx->scr_u16,
@@ -750,11 +757,14 @@ int pnp_set_tuning(pnp_ctx* ctx, int key, int value) {
       return;
     }
     if (key == PNP_TUNE_BODY_VARIANT) {
-      if (value < 0 || value > 3)
-        fail(ctx, PNP_E_ARG, "body variant must be 0 (one layer/launch), 1 (two), 2 (one, staggered) or 3 (one, 16x16x32)");
+      if (value < 0 || value > 4)
+        fail(ctx, PNP_E_ARG,
+             "body variant must be 0 (one layer/launch), 1 (two), 2 (one, staggered), 3 (one, 16x16x32) or 4 (one, "
+             "row Winograd F(2,3))");
       ctx->body_fused = value == 1;
       ctx->body_stagger = value == 2;
       ctx->body_mf16 = value == 3;
+      ctx->body_wg = value == 4;
       return;
     }
     if (key == PNP_TUNE_ABLATE) {          // profiling only
@@ -789,7 +799,7 @@ int pnp_set_denoiser(pnp_ctx* ctx, int channels, int depth, int width, const flo
       fail(ctx, PNP_E_ARG, "expected %zu parameters for C=%d depth=%d, got %zu", expect, channels, depth, n_params);
     const float* p = params;
     std::vector<uint16_t> hw(kHeadWBytes / 2), bw((size_t)(depth - 2) * kBodyWBytes / 2), tw(kTailWBytes / 2);
-    std::vector<uint16_t> bw16(bw.size());
+    std::vector<uint16_t> bw16(bw.size()), bwg((size_t)(depth - 2) * kBodyWgBytes / 2);
     std::vector<float> hb(kWidth), bb((size_t)(depth - 2) * kWidth), tb(kMaxC, 0.f);
     pack_head_weights(p, channels, hw.data());
     std::memcpy(hb.data(), p + kWidth * channels * 9, kWidth * sizeof(float));
@@ -797,6 +807,7 @@ int pnp_set_denoiser(pnp_ctx* ctx, int channels, int depth, int width, const flo
     for (int l = 0; l < depth - 2; ++l) {
       pack_body_weights(p, bw.data() + (size_t)l * kBodyWBytes / 2);
       pack_body_weights16(p, bw16.data() + (size_t)l * kBodyWBytes / 2);
+      pack_body_weights_wg(p, bwg.data() + (size_t)l * kBodyWgBytes / 2);
       std::memcpy(bb.data() + (size_t)l * kWidth, p + kWidth * kWidth * 9, kWidth * sizeof(float));
       p += n_body;
     }
@@ -806,6 +817,7 @@ int pnp_set_denoiser(pnp_ctx* ctx, int channels, int depth, int width, const flo
     ensure(ctx, ctx->head_b, hb.size() * 4);
     ensure(ctx, ctx->body_w, bw.size() * 2);
     ensure(ctx, ctx->body_w16, bw16.size() * 2);
+    ensure(ctx, ctx->body_wwg, bwg.size() * 2);
     ensure(ctx, ctx->body_b, bb.size() * 4);
     ensure(ctx, ctx->tail_w, tw.size() * 2);
     ensure(ctx, ctx->tail_b, tb.size() * 4);
@@ -813,6 +825,7 @@ int pnp_set_denoiser(pnp_ctx* ctx, int channels, int depth, int width, const flo
     HIPCHK(ctx, hipMemcpy(ctx->head_b.p, hb.data(), hb.size() * 4, hipMemcpyHostToDevice));
     HIPCHK(ctx, hipMemcpy(ctx->body_w.p, bw.data(), bw.size() * 2, hipMemcpyHostToDevice));
     HIPCHK(ctx, hipMemcpy(ctx->body_w16.p, bw16.data(), bw16.size() * 2, hipMemcpyHostToDevice));
+    HIPCHK(ctx, hipMemcpy(ctx->body_wwg.p, bwg.data(), bwg.size() * 2, hipMemcpyHostToDevice));
     HIPCHK(ctx, hipMemcpy(ctx->body_b.p, bb.data(), bb.size() * 4, hipMemcpyHostToDevice));
     HIPCHK(ctx, hipMemcpy(ctx->tail_w.p, tw.data(), tw.size() * 2, hipMemcpyHostToDevice));
     HIPCHK(ctx, hipMemcpy(ctx->tail_b.p, tb.data(), tb.size() * 4, hipMemcpyHostToDevice));

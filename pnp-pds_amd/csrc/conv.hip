@@ -73,6 +73,7 @@ __device__ __forceinline__ half8_t bias_act8(const floatx16& a, int off, const f
 }
 
 typedef int v4i_t __attribute__((ext_vector_type(4)));
+typedef int v2i_t __attribute__((ext_vector_type(2)));
 
 // ------------------------------------------------------------------------------------
 // LDS-DMA halo staging (buffer_load_dword... lds).  The 10 x 34 halo of an 8 x 32 tile
@@ -467,6 +468,180 @@ template __global__ void conv_body_v4_kernel<0>(const half_t* __restrict__, half
                                                 const uint4* __restrict__, const float* __restrict__, ConvShape);
 template __global__ void conv_body_v4_kernel<1>(const half_t* __restrict__, half_t* __restrict__,
                                                 const uint4* __restrict__, const float* __restrict__, ConvShape);
+
+// ------------------------------------------------------------------------------------
+// Body layer as a row-wise Winograd F(2,3) (PNP_TUNE_BODY_VARIANT 4).  Along x, each pair of
+// output pixels (2n, 2n+1) of a row is
+//   y0 = M0 + M1 + M2,  y1 = M1 - M2 - M3,   M_j = sum_{a, ci} U[a][j] . d'_j(row + a)
+// with the input transform d' = (d0 - d2, d1 + d2, d2 - d1, d1 - d3) of halo columns
+// 2n .. 2n+3 and the weight transform U = (g0, (g0+g1+g2)/2, (g0-g1+g2)/2, g2) of each
+// kernel row (pack_body_weights_wg, fp64 -> fp16).  12 MFMA taps per output pair instead of
+// 18: two thirds of the MFMA work of conv_body_v3.  Same tile, 3-deep LDS-DMA ring and
+// resident weights as conv_body_v4 (planar halo); wave w owns output channels 16(w&3) ..
+// +15 (one 16x16x32 M-tile, all 12 (a, j) x 2 K-halves = 96 VGPRs) of tile rows
+// 4(w>>2) .. +3, as 16 x 4 accumulators (one 16-pixel-pair N-tile per row and j).  Each
+// halo row of its 6 is read once per K-half (4 x ds_read_b128 for d0..d3), transformed
+// with 16 packed fp16 adds, and feeds the 1-3 output rows that use it.
+// Planar halo with an ODD plane stride (341 pixels): lane group q = lane>>4 reads chunk
+// 4ks+q of pixels 2n+c, so the two chunks of one ds_read_b128 lane group land on opposite
+// bank-slot parities and the 16 lanes hit 16 distinct slots.
+// Numerics: the fp16 rounding of d' and U replaces that of d and g; fp32 accumulation and
+// output transform.  Not bit-identical to variants 0-3 (tested against the oracle within
+// the fp16 tolerance).
+// LDS: 3 x 44032 B halo + bias = 132352 B.
+// Measured (B = 256): 1.37-1.40 ms vs 1.23-1.29 ms for conv_body_v3.  PMC at B = 64: 2/3 of
+// v3's MFMA cycles but 2x its vector instructions (192 packed transform adds + the output
+// transform per wave and tile), MFMA busy 27 vs 55 %, 45 % of wave cycles stalled on issue.
+// A forced 1 MFMA : 2 VALU : 1/2 LDS interleave (sched_group_barrier) changed nothing.
+// ------------------------------------------------------------------------------------
+// a - b on 8 fp16 as 4 v_pk_add_f16 with the second operand negated (the compiler splits a
+// vector fsub into per-half v_sub_f16 + repack: 3 instructions per pair instead of 1)
+__device__ __forceinline__ half8_t pk_sub8(const half8_t& a, const half8_t& b) {
+  const v4i_t ai = __builtin_bit_cast(v4i_t, a), bi = __builtin_bit_cast(v4i_t, b);
+  v4i_t r;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    asm("v_pk_add_f16 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1]" : "=v"(r[i]) : "v"(ai[i]), "v"(bi[i]));
+  return __builtin_bit_cast(half8_t, r);
+}
+
+constexpr int kWgPlanePix = 341;                               // odd, >= 340
+constexpr int kWgPlaneBytes = kWgPlanePix * 16;                // 5456
+constexpr int kWgPieces = (8 * kWgPlanePix + 63) / 64;         // 43 DMA pieces of 64 x 16 B
+constexpr int kWgHalo = kWgPieces * 1024;                      // 44032
+constexpr int kWgBias = 3 * kWgHalo;
+constexpr int kWgLds = kWgBias + 256;                          // 132352
+
+template <int ACT>
+__global__ __launch_bounds__(512, 2) void conv_body_wg_kernel(const half_t* __restrict__ in,
+                                                               half_t* __restrict__ out,
+                                                               const uint4* __restrict__ wpk,
+                                                               const float* __restrict__ bias,
+                                                               ConvShape s) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float* bias_l = reinterpret_cast<float*>(smem + kWgBias);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int mt = wave & 3, rq = wave >> 2;   // M-tile (16 channels), row quad
+  const int q = lane >> 4, n = lane & 15;
+  if (tid < kWidth) bias_l[tid] = bias[tid];
+
+  half8_t wU[3][4][2];                        // [kernel row a][j][K-half], resident for the launch
+#pragma unroll
+  for (int a = 0; a < 3; ++a)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        wU[a][j][ks] = *reinterpret_cast<const half8_t*>(reinterpret_cast<const unsigned char*>(wpk) +
+                                                         (((((a * 4 + j) * 2 + ks) * 4 + mt) * 64 + lane) * 16));
+
+  // DMA: piece g (64 lanes x 16 B) of the planar image; wave w issues g = w, w + 8, ...
+  constexpr int kSlotsPerWave = (kWgPieces + 7) / 8;            // 6 (waves >= 3: 5)
+  const int ndma = (kWgPieces - wave + 7) / 8;
+  unsigned doff[kSlotsPerWave];
+#pragma unroll
+  for (int j = 0; j < kSlotsPerWave; ++j) {
+    const int k = 64 * (8 * j + wave) + lane;                   // 16-B unit of the planar image
+    const int c = k / kWgPlanePix, p = min(k - c * kWgPlanePix, kHaloPix - 1);
+    const int pr = p / kHaloW, pc = p - pr * kHaloW;
+    doff[j] = (unsigned)(((pr * s.Wp + pc) * kWidth + 8 * min(c, 7)) * 2);
+  }
+  auto buf = [&](int i) { return smem + i * kWgHalo; };
+  auto issue_dma = [&](int tt, int bi) {
+    int b, ty0, tx0;
+    decode_tile(tt < s.tiles ? tt : s.tiles - 1, s, b, ty0, tx0);
+    const half_t* base = in + (((size_t)b * s.Hp + ty0 + s.pad - 1) * s.Wp + tx0 + s.pad - 1) * kWidth;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, 0x7fffffff, 0x00020000);
+#pragma unroll
+    for (int j = 0; j < kSlotsPerWave; ++j)
+      if (j < ndma)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(buf(bi) + (8 * j + wave) * 1024),
+                                                 16, doff[j], 0, 0, 0);
+  };
+
+  int t = blockIdx.x;
+  if (t < s.tiles) {
+    issue_dma(t, 0);
+    issue_dma(t + gridDim.x, 1);
+    if (ndma == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");   // tile t landed
+    else asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+  }
+  __syncthreads();
+  const int lane_off = q * kWgPlaneBytes + 2 * n * 16 + 4 * rq * kHaloW * 16;
+  int cur = 0;
+  for (; t < s.tiles; t += gridDim.x) {
+    int b, ty0, tx0;
+    decode_tile(t, s, b, ty0, tx0);
+    const int nxt2 = cur >= 1 ? cur - 1 : 2;  // (cur + 2) % 3
+    issue_dma(t + 2 * gridDim.x, nxt2);
+    const unsigned char* hl = buf(cur) + lane_off;
+    auto ldD = [&](int ks, int R, int c) {    // everything but lane_off is an immediate
+      return *reinterpret_cast<const half8_t*>(hl + 4 * ks * kWgPlaneBytes + (R * kHaloW + c) * 16);
+    };
+    floatx4 acc[4][4];                        // [output row][j]
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[r][j] = floatx4{};
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int R = 0; R < 6; ++R) {
+        const half8_t d0 = ldD(ks, R, 0), d1 = ldD(ks, R, 1), d2 = ldD(ks, R, 2), d3 = ldD(ks, R, 3);
+        half8_t B[4];
+        B[0] = pk_sub8(d0, d2);
+        B[1] = d1 + d2;
+        B[2] = pk_sub8(d2, d1);
+        B[3] = pk_sub8(d1, d3);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int a = R - r;
+          if (a < 0 || a > 2) continue;
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[r][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wU[a][j][ks], B[j], acc[r][j], 0, 0, 0);
+        }
+      }
+    {                                          // output transform + bias + activation -> 8 B per lane and pixel
+      const float* bl = bias_l + 16 * mt + 4 * q;
+      const float bv[4] = {bl[0], bl[1], bl[2], bl[3]};
+      const int ncols = min(kTileW, s.W - tx0);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int y = ty0 + 4 * rq + r;
+        half_t* row = out + (((size_t)b * s.Hp + y + s.pad) * s.Wp + tx0 + s.pad) * kWidth;
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc(row, (short)0, y < s.H ? ncols * 128 : 0, 0x00020000);
+#pragma unroll
+        for (int v = 0; v < 2; ++v) {
+          half4_t o;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            float z = v == 0 ? (acc[r][0][i] + acc[r][1][i]) + acc[r][2][i]
+                             : (acc[r][1][i] - acc[r][2][i]) - acc[r][3][i];
+            z += bv[i];
+            z = ACT == 0 ? fmaxf(z, 0.01f * z) : fmaxf(z, 0.f);
+            o[i] = (half_t)z;
+          }
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2i_t, o), rs,
+                                                (2 * n + v) * 128 + (16 * mt + 4 * q) * 2, 0, 0);
+        }
+      }
+    }
+    // tile t+1 landed: only the DMA of t+2 (ndma ops) and this tile's 8 stores are younger
+    if (ndma == 6) asm volatile("s_waitcnt vmcnt(14) lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(13) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    cur = cur == 2 ? 0 : cur + 1;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA may land after the workgroup ends
+}
+template __global__ void conv_body_wg_kernel<0>(const half_t* __restrict__, half_t* __restrict__,
+                                                const uint4* __restrict__, const float* __restrict__, ConvShape);
+template __global__ void conv_body_wg_kernel<1>(const half_t* __restrict__, half_t* __restrict__,
+                                                const uint4* __restrict__, const float* __restrict__, ConvShape);
+
 
 // ------------------------------------------------------------------------------------
 // Two body layers per launch (l+1 and l+2 of basic_models.py:29-33): the intermediate
@@ -983,6 +1158,24 @@ void pack_body_weights16(const float* W, uint16_t* out) {
   }
 }
 
+// conv_body_wg order: [kernel row a][j][K-half ks][M-tile mt][lane][8 x f16], lane l holding
+// U_j[a] of output channel 16mt + (l&15), input channels 32ks + 8(l>>4) .. +7, where
+// U = (g0, (g0+g1+g2)/2, (g0-g1+g2)/2, g2) of kernel row a (transformed in fp64, rounded once).
+void pack_body_weights_wg(const float* W, uint16_t* out) {
+  for (int a = 0; a < 3; ++a)
+    for (int j = 0; j < 4; ++j)
+      for (int ks = 0; ks < 2; ++ks)
+        for (int mt = 0; mt < 4; ++mt)
+          for (int l = 0; l < 64; ++l)
+            for (int e = 0; e < 8; ++e) {
+              const int co = 16 * mt + (l & 15), ci = 32 * ks + 8 * (l >> 4) + e;
+              const float* g = W + ((co * 64 + ci) * 3 + a) * 3;
+              const double g0 = g[0], g1 = g[1], g2 = g[2];
+              const double u = j == 0 ? g0 : j == 1 ? 0.5 * (g0 + g1 + g2) : j == 2 ? 0.5 * (g0 - g1 + g2) : g2;
+              out[((((a * 4 + j) * 2 + ks) * 4 + mt) * 64 + l) * 8 + e] = f32_to_f16_bits((float)u);
+            }
+}
+
 // W: [C][64][3][3].  16x16x32: lane l holds A[row l&15][k = 8(l>>4)+j]; k-step ks covers
 // tap ks/2, input channels 32*(ks&1) .. +31.
 void pack_tail_weights(const float* W, int C, uint16_t* out) {
@@ -1026,6 +1219,10 @@ hipError_t conv_kernels_init() {
   }
   for (const void* k : {(const void*)conv_body_v4_kernel<0>, (const void*)conv_body_v4_kernel<1>}) {
     e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kV5Lds);
+    if (e != hipSuccess) return e;
+  }
+  for (const void* k : {(const void*)conv_body_wg_kernel<0>, (const void*)conv_body_wg_kernel<1>}) {
+    e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kWgLds);
     if (e != hipSuccess) return e;
   }
   for (const void* k : {(const void*)conv_body2_kernel<0>, (const void*)conv_body2_kernel<1>}) {
@@ -1075,6 +1272,15 @@ void launch_conv_body16(const half_t* in, half_t* out, const void* w16, const fl
     hipLaunchKernelGGL((conv_body_v4_kernel<0>), dim3(grid), dim3(512), kV5Lds, st, in, out, (const uint4*)w16, bias, s);
   else
     hipLaunchKernelGGL((conv_body_v4_kernel<1>), dim3(grid), dim3(512), kV5Lds, st, in, out, (const uint4*)w16, bias, s);
+}
+
+void launch_conv_body_wg(const half_t* in, half_t* out, const void* wwg, const float* bias, const ConvShape& s,
+                         int act, int num_cus, hipStream_t st) {
+  const int grid = s.tiles < num_cus ? s.tiles : num_cus;
+  if (act == 0)
+    hipLaunchKernelGGL((conv_body_wg_kernel<0>), dim3(grid), dim3(512), kWgLds, st, in, out, (const uint4*)wwg, bias, s);
+  else
+    hipLaunchKernelGGL((conv_body_wg_kernel<1>), dim3(grid), dim3(512), kWgLds, st, in, out, (const uint4*)wwg, bias, s);
 }
 
 void launch_conv_body2(const half_t* in, half_t* out, const void* w1, const float* b1, const void* w2,

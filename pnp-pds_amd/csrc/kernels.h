@@ -17,6 +17,8 @@ ConvShape make_conv_shape(int B, int H, int W);
 hipError_t conv_kernels_init();
 void pack_body_weights(const float* W, uint16_t* out);
 void pack_body_weights16(const float* W, uint16_t* out);   // conv_body_v4 (16x16x32) order, same size
+void pack_body_weights_wg(const float* W, uint16_t* out);  // conv_body_wg (row Winograd F(2,3)), kBodyWgBytes
+constexpr int kBodyWgBytes = 3 * 4 * 64 * 64 * 2;           // 98304: U[a][j][co][ci] fp16
 void pack_head_weights(const float* W, int C, uint16_t* out);
 void pack_tail_weights(const float* W, int C, uint16_t* out);
 void launch_conv_head(const half_t* in4, half_t* out, const void* w, const float* bias, const ConvShape& s,
@@ -27,6 +29,9 @@ void launch_conv_body(const half_t* in, half_t* out, const void* w, const float*
 // one 64 -> 64 layer on 16x16x32 MFMAs (weights packed by pack_body_weights16)
 void launch_conv_body16(const half_t* in, half_t* out, const void* w16, const float* bias, const ConvShape& s,
                         int act, int num_cus, hipStream_t st);
+// one 64 -> 64 layer as a row-wise Winograd F(2,3) (weights packed by pack_body_weights_wg)
+void launch_conv_body_wg(const half_t* in, half_t* out, const void* wwg, const float* bias, const ConvShape& s,
+                         int act, int num_cus, hipStream_t st);
 // two 64 -> 64 layers in one launch (the intermediate stays in LDS); in needs pad >= 2
 void launch_conv_body2(const half_t* in, half_t* out, const void* w1, const float* b1, const void* w2,
                        const float* b2, const ConvShape& s, int act, int num_cus, hipStream_t st);

@@ -192,7 +192,8 @@ class Context:
     def set_body_variant(self, variant: int):
         """Body layers per launch: 0 = one (default), 1 = two fused layers, 2 = one with the
         staggered epilogue, 3 = one on 16x16x32 MFMAs (not bit-identical: another summation
-        order).  Performance only."""
+        order), 4 = one as a row-wise Winograd F(2,3) (fp16-rounded transformed operands;
+        within the fp16 tolerance).  Performance only."""
         self._check(self.lib.pnp_set_tuning(self.h, TUNE_BODY_VARIANT, int(variant)))
 
     def set_operator(self, kind: int, h=None, mask=None, key=None):

@@ -75,14 +75,15 @@ def test_body_variants_bit_identical(gpu_ctx, name, B, C, H, W):
         np.testing.assert_array_equal(outs[0], o)
 
 
-@pytest.mark.parametrize("variant", [3])
+@pytest.mark.parametrize("variant", [3, 4])
 @pytest.mark.parametrize("name,B,C,H,W", [("DnCNN_nobn_nch_3_nlev_0.01", 3, 3, 50, 70),
                                           ("DnCNN_nobn_nch_3_nlev_0.01", 2, 3, 256, 256),
                                           ("dncnn_15", 2, 1, 37, 45)])
 def test_body_variant_mfma16(gpu_ctx, variant, name, B, C, H, W):
     """Variant 3 (16x16x32 MFMAs, planar halo) sums each output's 576 products in another
-    order than the 32x32x16 kernels, so it matches the fp16-emulating oracle to the same
-    tolerance rather than variant 0 bit for bit."""
+    order than the 32x32x16 kernels, and variant 4 (row Winograd F(2,3)) rounds transformed
+    operands to fp16 instead of the plain ones, so they match the fp16-emulating oracle to
+    the same tolerance rather than variant 0 bit for bit."""
     rng = np.random.default_rng(12)
     w = DenoiserWeights.load_npz(os.path.join(WEIGHTS_DIR, name + ".npz"))
     x = rng.uniform(0, 1, (B, C, H, W)).astype(np.float32)
