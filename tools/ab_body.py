@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--size", type=int, default=256)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--ablates", default="", help="raw PNP_TUNE_ABLATE codes instead of variants (profiling)")
+    ap.add_argument("--chunks", default="", help="denoiser images per pass instead of variants (totals per pass)")
     a = ap.parse_args()
     import torch
     from bench import synthetic_batch
@@ -32,8 +33,8 @@ def main():
     B, C, H, W = a.batch, 3, a.size, a.size
     x = torch.from_numpy(synthetic_batch(B, C, H, W, seed=1)).cuda()
     y = torch.empty_like(x)
-    vs = [int(v) for v in (a.ablates or a.variants).split(",")]
-    setv = ctx.set_ablate if a.ablates else ctx.set_body_variant
+    vs = [int(v) for v in (a.chunks or a.ablates or a.variants).split(",")]
+    setv = ctx.set_denoise_chunk if a.chunks else ctx.set_ablate if a.ablates else ctx.set_body_variant
     res = {v: {} for v in vs}
     for v in vs:                                   # warm-up
         setv(v)
@@ -46,7 +47,7 @@ def main():
             ctx.op_denoise(x.data_ptr(), y.data_ptr(), B, C, H, W)
             ctx.synchronize()
             for k, (ms, n) in ctx.profile_read().items():
-                res[v].setdefault(k, []).append(ms)
+                res[v].setdefault(k, []).append(ms * n if a.chunks else ms)
             ctx.profile_enable(False)
     for v in vs:
         print(f"variant {v}: " + "  ".join(f"{k} {statistics.median(t):.4f}" for k, t in sorted(res[v].items())),
