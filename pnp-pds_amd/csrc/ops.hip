@@ -821,6 +821,25 @@ __device__ __forceinline__ void rb_tile_origin(int tile, int tiles_x, int& i0, i
   j0 = (tile - ty * tiles_x) * kRbW;
 }
 
+// Column-pair loads / stores of the blur kernels' epilogues: nv valid columns (0..2);
+// vec = both valid and 8-B aligned (one dwordx2), else guarded scalar accesses.
+__device__ __forceinline__ f2_t ld2g(const float* __restrict__ p, size_t idx, int nv, bool vec) {
+  if (vec) return *reinterpret_cast<const f2_t*>(p + idx);
+  f2_t v = {0.f, 0.f};
+  if (nv > 0) v.x = p[idx];
+  if (nv > 1) v.y = p[idx + 1];
+  return v;
+}
+__device__ __forceinline__ void st2g(float* __restrict__ p, size_t idx, const f2_t& v, int nv, bool vec) {
+  if (vec) {
+    *reinterpret_cast<f2_t*>(p + idx) = v;
+    return;
+  }
+  if (nv > 0) p[idx] = v.x;
+  if (nv > 1) p[idx + 1] = v.y;
+}
+constexpr int kRbBatch = 2;                   // epilogue rows whose loads are in flight together
+
 // K1: u = [clamp](x - g1 Phi^T y) -> u32 and its channel of the NHWC4 fp16 denoiser input
 // u16 (2-byte stores); B: w = s - g1 y.  Block = one (plane, 64 x 64 tile).
 template <class T>
@@ -843,19 +862,40 @@ __global__ __launch_bounds__(256) void k1_blur_rb(const float* __restrict__ x, c
   __syncthreads();
   f2_t g[kRbRows];
   rb_stencil<T>(lds, wd_adj, g);
+  const int ncol = j < W ? min(2, W - j) : 0;
+  const bool al = (W & 1) == 0;              // column pairs 8-B aligned
 #pragma unroll
-  for (int r = 0; r < kRbRows; ++r) {
-    const int i = i0 + ty * kRbRows + r;
-    if (i >= H) break;
+  for (int rb = 0; rb < kRbRows; rb += kRbBatch) {   // batched loads, as in k2_blur_rb
+    f2_t xv[kRbBatch], sv[kRbBatch], yv[kRbBatch];
+    int nv[kRbBatch];
+    size_t ix[kRbBatch];
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      if (j + q >= W) break;
-      const size_t idx = pb + (size_t)i * W + j + q;
-      float uu = x[idx] - gamma1 * g[r][q];
-      if (clamp_in) uu = fminf(fmaxf(uu, 0.f), 1.f);
-      u32[idx] = uu;
-      u16[(((size_t)b * (H + 2) + i + 1) * (W + 2) + j + q + 1) * 4 + c] = (half_t)uu;
-      if (method_b) w[idx] = s[idx] - gamma1 * y[idx];
+    for (int k = 0; k < kRbBatch; ++k) {
+      const int i = i0 + ty * kRbRows + rb + k;
+      nv[k] = i < H ? ncol : 0;
+      ix[k] = pb + (size_t)min(i, H - 1) * W + j;
+      const bool vec = al && nv[k] == 2;
+      xv[k] = ld2g(x, ix[k], nv[k], vec);
+      if (method_b) {
+        sv[k] = ld2g(s, ix[k], nv[k], vec);
+        yv[k] = ld2g(y, ix[k], nv[k], vec);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kRbBatch; ++k) {
+      const int i = i0 + ty * kRbRows + rb + k;
+      f2_t uo, wo;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        float uu = xv[k][q] - gamma1 * g[rb + k][q];
+        if (clamp_in) uu = fminf(fmaxf(uu, 0.f), 1.f);
+        uo[q] = uu;
+        if (q < nv[k]) u16[(((size_t)b * (H + 2) + i + 1) * (W + 2) + j + q + 1) * 4 + c] = (half_t)uu;
+        wo[q] = sv[k][q] - gamma1 * yv[k][q];
+      }
+      const bool vec = al && nv[k] == 2;
+      st2g(u32, ix[k], uo, nv[k], vec);
+      if (method_b) st2g(w, ix[k], wo, nv[k], vec);
     }
   }
 }
@@ -894,41 +934,70 @@ __global__ __launch_bounds__(256) void k2_blur_rb(const float* __restrict__ xn, 
     double d2 = 0, e2 = 0, n2 = 0, t2 = 0;
     const float th = METHOD == M_B ? theta[b] : 0.f;
     const int j = j0 + 2 * tx;
+    const int ncol = j < W ? min(2, W - j) : 0;
+    const bool al = (W & 1) == 0;            // column pairs 8-B aligned
+    // Four rows at a time: every stream's loads of the batch are issued before the first
+    // use (the per-pixel form waited on each load in turn: y is read and written).
 #pragma unroll
-    for (int r = 0; r < kRbRows; ++r) {
-      const int i = i0 + ty * kRbRows + r;
-      if (i >= H) break;
+    for (int rb = 0; rb < kRbRows; rb += kRbBatch) {
+      f2_t yv[kRbBatch], bv[kRbBatch], av[kRbBatch], ov[kRbBatch], tv[kRbBatch], sv[kRbBatch], wv[kRbBatch];
+      int nv[kRbBatch];
+      size_t ix[kRbBatch];
 #pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        if (j + q >= W) break;
-        const size_t idx = (size_t)bc * plane + (size_t)i * W + j + q;
-        double gv = g[r][q];
+      for (int k = 0; k < kRbBatch; ++k) {
+        const int i = i0 + ty * kRbRows + rb + k;
+        nv[k] = i < H ? ncol : 0;
+        ix[k] = (size_t)bc * plane + (size_t)min(i, H - 1) * W + j;
+        const bool vec = al && nv[k] == 2;
+        yv[k] = ld2g(y, ix[k], nv[k], vec);
+        bv[k] = ld2g(xobs, ix[k], nv[k], vec);
         if (METHOD == M_B) {
-          const float wv = w[idx];
-          const float sp = copysignf(fmaxf(fabsf(wv) - th, 0.f), wv);   // operators.py:98
-          gv += 2.0 * (double)sp - (double)s[idx];
-          s[idx] = sp;
-        }
-        const double v = (double)y[idx] + gamma2 * gv;
-        const double ob = xobs[idx];
-        if (METHOD == M_C) {
-          const double tt = v * inv_g2 - gkl_gamma * gkl_alpha;
-          const double p = 0.5 * (tt + sqrt(tt * tt + 4.0 * gkl_gamma * ob));
-          y[idx] = (float)(v - gamma2 * p);
-        } else {
-          y[idx] = (float)v;
-          const double dd = v * inv_g2 - ob;
-          d2 += dd * dd;
+          sv[k] = ld2g(s, ix[k], nv[k], vec);
+          wv[k] = ld2g(w, ix[k], nv[k], vec);
         }
         if (record) {
-          const double a = xn[idx], o = xo[idx];
-          e2 += (a - o) * (a - o);
-          n2 += o * o;
-          if (xtrue) {
-            const double qv = (double)xtrue[idx] - a;
-            t2 += qv * qv;
+          av[k] = ld2g(xn, ix[k], nv[k], vec);
+          ov[k] = ld2g(xo, ix[k], nv[k], vec);
+          tv[k] = xtrue ? ld2g(xtrue, ix[k], nv[k], vec) : f2_t{0.f, 0.f};
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < kRbBatch; ++k) {
+        f2_t yo = yv[k], so = {0.f, 0.f};
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          if (q >= nv[k]) break;
+          double gv = g[rb + k][q];
+          if (METHOD == M_B) {
+            const float wq = wv[k][q];
+            const float sp = copysignf(fmaxf(fabsf(wq) - th, 0.f), wq);   // operators.py:98
+            gv += 2.0 * (double)sp - (double)sv[k][q];
+            so[q] = sp;
+          }
+          const double v = (double)yv[k][q] + gamma2 * gv;
+          const double ob = bv[k][q];
+          if (METHOD == M_C) {
+            const double tt = v * inv_g2 - gkl_gamma * gkl_alpha;
+            const double p = 0.5 * (tt + sqrt(tt * tt + 4.0 * gkl_gamma * ob));
+            yo[q] = (float)(v - gamma2 * p);
+          } else {
+            yo[q] = (float)v;
+            const double dd = v * inv_g2 - ob;
+            d2 += dd * dd;
+          }
+          if (record) {
+            const double a = av[k][q], o = ov[k][q];
+            e2 += (a - o) * (a - o);
+            n2 += o * o;
+            if (xtrue) {
+              const double qv = (double)tv[k][q] - a;
+              t2 += qv * qv;
+            }
           }
         }
+        const bool vec = al && nv[k] == 2;
+        st2g(y, ix[k], yo, nv[k], vec);
+        if (METHOD == M_B) st2g(s, ix[k], so, nv[k], vec);
       }
     }
     // 32 x 32 cell = 16 threads (tx) x 4 thread rows (ty) = two half-cells of two waves:

@@ -13,7 +13,7 @@ import threading
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libpnppds.so")
+LIB_PATH = os.environ.get("PNP_LIB_PATH") or os.path.join(os.path.dirname(_HERE), "lib", "libpnppds.so")   # override: profiling A/B only
 
 PNP_OK = 0
 ERRORS = {-1: "PNP_E_ARG", -2: "PNP_E_UNSUPPORTED", -3: "PNP_E_HIP", -4: "PNP_E_OOM", -5: "PNP_E_STATE", -6: "PNP_E_INTERNAL"}
