@@ -19,6 +19,7 @@
 #include "kernels.h"
 #include "taps_gen.h"
 
+#include <type_traits>
 #include <utility>
 
 namespace pnp {
@@ -221,11 +222,15 @@ __global__ __launch_bounds__(256) void k2_dual(const float* __restrict__ xn, con
 // scalar otherwise.  K2's four partial sums are reduced once per block (wave shuffles, then
 // the 4 waves in a fixed order): partials [B][tiles][4], the layout k3 re-reduces.
 // =====================================================================================
-template <int KIND>
-__device__ __forceinline__ float4 op_apply4(float4 v, const uint8_t* __restrict__ mask, size_t pix, bool vec, int nv) {
+// VEC (compile time): 16-B accesses; else nv (0..4) guarded scalar ones.  Callers branch
+// once on a uniform-per-thread flag into a VEC and a scalar instantiation: with a runtime
+// flag inside each access the compiler merged the two paths into partial loads, each behind
+// its own branch and vmcnt(0) wait.
+template <int KIND, bool VEC>
+__device__ __forceinline__ float4 op_apply4(float4 v, const uint8_t* __restrict__ mask, size_t pix, int nv) {
   if (KIND == OP_MASK) {                 // select (t[q] = 0), so a NaN/inf at a dropped pixel cannot leak
     uchar4 m = {0, 0, 0, 0};
-    if (vec) {
+    if (VEC) {
       m = *reinterpret_cast<const uchar4*>(mask + pix);
     } else {
       if (nv > 0) m.x = mask[pix];
@@ -238,8 +243,9 @@ __device__ __forceinline__ float4 op_apply4(float4 v, const uint8_t* __restrict_
   return v;
 }
 
-__device__ __forceinline__ float4 ld4(const float* __restrict__ p, bool vec, int nv) {
-  if (vec) return *reinterpret_cast<const float4*>(p);
+template <bool VEC>
+__device__ __forceinline__ float4 ld4(const float* __restrict__ p, int nv) {
+  if (VEC) return *reinterpret_cast<const float4*>(p);
   float4 v = {0.f, 0.f, 0.f, 0.f};
   if (nv > 0) v.x = p[0];
   if (nv > 1) v.y = p[1];
@@ -247,8 +253,9 @@ __device__ __forceinline__ float4 ld4(const float* __restrict__ p, bool vec, int
   if (nv > 3) v.w = p[3];
   return v;
 }
-__device__ __forceinline__ void st4(float* __restrict__ p, float4 v, bool vec, int nv) {
-  if (vec) { *reinterpret_cast<float4*>(p) = v; return; }
+template <bool VEC>
+__device__ __forceinline__ void st4(float* __restrict__ p, float4 v, int nv) {
+  if (VEC) { *reinterpret_cast<float4*>(p) = v; return; }
   if (nv > 0) p[0] = v.x;
   if (nv > 1) p[1] = v.y;
   if (nv > 2) p[2] = v.z;
@@ -272,34 +279,49 @@ __global__ __launch_bounds__(256) void k1_elem(const float* __restrict__ x, cons
   const int i0 = ty * kST + 4 * (threadIdx.x >> 5), j = (tile - ty * tiles_x) * kST + (threadIdx.x & 31);
   if (j >= W) return;
   const size_t plane = (size_t)H * W;
+  const int nr = min(4, H - i0);
+  // all rows' loads first, B's extra streams a compile-time choice (a runtime branch
+  // around a load made the compiler wait vmcnt(0) at the join)
+  auto body = [&](auto mb_c) {
+    constexpr bool MB = decltype(mb_c)::value;
+    float xv[4][CM], yv[4][CM], sv[4][CM];
+    uint8_t keep[4];                          // compared only after every load is in flight
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int i = i0 + r;
-    if (i >= H) break;
-    const size_t pix = (size_t)i * W + j;
-    const bool keep = KIND != OP_MASK || mask[pix] != 0;
-    float xv[CM], yv[CM];
+    for (int r = 0; r < 4; ++r) {
+      if (r >= nr) break;
+      const size_t pix = (size_t)(i0 + r) * W + j;
+      keep[r] = KIND == OP_MASK ? mask[pix] : 1;
 #pragma unroll
-    for (int c = 0; c < CM; ++c) {
-      if (c >= C) break;
-      const size_t o = ((size_t)b * C + c) * plane + pix;
-      xv[c] = x[o];
-      yv[c] = y[o];
+      for (int c = 0; c < CM; ++c) {
+        if (c >= C) break;
+        const size_t o = ((size_t)b * C + c) * plane + pix;
+        xv[r][c] = x[o];
+        yv[r][c] = y[o];
+        if (MB) sv[r][c] = s[o];
+      }
     }
-    half4_t h4 = {0, 0, 0, 0};
 #pragma unroll
-    for (int c = 0; c < CM; ++c) {
-      if (c >= C) break;
-      const size_t o = ((size_t)b * C + c) * plane + pix;
-      const float g = keep ? yv[c] : 0.f;    // random_sampling: t[q] = 0 (a NaN cannot leak)
-      float u = xv[c] - gamma1 * g;
-      if (clamp_in) u = fminf(fmaxf(u, 0.f), 1.f);
-      u32[o] = u;
-      h4[c] = (half_t)u;
-      if (method_b) w[o] = s[o] - gamma1 * yv[c];
+    for (int r = 0; r < 4; ++r) {
+      if (r >= nr) break;
+      const int i = i0 + r;
+      const size_t pix = (size_t)i * W + j;
+      half4_t h4 = {0, 0, 0, 0};
+#pragma unroll
+      for (int c = 0; c < CM; ++c) {
+        if (c >= C) break;
+        const size_t o = ((size_t)b * C + c) * plane + pix;
+        const float g = keep[r] != 0 ? yv[r][c] : 0.f;   // random_sampling: t[q] = 0 (a NaN cannot leak)
+        float u = xv[r][c] - gamma1 * g;
+        if (clamp_in) u = fminf(fmaxf(u, 0.f), 1.f);
+        u32[o] = u;
+        h4[c] = (half_t)u;
+        if (MB) w[o] = sv[r][c] - gamma1 * yv[r][c];
+      }
+      *reinterpret_cast<half4_t*>(u16 + (((size_t)b * (H + 2) + i + 1) * (W + 2) + j + 1) * 4) = h4;
     }
-    *reinterpret_cast<half4_t*>(u16 + (((size_t)b * (H + 2) + i + 1) * (W + 2) + j + 1) * 4) = h4;
-  }
+  };
+  if (method_b) body(std::true_type{});
+  else body(std::false_type{});
 }
 
 template <int KIND, int METHOD, int NC>
@@ -322,52 +344,72 @@ __global__ __launch_bounds__(256) void k2_elem(const float* __restrict__ xn, con
     const bool vec = (W & 3) == 0 && nv == 4;
     const size_t plane = (size_t)H * W, pix = (size_t)i * W + j;
     const float th = METHOD == M_B ? theta[b] : 0.f;
+    auto body = [&](auto vec_c, auto true_c) {
+      constexpr bool VEC = decltype(vec_c)::value, TRUE_ = decltype(true_c)::value;   // TRUE_: record && xtrue
+      // every channel's loads first (stores to y could otherwise not pass loads of y)
+      float4 a4[CM], o4[CM], y4[CM], b4[CM], s4[CM], w4[CM], t4[CM];
 #pragma unroll
-    for (int c = 0; c < CM; ++c) {
-      if (c >= C) break;
-      const size_t o = ((size_t)b * C + c) * plane + pix;
-      const float4 a4 = ld4(xn + o, vec, nv), o4 = ld4(xo + o, vec, nv);
-      float4 g4;
-      g4.x = 2.f * a4.x - o4.x; g4.y = 2.f * a4.y - o4.y; g4.z = 2.f * a4.z - o4.z; g4.w = 2.f * a4.w - o4.w;
-      g4 = op_apply4<KIND>(g4, mask, pix, vec, nv);
-      const float4 y4 = ld4(y + o, vec, nv), b4 = ld4(xobs + o, vec, nv);
-      float4 s4 = {}, w4 = {}, sp4 = {}, t4 = {}, yo;
-      if (METHOD == M_B) { s4 = ld4(s + o, vec, nv); w4 = ld4(w + o, vec, nv); }
-      if (record && xtrue) t4 = ld4(xtrue + o, vec, nv);
+      for (int c = 0; c < CM; ++c) {
+        if (c >= C) break;
+        const size_t o = ((size_t)b * C + c) * plane + pix;
+        a4[c] = ld4<VEC>(xn + o, nv);
+        o4[c] = ld4<VEC>(xo + o, nv);
+        y4[c] = ld4<VEC>(y + o, nv);
+        b4[c] = ld4<VEC>(xobs + o, nv);
+        if (METHOD == M_B) { s4[c] = ld4<VEC>(s + o, nv); w4[c] = ld4<VEC>(w + o, nv); }
+        if (TRUE_) t4[c] = ld4<VEC>(xtrue + o, nv);   // compile-time: a runtime branch here waited vmcnt(0)
+      }
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        double gv = f4get(g4, k);
-        if (METHOD == M_B) {
-          const float wv = f4get(w4, k);
-          const float sp = copysignf(fmaxf(fabsf(wv) - th, 0.f), wv);   // operators.py:98
-          gv += 2.0 * (double)sp - (double)f4get(s4, k);
-          (k == 0 ? sp4.x : k == 1 ? sp4.y : k == 2 ? sp4.z : sp4.w) = sp;
-        }
-        const double v = (double)f4get(y4, k) + gamma2 * gv;
-        const double ob = f4get(b4, k);
-        float yk;
-        if (METHOD == M_C) {
-          const double tt = v * inv_g2 - gkl_gamma * gkl_alpha;
-          const double p = 0.5 * (tt + sqrt(tt * tt + 4.0 * gkl_gamma * ob));
-          yk = (float)(v - gamma2 * p);
-        } else {
-          yk = (float)v;
-          const double dd = v * inv_g2 - ob;
-          if (k < nv) d2 += dd * dd;
-        }
-        (k == 0 ? yo.x : k == 1 ? yo.y : k == 2 ? yo.z : yo.w) = yk;
-        if (record && k < nv) {
-          const double a = f4get(a4, k), oo = f4get(o4, k);
-          e2 += (a - oo) * (a - oo);
-          n2 += oo * oo;
-          if (xtrue) {
-            const double q = (double)f4get(t4, k) - a;
-            t2 += q * q;
+      for (int c = 0; c < CM; ++c) {
+        if (c >= C) break;
+        const size_t o = ((size_t)b * C + c) * plane + pix;
+        float4 g4;
+        g4.x = 2.f * a4[c].x - o4[c].x; g4.y = 2.f * a4[c].y - o4[c].y;
+        g4.z = 2.f * a4[c].z - o4[c].z; g4.w = 2.f * a4[c].w - o4[c].w;
+        g4 = op_apply4<KIND, VEC>(g4, mask, pix, nv);
+        float4 sp4 = {}, yo;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          double gv = f4get(g4, k);
+          if (METHOD == M_B) {
+            const float wv = f4get(w4[c], k);
+            const float sp = copysignf(fmaxf(fabsf(wv) - th, 0.f), wv);   // operators.py:98
+            gv += 2.0 * (double)sp - (double)f4get(s4[c], k);
+            (k == 0 ? sp4.x : k == 1 ? sp4.y : k == 2 ? sp4.z : sp4.w) = sp;
+          }
+          const double v = (double)f4get(y4[c], k) + gamma2 * gv;
+          const double ob = f4get(b4[c], k);
+          float yk;
+          if (METHOD == M_C) {
+            const double tt = v * inv_g2 - gkl_gamma * gkl_alpha;
+            const double p = 0.5 * (tt + sqrt(tt * tt + 4.0 * gkl_gamma * ob));
+            yk = (float)(v - gamma2 * p);
+          } else {
+            yk = (float)v;
+            const double dd = v * inv_g2 - ob;
+            if (k < nv) d2 += dd * dd;
+          }
+          (k == 0 ? yo.x : k == 1 ? yo.y : k == 2 ? yo.z : yo.w) = yk;
+          if (record && k < nv) {
+            const double a = f4get(a4[c], k), oo = f4get(o4[c], k);
+            e2 += (a - oo) * (a - oo);
+            n2 += oo * oo;
+            if (TRUE_) {
+              const double q = (double)f4get(t4[c], k) - a;
+              t2 += q * q;
+            }
           }
         }
+        st4<VEC>(y + o, yo, nv);
+        if (METHOD == M_B) st4<VEC>(s + o, sp4, nv);
       }
-      st4(y + o, yo, vec, nv);
-      if (METHOD == M_B) st4(s + o, sp4, vec, nv);
+    };
+    if (record && xtrue) {
+      if (vec) body(std::true_type{}, std::true_type{});
+      else body(std::false_type{}, std::true_type{});
+    } else {
+      if (vec) body(std::true_type{}, std::false_type{});
+      else body(std::false_type{}, std::false_type{});
     }
   }
   d2 = wave_sum(d2);
