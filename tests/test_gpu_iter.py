@@ -130,3 +130,27 @@ def test_ragged_shapes_vs_oracle(deg_op, method, C, H, W):
     np.testing.assert_allclose(psnr, po, atol=0.01)
     np.testing.assert_allclose(x, xo, atol=5e-3)
     np.testing.assert_allclose(s, so, atol=5e-3)
+
+
+@pytest.mark.parametrize("case", ["A_blur", "A_rs", "B_blur", "C_rs"])
+def test_metrics_paths_do_not_change_iterates(case):
+    """x_true and metric recording feed only the metrics: with x_true absent (PSNR/SSIM NaN) or
+    recording off (all metrics NaN) the iterates are the same bits.  Covers the kernels'
+    compile-time no-x_true / no-record instantiations."""
+    from pnppds import operators as ops
+    from pnppds.iteration import test_iter_batch
+    g = load_golden(f"iter_{case}.npz")
+    g1, g2, as_, an, lam, m1, m2, gadmm, sig, sp, palpha, iters, ch, r = g["params"]
+    phi, adj = ops.get_observation_operators(str(g["deg_op"]), "blur_1", r)
+    arch = str(g["arch"]) + ".pth"
+    args = (g1, g2, as_, an, lam, int(m1), int(m2), gadmm, sig, sp, palpha, arch, int(iters), str(g["method"]),
+            int(ch), r)
+    x0, xo, xt = g["x_0"][None], g["x_obs"][None], g["x_true"][None]
+    full = test_iter_batch(x0, xo, xt, phi, adj, *args)
+    no_true = test_iter_batch(x0, xo, None, phi, adj, *args)
+    no_rec = test_iter_batch(x0, xo, xt, phi, adj, *args, record_metrics=False)
+    for other in (no_true, no_rec):
+        np.testing.assert_array_equal(other[0], full[0])     # x
+        np.testing.assert_array_equal(other[1], full[1])     # s
+    np.testing.assert_array_equal(no_true[2], full[2])       # c_n does not use x_true
+    assert np.isnan(no_true[3]).all() and np.isfinite(full[3]).all()
