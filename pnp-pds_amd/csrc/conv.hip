@@ -51,6 +51,13 @@ __device__ __forceinline__ void store_act64(half_t* __restrict__ out, const Conv
 }
 
 
+// XCD-aware tile order for a persistent grid: workgroup b runs on XCD b % 8, so logical
+// block (b % 8) * (G / 8) + b / 8 gives each XCD a contiguous run of G / 8 tiles per round
+// (neighbouring tiles, whose halos overlap, share one L2).  Identity when G % 8 != 0.
+__device__ __forceinline__ int xcd_block(int b, int G) {
+  return (G & 7) ? b : (b & 7) * (G >> 3) + (b >> 3);
+}
+
 // bias + activation of 8 accumulator rows -> 8 fp16 (packed adds/muls; LeakyReLU(x) = max(x, 0.01x),
 // ReLU(x) = max(x, 0): bit-identical to act_fn, half the VALU of the select form)
 typedef float f2v_t __attribute__((ext_vector_type(2)));
@@ -183,7 +190,7 @@ __global__ __launch_bounds__(512, 2) void conv_body_v3_kernel(const half_t* __re
   };
   const int ndma = dma_count<8>(wave);
 
-  int t = blockIdx.x;
+  int t = xcd_block(blockIdx.x, gridDim.x);
   if (t < s.tiles) {
     issue_dma(t, 0);
     issue_dma(t + gridDim.x, 1);
