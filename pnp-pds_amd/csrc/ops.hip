@@ -243,9 +243,13 @@ __device__ __forceinline__ float4 op_apply4(float4 v, const uint8_t* __restrict_
   return v;
 }
 
+typedef float f4v_t __attribute__((ext_vector_type(4)));
 template <bool VEC>
 __device__ __forceinline__ float4 ld4(const float* __restrict__ p, int nv) {
-  if (VEC) return *reinterpret_cast<const float4*>(p);
+  if (VEC) {
+    const f4v_t v = __builtin_nontemporal_load(reinterpret_cast<const f4v_t*>(p));
+    return float4{v.x, v.y, v.z, v.w};
+  }
   float4 v = {0.f, 0.f, 0.f, 0.f};
   if (nv > 0) v.x = p[0];
   if (nv > 1) v.y = p[1];
@@ -255,7 +259,7 @@ __device__ __forceinline__ float4 ld4(const float* __restrict__ p, int nv) {
 }
 template <bool VEC>
 __device__ __forceinline__ void st4(float* __restrict__ p, float4 v, int nv) {
-  if (VEC) { *reinterpret_cast<float4*>(p) = v; return; }
+  if (VEC) { __builtin_nontemporal_store(f4v_t{v.x, v.y, v.z, v.w}, reinterpret_cast<f4v_t*>(p)); return; }
   if (nv > 0) p[0] = v.x;
   if (nv > 1) p[1] = v.y;
   if (nv > 2) p[2] = v.z;
@@ -295,9 +299,9 @@ __global__ __launch_bounds__(256) void k1_elem(const float* __restrict__ x, cons
       for (int c = 0; c < CM; ++c) {
         if (c >= C) break;
         const size_t o = ((size_t)b * C + c) * plane + pix;
-        xv[r][c] = x[o];
-        yv[r][c] = y[o];
-        if (MB) sv[r][c] = s[o];
+        xv[r][c] = __builtin_nontemporal_load(x + o);   // streamed once
+        yv[r][c] = __builtin_nontemporal_load(y + o);
+        if (MB) sv[r][c] = __builtin_nontemporal_load(s + o);
       }
     }
 #pragma unroll
@@ -492,20 +496,35 @@ __device__ __forceinline__ double block_sum1024(double v, double* scratch) {
 
 // One radix level: histogram of candidates whose bits above this level equal `prefix`,
 // then the highest bin j with f(lo_j) >= 0.  Updates prefix / (Khi, Shi).
+// Bin sums are kept exactly: every value of a bin shares its float exponent (the bins split
+// the bit pattern below the 8 exponent bits), so a bin's sum is (sum of 24-bit significands,
+// a uint64 that LDS atomics add in any order to the same result) x 2^(exponent - 150).
+// fp32 atomic adds here made theta depend on the atomics' order: a batch and a one-image run
+// could pick another bin near the threshold (a batch-vs-single mismatch seen once in ~20 runs).
+__device__ __forceinline__ unsigned sel_significand(unsigned u) {
+  const unsigned e = u >> 23, m = u & 0x7fffffu;
+  return e ? (m | 0x800000u) : m;
+}
+template <int SH>
+__device__ __forceinline__ double sel_bin_sum(const unsigned long long* sm, unsigned prefix, int j) {
+  const int e = (int)(((prefix | ((unsigned)j << SH)) >> 23) & 0xffu);
+  return ldexp((double)sm[j], e ? e - 150 : -149);   // exact: the sum has < 48 significant bits
+}
+
 template <int SH, int NBITS>
 __device__ __forceinline__ void select_level(const unsigned* __restrict__ vb, size_t n, double eta,
                                              unsigned& prefix, double& Khi, double& Shi, unsigned* cnt,
-                                             float* sm, int* s_j, double* s_KS) {
+                                             unsigned long long* sm, int* s_j, double* s_KS) {
   constexpr int nb = 1 << NBITS;
   constexpr unsigned hi_mask = (SH + NBITS >= 31) ? 0u : (0x7fffffffu & ~((1u << (SH + NBITS)) - 1u));
-  for (int j = threadIdx.x; j < nb; j += kSelThreads) { cnt[j] = 0; sm[j] = 0.f; }
+  for (int j = threadIdx.x; j < nb; j += kSelThreads) { cnt[j] = 0; sm[j] = 0ull; }
   __syncthreads();
   for (size_t i = threadIdx.x; i < n; i += kSelThreads) {
     const unsigned u = vb[i] & 0x7fffffffu;
     if ((u & hi_mask) == prefix) {
       const unsigned j = (u >> SH) & (unsigned)(nb - 1);
       atomicAdd(&cnt[j], 1u);
-      atomicAdd(&sm[j], __uint_as_float(u));
+      atomicAdd(&sm[j], (unsigned long long)sel_significand(u));   // exact, so order-independent
     }
   }
   __syncthreads();
@@ -513,7 +532,7 @@ __device__ __forceinline__ void select_level(const unsigned* __restrict__ vb, si
     constexpr int per = nb / 64;
     const int lane = threadIdx.x;
     double kc = 0, sc = 0;
-    for (int q = 0; q < per; ++q) { kc += cnt[lane * per + q]; sc += sm[lane * per + q]; }
+    for (int q = 0; q < per; ++q) { kc += cnt[lane * per + q]; sc += sel_bin_sum<SH>(sm, prefix, lane * per + q); }
     double ks = kc, ss = sc;                   // inclusive suffix over lanes lane..63
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
@@ -525,7 +544,7 @@ __device__ __forceinline__ void select_level(const unsigned* __restrict__ vb, si
     double fK = 0, fS = 0;
     for (int q = per - 1; q >= 0; --q) {
       const int j = lane * per + q;
-      const double K2 = K + cnt[j], S2 = S + sm[j];
+      const double K2 = K + cnt[j], S2 = S + sel_bin_sum<SH>(sm, prefix, j);
       const double lo = (double)__uint_as_float(prefix | ((unsigned)j << SH));
       if (S2 - K2 * lo - eta >= 0.0) { found = j; fK = K; fS = S; break; }
       K = K2; S = S2;
@@ -542,7 +561,7 @@ __device__ __forceinline__ void select_level(const unsigned* __restrict__ vb, si
   __syncthreads();
   if (*s_j == 0 && threadIdx.x == 0) {         // "above bin 0" = Khi + all bins >= 1, exactly
     double K = Khi, S = Shi;
-    for (int j = nb - 1; j >= 1; --j) { K += cnt[j]; S += sm[j]; }
+    for (int j = nb - 1; j >= 1; --j) { K += cnt[j]; S += sel_bin_sum<SH>(sm, prefix, j); }
     s_KS[0] = K; s_KS[1] = S;
   }
   __syncthreads();
@@ -555,7 +574,7 @@ __device__ __forceinline__ void select_level(const unsigned* __restrict__ vb, si
 __global__ __launch_bounds__(kSelThreads) void l1_select_kernel(const float* __restrict__ v, float* __restrict__ theta,
                                                                  size_t n, double eta) {
   __shared__ unsigned cnt[2048];
-  __shared__ float sm[2048];
+  __shared__ unsigned long long sm[2048];
   __shared__ double red[8];
   __shared__ int s_j;
   __shared__ double s_KS[2];
