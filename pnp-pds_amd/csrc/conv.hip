@@ -962,12 +962,12 @@ __global__ __launch_bounds__(256) void conv_head_kernel(const half_t* __restrict
       unsigned char* px = stg + (n * 32 + col) * 128;
       const int sw = col & 7;
       half8_t v[4];
-#pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        v[0][r] = (half_t)act_fn(a0[r] + bias_r[0][r], act);
-        v[1][r] = (half_t)act_fn(a0[r + 8] + bias_r[0][r + 8], act);
-        v[2][r] = (half_t)act_fn(a1[r] + bias_r[1][r], act);
-        v[3][r] = (half_t)act_fn(a1[r + 8] + bias_r[1][r + 8], act);
+      if (act == 0) {                         // packed bias + activation (bit-identical to act_fn)
+        v[0] = bias_act8<0>(a0, 0, bias_r[0]); v[1] = bias_act8<0>(a0, 8, bias_r[0] + 8);
+        v[2] = bias_act8<0>(a1, 0, bias_r[1]); v[3] = bias_act8<0>(a1, 8, bias_r[1] + 8);
+      } else {
+        v[0] = bias_act8<1>(a0, 0, bias_r[0]); v[1] = bias_act8<1>(a0, 8, bias_r[0] + 8);
+        v[2] = bias_act8<1>(a1, 0, bias_r[1]); v[3] = bias_act8<1>(a1, 8, bias_r[1] + 8);
       }
       *reinterpret_cast<half8_t*>(px + 16 * ((2 * h) ^ sw)) = v[0];          // channels 16h .. +7
       *reinterpret_cast<half8_t*>(px + 16 * ((2 * h + 1) ^ sw)) = v[1];      // 16h+8 .. +15
