@@ -1,24 +1,32 @@
 """Benchmark: PnP-PDS iterations/s on batch=256 RGB 256x256 (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--size S]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config metric|cfg1..cfg5] [--batch B]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
 
-A "step" is one PnP-PDS iteration (iteration.py:48-52, ours-A with the blur operator,
-blur_1.mat, sigma=0.01, real DnCNN_nobn_nch_3_nlev_0.01 weights) over a batch of 256
-synthetic RGB 256x256 images per GPU, inputs resident in HBM.  Images are independent, so
-ranks process disjoint shards with no data-path collective (weak scaling: 256 images per
-GPU).  ``value`` = image-iterations/s over the whole job (sum over ranks / max rank time).
+A "step" is one PnP-PDS iteration over the whole per-GPU batch, inputs resident in HBM.  The
+default (``--config metric``) is the metric's workload: ours-A (iteration.py:48-52) with the
+blur operator (blur_1.mat), sigma = 0.01, real DnCNN_nobn_nch_3_nlev_0.01 weights, 256
+synthetic RGB 256x256 images per GPU.  The other configurations are BASELINE.json's
+(SURVEY.md §8d parameters), timed the same way:
+    cfg1  1 x gray 256^2, Id, ours-A (nch_1 weights)
+    cfg2  1 x RGB 256^2, blur, ours-A
+    cfg3  64 x RGB 256^2, blur + Gaussian + salt-and-pepper, ours-B (l1-ball path)
+    cfg4  32 x RGB 512^2 per GPU (256 over 8 GPUs), random sampling + Poisson, ours-C
+    cfg5  64 x RGB 1024^2 per GPU (512 over 8), blur + Gaussian + sparse, comparisonB-2 (ADMM,
+          m1 = 35, m2 = 5); one step = one outer iteration.
+Images are independent, so ranks process disjoint shards with no data-path collective (weak
+scaling).  ``value`` = image-iterations/s over the whole job (sum over ranks / max rank time).
 
-Also reported: ``roofline`` of the dominant kernel (conv_body: 288 FLOP/B, below the
-2500/8 = 312 FLOP/B ridge, so HBM-bound: algorithmic bytes / HIP-event duration vs 8 TB/s,
-with the MFMA fraction alongside and ``traffic`` = PMC-measured bytes per launch from this
-round's committed profile), HBM fractions of the fused
+Also reported: ``roofline`` of the dominant kernel (conv_body, HBM-bound at 288 FLOP/B:
+algorithmic bytes / HIP-event duration vs 8 TB/s, MFMA fraction alongside, ``traffic`` =
+PMC-measured bytes per launch from the committed profile), HBM fractions of the fused
 prox/operator kernels, PSNR delta vs the CPU oracle on image 0, and ``cpu_baseline``: the
 oracle restatement of the reference's test_iter timed on this host (rank 0, N=1 only).
 """
 import argparse
 import json
 import os
+import platform
 import sys
 import time
 
@@ -31,10 +39,32 @@ sys.path.insert(0, REPO)
 METRIC = "PDS iters/sec, batch=256 RGB 256×256, 1/2/4/8 GPU; PSNR Δ vs ref"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 FP16_PEAK_TFLOPS = 2500.0      # dense fp16/bf16 MFMA (spec, no sparsity)
-ARCH = "DnCNN_nobn_nch_3_nlev_0.01"
-GAMMA1 = GAMMA2 = 0.99         # main.py:144-147 / ideas/param_memo.py:7
-ALPHA_N = 0.95
-SIGMA = 0.01
+FP32_PEAK_TFLOPS = 157.3       # fp32 MFMA (= fp32 vector peak)
+
+# SURVEY.md §8(d) per-config parameters (param_memo.py / utils_parse_args.py defaults)
+CONFIGS = {
+    "metric": dict(B=256, C=3, S=256, op="blur", method="A-Proposed", sigma=0.01, sp=0.0, poisson=False,
+                   g1=0.99, g2=0.99, a_n=0.95, a_s=1.0, lam=1.0, r=0.8, m1=15, m2=15,
+                   desc="ours-A (A-Proposed) blur, batch={B}/GPU RGB {S}x{S}"),
+    "cfg1": dict(B=1, C=1, S=256, op="Id", method="A-Proposed", sigma=0.01, sp=0.0, poisson=False,
+                 g1=0.99, g2=0.99, a_n=0.95, a_s=1.0, lam=1.0, r=0.8, m1=15, m2=15,
+                 desc="cfg1: ours-A Id, {B} x gray {S}x{S}"),
+    "cfg2": dict(B=1, C=3, S=256, op="blur", method="A-Proposed", sigma=0.01, sp=0.0, poisson=False,
+                 g1=0.99, g2=0.99, a_n=0.95, a_s=1.0, lam=1.0, r=0.8, m1=15, m2=15,
+                 desc="cfg2: ours-A blur, {B} x RGB {S}x{S}"),
+    "cfg3": dict(B=64, C=3, S=256, op="blur", method="B-Proposed", sigma=0.01, sp=0.1, poisson=False,
+                 g1=1.0, g2=0.49, a_n=0.95, a_s=0.95, lam=1.0, r=0.8, m1=15, m2=15,
+                 desc="cfg3: ours-B blur + Gaussian + salt-and-pepper, batch={B}/GPU RGB {S}x{S}"),
+    "cfg4": dict(B=32, C=3, S=512, op="random_sampling", method="C-Proposed", sigma=0.0, sp=0.0, poisson=True,
+                 g1=0.00035, g2=1 / 0.00035, a_n=1.0, a_s=1.0, lam=1.0, r=0.8, m1=15, m2=15,
+                 desc="cfg4: ours-C random_sampling(r=0.8) + Poisson(alpha=300), batch={B}/GPU "
+                      "(256 over 8 GPUs) RGB {S}x{S}"),
+    "cfg5": dict(B=64, C=3, S=1024, op="blur", method="comparisonB-2", sigma=0.01, sp=0.1, poisson=False,
+                 g1=0.99, g2=0.99, a_n=0.95, a_s=0.95, lam=1.0, r=0.8, m1=35, m2=5,
+                 desc="cfg5: comparisonB-2 ADMM (m1=35, m2=5) blur + Gaussian + sparse, batch={B}/GPU "
+                      "(512 over 8 GPUs) RGB {S}x{S}; one step = one outer iteration"),
+}
+POISSON_ALPHA = 300.0
 
 
 def log(*a):
@@ -60,11 +90,13 @@ def synthetic_batch(B, C, H, W, seed):
     return out
 
 
-def images_per_launch(B, H, W, chunk):
-    """Mirror of capi.hip denoise_chunk(): images per conv launch."""
+def images_per_launch(B, H, W, chunk, fp32=False):
+    """Mirror of capi.hip denoise_chunk() / run_denoiser32(): images per conv launch."""
     if chunk > 0:
         return min(chunk, B)
-    per_img = 2.0 * (H + 2) * (W + 2) * 64 * 2
+    if fp32:
+        return max(1, min(int(16e9 // (2.0 * (H + 2) * (W + 2) * 64 * 4)), B))
+    per_img = 2.0 * (H + 4) * (W + 4) * 64 * 2
     return max(1, min(int(8e9 // per_img), B))
 
 
@@ -73,59 +105,115 @@ def conv_flops_per_launch(m, H, W):
     return 2.0 * 64 * 64 * 9 * m * H * W
 
 
-def conv_bytes_per_launch(m, H, W):
+def conv_bytes_per_launch(m, H, W, elem=2):
     """Algorithmic HBM bytes of one 64->64 conv launch over m images: read and write the
-    fp16 64-channel activations once (the zero border, halo re-reads and weights are not
-    algorithmic)."""
-    return 2 * m * H * W * 64 * 2
+    64-channel activations once (the zero border, halo re-reads and weights are not
+    algorithmic); elem = 2 (fp16) or 4 (fp32 path)."""
+    return 2 * m * H * W * 64 * elem
 
 
-TRAFFIC_JSON = "profiles/r01/bench/traffic.json"
+TRAFFIC_JSON = "profiles/r02/bench/traffic.json"
 
 
-def measured_traffic(kernel, B):
+def measured_traffic(kernel, cfg_name, B):
     """HBM bytes per launch from this round's committed PMC passes of this bench command
     (tools/profile_bench.sh + tools/traffic_from_pmc.py), or None."""
-    try:
-        with open(os.path.join(REPO, TRAFFIC_JSON)) as f:
-            t = json.load(f)
-        return t["kernels"][kernel]["bytes"] if B == 256 else None
-    except (OSError, KeyError, ValueError):
-        return None
+    for path in (TRAFFIC_JSON, "profiles/r01/bench/traffic.json"):
+        try:
+            with open(os.path.join(REPO, path)) as f:
+                t = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if cfg_name == "metric" and B == 256 and kernel in t.get("kernels", {}):
+            return t["kernels"][kernel]["bytes"], path
+    return None, None
 
 
-def prox_bytes(B, C, H, W):
-    """Algorithmic HBM bytes per launch of the fused ours-A passes."""
+def prox_bytes(method, B, C, H, W):
+    """Algorithmic HBM bytes per launch of the fused passes (fp32 state)."""
     n = B * C * H * W
     npx = B * H * W
-    return {
-        "k1_primal_pre": 4 * n * 3 + 8 * npx,      # read x, y; write u32; write u16 (8 B/pixel)
-        "k2_dual": 4 * n * 6,                      # read x+, x, y, xobs, xtrue; write v
-        "k3_dual": 4 * n * 3,                      # read v, xobs; write y
-    }
+    if method == "A-Proposed":
+        return {"k1_primal_pre": 4 * n * 3 + 8 * npx,      # read x, y; write u32; write u16 (8 B/pixel)
+                "k2_dual": 4 * n * 6,                      # read x+, x, y, xobs, xtrue; write v
+                "k3_dual": 4 * n * 3}                      # read v, xobs; write y
+    if method == "B-Proposed":
+        return {"k1_primal_pre": 4 * n * 5 + 8 * npx,      # read x, y, s; write u32, w; write u16
+                "l1_select": 4 * n * 5,                    # |w| total + 3 radix levels + exact pass
+                "k2_dual": 4 * n * 9,                      # read x+, x, y, xobs, xtrue, s, w; write v, s+
+                "k3_dual": 4 * n * 3}
+    if method == "C-Proposed":
+        return {"k1_primal_pre": 4 * n * 3 + 8 * npx,
+                "k2_dual": 4 * n * 6}                      # read x+, x, y, xobs, xtrue; write y+ (GKL fused)
+    return {}
 
 
-def cpu_baseline(x_true, x_obs, h, budget_s, max_iter):
-    """Oracle restatement of test_iter (numpy FFT + torch-CPU conv, all host cores) on image 0."""
+def host_cpu_info():
+    """CPU model, logical CPUs, the CPUs this process may run on and the cgroup CPU quota."""
+    model = platform.processor() or "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    affinity = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()
+            if q != "max":
+                quota = max(1, int(round(int(q) / int(per))))
+    except (OSError, ValueError):
+        pass
+    usable = min(affinity, quota) if quota else affinity
+    return {"model": model, "logical_cpus": os.cpu_count(), "affinity": affinity, "cgroup_quota_cpus": quota,
+            "threads_used": usable}
+
+
+def cpu_baseline(cfg, x_true, x_obs, x_0, h, budget_s, max_iter):
+    """Oracle restatement of test_iter (numpy FFT / mask, sort-based l1, torch-CPU conv) on
+    image 0, with every CPU this process may use.  Returns (image-iters/s,
+    sample description, PSNR track, threads)."""
     import torch
     from oracle import pnp_oracle as O
     from pnppds.weights import resolve_weights
-    torch.set_num_threads(int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1))
-    den = O.OracleDenoiser(resolve_weights(ARCH, 3))
-    phi, adj = O.observation_operators("blur", h)
-    xo = x_obs.astype(np.float64)
-    O.test_iter(xo, xo, x_true, phi, adj, GAMMA1, GAMMA2, 1.0, ALPHA_N, 1.0, 15, 15, 0.1, SIGMA, 0.0, 300, den, 1,
-                "A-Proposed", 3, 0.8)                                            # warm-up
-    t = time.perf_counter()                                                      # size the sample
-    O.test_iter(xo, xo, x_true, phi, adj, GAMMA1, GAMMA2, 1.0, ALPHA_N, 1.0, 15, 15, 0.1, SIGMA, 0.0, 300, den, 2,
-                "A-Proposed", 3, 0.8)
-    per = (time.perf_counter() - t) / 2
-    n_total = int(min(max_iter, max(2, budget_s / per)))
-    t = time.perf_counter()
-    res = O.test_iter(xo, xo, x_true, phi, adj, GAMMA1, GAMMA2, 1.0, ALPHA_N, 1.0, 15, 15, 0.1, SIGMA, 0.0, 300,
-                      den, n_total, "A-Proposed", 3, 0.8)
-    el = time.perf_counter() - t
-    return n_total / el, n_total, res[3], torch.get_num_threads()
+    info = host_cpu_info()
+    torch.set_num_threads(info["threads_used"])
+    C = cfg["C"]
+    den = O.OracleDenoiser(resolve_weights(f"DnCNN_nobn_nch_{C}_nlev_0.01", C))
+    phi, adj = O.observation_operators(cfg["op"], h, cfg["r"])
+    sq = (lambda a: a[0]) if C == 1 else (lambda a: a)          # gray: the reference's (H, W) arrays
+    xo, x0, xt = sq(x_obs.astype(np.float64)), sq(x_0.astype(np.float64)), sq(x_true)
+
+    def run(n, m1=cfg["m1"], m2=cfg["m2"]):
+        t = time.perf_counter()
+        res = O.test_iter(x0, xo, xt, phi, adj, cfg["g1"], cfg["g2"], cfg["a_s"], cfg["a_n"], cfg["lam"], m1, m2,
+                          0.1, cfg["sigma"], cfg["sp"], POISSON_ALPHA, den, n, cfg["method"], C, cfg["r"])
+        return time.perf_counter() - t, res
+
+    if cfg["method"] == "comparisonB-2":
+        # one outer iteration costs a + m1 tx + m2 ts; at 1024^2 (about 2 s per CPU denoiser pass)
+        # m1 = 35 does not fit the budget, so tx / ts / a are timed at small m1, m2 and scaled.
+        t11, res = run(1, 1, 1)
+        t21, _ = run(1, 2, 1)
+        t12, _ = run(1, 1, 2)
+        tx, ts = max(t21 - t11, 0.0), max(t12 - t11, 0.0)
+        a = max(t11 - tx - ts, 0.0)
+        per = a + cfg["m1"] * tx + cfg["m2"] * ts
+        sample = (f"oracle comparisonB-2 on image 0: one outer iteration timed at (m1, m2) = (1, 1), (2, 1), (1, 2) "
+                  f"-> fixed {a:.2f} s + {tx:.2f} s per x-step + {ts:.3f} s per s-step, scaled to m1={cfg['m1']}, "
+                  f"m2={cfg['m2']}: {per:.1f} s per outer iteration")
+        return 1.0 / per, sample, None, info
+    run(1)                                                        # warm-up
+    t1, _ = run(2)
+    n_total = int(min(max_iter, max(2, budget_s / (t1 / 2))))
+    el, res = run(n_total)
+    sample = (f"oracle test_iter ({cfg['method']}, {cfg['op']}) on image 0, {n_total} iterations after a "
+              f"warm-up, wall clock")
+    return n_total / el, sample, res[3], info
 
 
 def main():
@@ -133,20 +221,29 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=256, help="images per GPU")
-    ap.add_argument("--size", type=int, default=256)
+    ap.add_argument("--config", default="metric", choices=sorted(CONFIGS))
+    ap.add_argument("--batch", type=int, default=0, help="images per GPU (0 = the config's)")
+    ap.add_argument("--size", type=int, default=0, help="image side (0 = the config's)")
+    ap.add_argument("--op", default="", choices=["", "blur", "Id", "random_sampling"],
+                    help="override the config's degradation operator (profiling the elementwise K1/K2)")
+    ap.add_argument("--precision", default="auto", choices=["auto", "fp16", "fp32"],
+                    help="denoiser operands: auto = the solver's policy (fp32 for the Poisson methods, "
+                         "fp16 otherwise; pnppds.iteration.FP32_METHODS)")
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU-baseline work")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile", type=int, default=1, help="HIP-event per-kernel timing in the timed region")
     ap.add_argument("--chunk", type=int, default=0, help="images per denoiser pass (0 = auto)")
-    ap.add_argument("--chunk-sweep", type=str, default="", help="e.g. 4,8,16,256: time each (stderr)")
-    ap.add_argument("--variant", type=int, default=0, help="body layers per launch: 0 = one (default), 1 = two fused")
-    ap.add_argument("--variant-sweep", type=str, default="", help="e.g. 0,1: interleaved A/B (stderr)")
-    ap.add_argument("--op", default="blur", choices=["blur", "Id", "random_sampling"],
-                    help="degradation operator (the metric's is blur; the others time the elementwise K1/K2)")
-    ap.add_argument("--ablate", type=int, default=0, help="profiling only (results wrong): 1 DMA, 2 stores, 4 MFMA")
+    ap.add_argument("--ablate", type=int, default=0,
+                    help="profiling build only (PNP_LIB_PATH=lib_prof/...; results wrong): 1 DMA, 2 stores, 4 MFMA")
     args = ap.parse_args()
 
+    cfg = dict(CONFIGS[args.config])
+    if args.batch:
+        cfg["B"] = args.batch
+    if args.size:
+        cfg["S"] = args.size
+    if args.op:
+        cfg["op"] = args.op
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -162,72 +259,48 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group(backend, init_method="env://")
     from pnppds import _lib
-    from pnppds.iteration import make_params
-    from pnppds.operators import load_blur_kernel
+    from pnppds.iteration import make_params, resolve_method, resolve_precision
+    from pnppds.operators import load_blur_kernel, sampling_keep_mask
     from pnppds.shard import max_over_ranks
     from pnppds.weights import resolve_weights
 
-    B, C, H, W = args.batch, 3, args.size, args.size
+    B, C, H, W = cfg["B"], cfg["C"], cfg["S"], cfg["S"]
     K, Wm = args.steps, args.warmup
+    arch = f"DnCNN_nobn_nch_{C}_nlev_0.01"
     ctx = _lib.Context(local)
-    ctx.set_denoiser(resolve_weights(ARCH, 3))
+    ctx.set_denoiser(resolve_weights(arch, C))
+    args.precision = resolve_precision(args.precision, resolve_method(cfg["method"]))
+    ctx.set_precision(args.precision)
     h = load_blur_kernel("blur_1")
-    if args.op == "blur":
+    if cfg["op"] == "blur":
         ctx.set_operator(_lib.OP_BLUR, h=h)
-    elif args.op == "Id":
+    elif cfg["op"] == "Id":
         ctx.set_operator(_lib.OP_ID)
     else:
-        from pnppds.operators import sampling_keep_mask
-        ctx.set_operator(_lib.OP_RANDOM_SAMPLING, mask=sampling_keep_mask(H, W, 0.8))
+        ctx.set_operator(_lib.OP_RANDOM_SAMPLING, mask=sampling_keep_mask(H, W, cfg["r"]))
 
     # ---- synthetic inputs, degraded on the device exactly as main.py:49-64 does ---------------
     t0 = time.perf_counter()
     x_true = synthetic_batch(B, C, H, W, seed=1000 * rank + 1)
     d_true = torch.from_numpy(x_true).cuda(local)
     d_obs = torch.empty_like(d_true)
-    ctx.degrade(_lib.pnp_degrade_params(SIGMA, 0.0, 300.0, 0, 1234), d_true.data_ptr(), B, C, H, W,
-                xobs=d_obs.data_ptr())           # blur_1 + 0.01 * np.random.seed(1234) randn
+    d_x0 = torch.empty_like(d_true)
+    ctx.degrade(_lib.pnp_degrade_params(cfg["sigma"], cfg["sp"], POISSON_ALPHA, 1 if cfg["poisson"] else 0, 1234),
+                d_true.data_ptr(), B, C, H, W, xobs=d_obs.data_ptr(), x0=d_x0.data_ptr())
     torch.cuda.synchronize()
     log(f"[rank {rank}] inputs ready in {time.perf_counter() - t0:.1f}s")
 
     cap = Wm + K
-    prm = make_params(GAMMA1, GAMMA2, 1.0, ALPHA_N, 1.0, 15, 15, 0.1, SIGMA, 0.0, 300, 0.8, True)
+    prm = make_params(cfg["g1"], cfg["g2"], cfg["a_s"], cfg["a_n"], cfg["lam"], cfg["m1"], cfg["m2"], 0.1,
+                      cfg["sigma"], cfg["sp"], POISSON_ALPHA, cfg["r"], True)
     ctx.set_denoise_chunk(args.chunk)
-    ctx.solver_setup(_lib.METHOD_A, prm, B, C, H, W, cap)
-    ctx.solver_load_device(d_obs.data_ptr(), d_obs.data_ptr(), d_true.data_ptr())   # x_0 = x_obs (main.py:62)
+    ctx.solver_setup(resolve_method(cfg["method"]), prm, B, C, H, W, cap)
+    ctx.solver_load_device(d_x0.data_ptr(), d_obs.data_ptr(), d_true.data_ptr())   # x_0 (main.py:62-64)
+    if args.ablate:
+        ctx.set_ablate(args.ablate)
     ctx.solver_iterate(Wm)
     ctx.synchronize()
     torch.cuda.synchronize()
-    for ch in [int(v) for v in args.chunk_sweep.split(",") if v]:
-        ctx.set_denoise_chunk(ch)
-        ctx.solver_iterate(1)
-        ctx.synchronize()
-        ts = time.perf_counter()
-        ctx.solver_iterate(3)
-        ctx.synchronize()
-        log(f"[sweep] chunk={ch}: {(time.perf_counter() - ts) / 3 * 1e3:.2f} ms/iter")
-    vs = [int(v) for v in args.variant_sweep.split(",") if v]
-    if vs:
-        res = {v: [] for v in vs}
-        for _ in range(3):                     # interleaved rounds in one process
-            for v in vs:
-                ctx.set_body_variant(v)
-                ctx.solver_iterate(1)
-                ctx.synchronize()
-                ts = time.perf_counter()
-                ctx.solver_iterate(2)
-                ctx.synchronize()
-                res[v].append((time.perf_counter() - ts) / 2 * 1e3)
-        for v in vs:
-            log(f"[variant] {v}: ms/iter median {sorted(res[v])[1]:.2f} min {min(res[v]):.2f}")
-    ctx.set_body_variant(args.variant)
-    if args.ablate:
-        ctx.set_ablate(args.ablate)
-    if args.chunk_sweep or vs:                 # restart the trajectory after the sweep
-        ctx.set_denoise_chunk(args.chunk)
-        ctx.solver_load_device(d_obs.data_ptr(), d_obs.data_ptr(), d_true.data_ptr())
-        ctx.solver_iterate(Wm)
-        ctx.synchronize()
 
     # ---- timed region ------------------------------------------------------------------------
     if args.profile:
@@ -248,61 +321,69 @@ def main():
 
     value = B * world * K / t_el
     if rank == 0:
+        metric = METRIC if args.config == "metric" and cfg["op"] == "blur" else \
+            f"PDS iters/sec ({args.config}: {cfg['method']} {cfg['op']}, {C}x{H}x{W}); PSNR Δ vs ref"
         line = {
-            "metric": METRIC, "value": round(value, 2), "unit": "image-iterations/s",
+            "metric": metric, "value": round(value, 2), "unit": "image-iterations/s",
             "n_gpus": world, "steps": K, "warmup": Wm,
             "ms_per_step": round(1e3 * t_el / K, 3), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "fp16-mfma/fp32-acc+state",
-            "data": "synthetic structured RGB images, x_obs = blur_1(x_true) + 0.01 randn of np.random.seed(1234) "
-                    "(main.py:49-64, generated on device); real "
-                    "DnCNN_nobn_nch_3_nlev_0.01 weights",
-            "config": {"workload": f"ours-A (A-Proposed) blur, batch={B}/GPU RGB {H}x{W}", "global_batch": B * world,
-                       "image": f"{C}x{H}x{W}", "deg_op": "blur_1" if args.op == "blur" else args.op,
-                       "method": "ours-A",
+            "vs_baseline": None,
+            "dtype": "fp16-mfma/fp32-acc+state" if args.precision == "fp16" else "fp32-mfma/fp32-state",
+            "data": f"synthetic structured images, x_obs from the device observation pipeline (main.py:49-64: "
+                    f"{cfg['op']}, sigma={cfg['sigma']}, sp={cfg['sp']}, poisson={cfg['poisson']}, "
+                    f"np.random.seed(1234) streams); real {arch} weights",
+            "config": {"workload": cfg["desc"].format(B=B, S=H), "config": args.config, "global_batch": B * world,
+                       "image": f"{C}x{H}x{W}", "deg_op": "blur_1" if cfg["op"] == "blur" else cfg["op"],
+                       "method": cfg["method"], "precision": args.precision,
                        "parallelism": f"dp{world} (independent image shards, no collective)"},
             "batch_iters_per_s": round(K / t_el, 3),
+            "build_id": _lib.build_id(),
         }
         if prof:
             kt = {k: round(v[0], 4) for k, v in prof.items()}
             line["kernel_ms"] = kt
-            fused = "conv_body2" in prof          # two 64->64 layers per launch (intermediate in LDS)
-            kname = "conv_body2" if fused else "conv_body"
-            body_ms = prof[kname][0]
-            m = images_per_launch(B, H, W, args.chunk)
-            nl = 2 if fused else 1
-            fl = nl * conv_flops_per_launch(m, H, W)
-            by = conv_bytes_per_launch(m, H, W)    # read + write the fp16 activations once per launch
-            gbs = by / (body_ms * 1e-3) / 1e9
-            tfl = fl / (body_ms * 1e-3) / 1e12
-            # per launch: 288 FLOP/B (one layer, below the 312 FLOP/B ridge: HBM roof) or 576 FLOP/B
-            # (two fused layers, above it: MFMA roof)
-            if fused:
-                line["roofline"] = {"kernel": "conv_body2 (two fused 64->64 3x3 layers, fp16 MFMA)", "bound": "mfma",
-                                    "achieved": round(tfl, 1), "peak": FP16_PEAK_TFLOPS, "unit": "TFLOP/s",
-                                    "frac": round(tfl / FP16_PEAK_TFLOPS, 4),
-                                    "traffic": measured_traffic(kname, B), "bytes_per_launch": by,
-                                    "flops_per_launch": fl, "hbm_gbs": round(gbs, 1),
-                                    "hbm_frac": round(gbs / HBM_PEAK_GBS, 4), "traffic_source": TRAFFIC_JSON}
-            else:
-                line["roofline"] = {"kernel": "conv_body (64->64 3x3 implicit GEMM, fp16 MFMA)", "bound": "hbm",
-                                    "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                    "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": measured_traffic(kname, B),
-                                    "bytes_per_launch": by, "flops_per_launch": fl,
-                                    "mfma_tflops": round(tfl, 1), "mfma_frac": round(tfl / FP16_PEAK_TFLOPS, 4),
-                                    "traffic_source": TRAFFIC_JSON}
-            pb = prox_bytes(B, C, H, W)
+            line["kernel_calls_per_step"] = {k: round(v[1] / K, 2) for k, v in prof.items()}
+            fp32 = args.precision == "fp32"
+            kname = "conv32_body" if fp32 else "conv_body"
+            if kname in prof:
+                body_ms = prof[kname][0]
+                m = images_per_launch(B, H, W, args.chunk, fp32)
+                fl = conv_flops_per_launch(m, H, W)
+                by = conv_bytes_per_launch(m, H, W, 4 if fp32 else 2)
+                gbs = by / (body_ms * 1e-3) / 1e9
+                tfl = fl / (body_ms * 1e-3) / 1e12
+                traffic, src = measured_traffic(kname, args.config, B) if not fp32 else (None, None)
+                if fp32:   # 144 FLOP/B on fp32 activations vs a 157.3 / 8 = 20 FLOP/B ridge: MFMA-bound
+                    line["roofline"] = {"kernel": "conv32_body (64->64 3x3, fp32 MFMA 32x32x2)", "bound": "mfma",
+                                        "achieved": round(tfl, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                                        "frac": round(tfl / FP32_PEAK_TFLOPS, 4), "traffic": None,
+                                        "bytes_per_launch": by, "flops_per_launch": fl, "hbm_gbs": round(gbs, 1)}
+                else:      # 288 FLOP/B, below the 2500 / 8 = 312 FLOP/B ridge: HBM roof
+                    line["roofline"] = {"kernel": "conv_body (64->64 3x3 implicit GEMM, fp16 MFMA)", "bound": "hbm",
+                                        "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                        "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
+                                        "bytes_per_launch": by, "flops_per_launch": fl,
+                                        "mfma_tflops": round(tfl, 1), "mfma_frac": round(tfl / FP16_PEAK_TFLOPS, 4),
+                                        "traffic_source": src}
+            pb = prox_bytes(cfg["method"], B, C, H, W)
             line["prox_hbm"] = {k: {"GB/s": round(pb[k] / (prof[k][0] * 1e-3) / 1e9, 1),
                                     "frac": round(pb[k] / (prof[k][0] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
                                 for k in pb if k in prof}
         line["psnr_img0_db"] = [round(float(psnr_hist[0, 0]), 4), round(float(psnr_hist[0, cap - 1]), 4)]
         line["ssim_img0"] = [round(float(ssim_hist[0, 0]), 5), round(float(ssim_hist[0, cap - 1]), 5)]
-        if world == 1 and not args.no_cpu_baseline and args.op == "blur":
-            rate, n_cpu, ps_cpu, thr = cpu_baseline(x_true[0], d_obs[0].cpu().numpy(), h, args.cpu_budget, cap)
-            line["cpu_baseline"] = {"value": round(rate, 3), "unit": "image-iterations/s", "cores": thr,
-                                    "kind": "port",
-                                    "sample": f"oracle test_iter (numpy FFT blur + torch-CPU conv), image 0, "
-                                              f"{n_cpu} iterations after 1 warm-up"}
-            line["psnr_delta_db_vs_oracle"] = round(float(np.max(np.abs(ps_cpu - psnr_hist[0, :n_cpu]))), 5)
+        if world == 1 and not args.no_cpu_baseline:
+            rate, sample, ps_cpu, info = cpu_baseline(cfg, x_true[0:1][0], d_obs[0].cpu().numpy(),
+                                                      d_x0[0].cpu().numpy(), h, args.cpu_budget, cap)
+            line["cpu_baseline"] = {"value": round(rate, 4), "unit": "image-iterations/s",
+                                    "cores": info["threads_used"], "kind": "port", "sample": sample,
+                                    "cpu_model": info["model"], "logical_cpus": info["logical_cpus"],
+                                    "cpus_in_affinity": info["affinity"],
+                                    "cgroup_quota_cpus": info["cgroup_quota_cpus"],
+                                    "batch_rate_extrapolated": f"{rate:.4g} image-iterations/s for any batch "
+                                                               f"(the reference runs images one at a time, main.py:36)"}
+            if ps_cpu is not None:
+                n_cpu = len(ps_cpu)
+                line["psnr_delta_db_vs_oracle"] = round(float(np.max(np.abs(ps_cpu - psnr_hist[0, :n_cpu]))), 5)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define PNP_ABI_VERSION 2
+#define PNP_ABI_VERSION 3
 
 typedef struct pnp_ctx pnp_ctx;
 
@@ -80,7 +80,10 @@ enum pnp_operator_kind {
 enum pnp_activation { PNP_ACT_LEAKY_RELU = 0 /* slope 0.01 */, PNP_ACT_RELU = 1 };
 
 enum pnp_precision {
-  PNP_PREC_FP16 = 0  /* fp16 MFMA operands, fp32 accumulation (default)            */
+  PNP_PREC_FP16 = 0, /* fp16 MFMA operands, fp32 accumulation (default)            */
+  PNP_PREC_FP32 = 1  /* fp32 operands and accumulation (v_mfma_f32_32x32x2_f32): the
+                        reference denoiser's own precision (models/denoiser.py:37), the
+                        parity fallback; about 1/10 of the fp16 path's throughput     */
 };
 
 /* Scalar parameters of iteration.test_iter (iteration.py:10), same names/meaning. */
@@ -99,6 +102,9 @@ typedef struct pnp_params {
 
 /* ---- library / context -------------------------------------------------------- */
 int pnp_abi_version(void);
+/* SHA-256 prefix (16 hex digits) of the library's sources (pnp-pds_amd/Makefile HASHSRC),
+ * baked in at build time: lets a caller detect a library built from other sources.    */
+const char* pnp_build_id(void);
 int pnp_device_count(int* count);
 int pnp_create(int device, pnp_ctx** out);
 int pnp_destroy(pnp_ctx* ctx);
@@ -113,20 +119,14 @@ int pnp_synchronize(pnp_ctx* ctx);
  * clamp_io: 1 => clamp input and output to [0,1] (denoiser.py:40,42).            */
 int pnp_set_denoiser(pnp_ctx* ctx, int channels, int depth, int width, const float* params,
                      size_t n_params, int activation, int residual_sign, int clamp_io);
+/* Denoiser operand precision (pnp_precision); applies to every later denoiser call. */
 int pnp_set_precision(pnp_ctx* ctx, int precision);
 
 /* Performance knobs (no effect on results).
- * PNP_TUNE_DENOISE_CHUNK: images per denoiser pass (0 = auto: the activation ping-pong
- * pair of a pass is sized to stay resident in the 256 MB Infinity Cache).             */
+ * PNP_TUNE_DENOISE_CHUNK: images per denoiser pass (0 = auto: the whole batch, unless its
+ * activation ping-pong pair would exceed 8 GB (fp16) / 16 GB (fp32)).                */
 enum pnp_tuning_key {
-  PNP_TUNE_DENOISE_CHUNK = 1,
-  PNP_TUNE_BODY_VARIANT = 2,  /* 64->64 body layers: 1 = two layers per launch, the intermediate
-                                 kept in LDS; 0 = one layer per launch (default); 2 = one
-                                 layer, staggered epilogue; 3 = one layer on 16x16x32 MFMAs;
-                                 4 = one layer as a row-wise Winograd F(2,3) (3 and 4 round
-                                 differently, within the fp16 tolerance) */
-  PNP_TUNE_ABLATE = 3         /* profiling only, results are wrong: one-layer body kernel with parts
-                                 skipped (1 = halo DMA, 2 = output stores, 4 = MFMA K-loop) */
+  PNP_TUNE_DENOISE_CHUNK = 1
 };
 int pnp_set_tuning(pnp_ctx* ctx, int key, int value);
 

@@ -48,13 +48,11 @@ struct pnp_ctx {
   // denoiser
   int den_C = 0, den_depth = 0, den_act = 0, den_residual = 1, den_clamp = 1;
   int den_chunk = 0;   // images per denoiser pass; 0 = auto
-  int body_fused = 0;     // 1: body layers two per launch (conv_body2), 0: one per launch (conv_body_v3)
-  int body_stagger = 0;   // PNP_TUNE_BODY_VARIANT 2: staggered epilogue in conv_body_v3
-  int body_mf16 = 0;      // PNP_TUNE_BODY_VARIANT 3: conv_body_v4 (16x16x32 MFMAs)
-  int body_wg = 0;        // PNP_TUNE_BODY_VARIANT 4: conv_body_wg (row Winograd F(2,3))
-  int ablate = 0;         // profiling only (PNP_TUNE_ABLATE): parts of conv_body_v3 skipped, results wrong
+  int ablate = 0;         // PNP_PROFILING build only: parts of conv_body_v3 skipped, results wrong
   bool den_ready = false;
-  DevBuf head_w, head_b, body_w, body_w16, body_wwg, body_b, tail_w, tail_b;
+  int prec = PNP_PREC_FP16;   // pnp_set_precision: fp16 MFMA operands (conv.hip) or fp32 (conv32.hip)
+  DevBuf head_w, head_b, body_w, body_b, tail_w, tail_b;
+  DevBuf head_w32, body_w32, tail_w32;   // fp32 MFMA fragments (PNP_PREC_FP32)
 
   // operator
   int op_kind = PNP_OP_ID;
@@ -79,6 +77,7 @@ struct pnp_ctx {
 
   // scratch for single ops
   DevBuf scr_u32, scr_u16, scr_act[2], scr_part, scr_theta;
+  DevBuf act32[2];   // fp32 hidden activations (PNP_PREC_FP32), shared by the solver and pnp_op_denoise
 
   // profiling
   bool prof = false;
@@ -248,10 +247,57 @@ int denoise_chunk(pnp_ctx* ctx, int B, int H, int W) {
   return std::max(1, std::min(m, B));
 }
 
+// fp32-operand forward (PNP_PREC_FP32): u32 (NCHW, clamped input) -> xout, conv32.hip.
+void run_denoiser32(pnp_ctx* ctx, const float* u32, float* xout, int B, int H, int W, hipStream_t st) {
+  const double per_img = 2.0 * act32_bytes(1, H, W);
+  const int m = ctx->den_chunk > 0 ? std::min(ctx->den_chunk, B)
+                                   : std::max(1, std::min((int)std::floor(16e9 / per_img), B));
+  for (int i = 0; i < 2; ++i) {                 // one-pixel zero border, zeroed once per geometry
+    const long long geom = ((long long)m << 40) ^ ((long long)H << 20) ^ (long long)W;
+    ensure(ctx, ctx->act32[i], act32_bytes(m, H, W));
+    if (ctx->act32[i].geom != geom) {
+      HIPCHK(ctx, hipMemsetAsync(ctx->act32[i].p, 0, act32_bytes(m, H, W), st));
+      ctx->act32[i].geom = geom;
+    }
+  }
+  const int C = ctx->den_C, nbody = ctx->den_depth - 2;
+  const size_t wb = conv32_weight_floats(1);
+  for (int b0 = 0; b0 < B; b0 += m) {
+    const int mb = std::min(m, B - b0);
+    ConvShape s = make_conv_shape(mb, H, W);
+    const float* xin = u32 + (size_t)b0 * C * H * W;
+    float* xo = xout + (size_t)b0 * C * H * W;
+    {
+      ProfScope ps(ctx, "conv32_head", st);
+      launch_conv32(0, xin, P<float>(ctx->act32[0]), nullptr, P<float>(ctx->head_w32), P<float>(ctx->head_b), s, C,
+                    ctx->den_act, 1, 0, ctx->num_cus, st);
+      check_launch(ctx, "conv32_head");
+    }
+    int cur = 0;
+    for (int l = 0; l < nbody; ++l, cur ^= 1) {
+      ProfScope ps(ctx, "conv32_body", st);
+      launch_conv32(1, P<float>(ctx->act32[cur]), P<float>(ctx->act32[cur ^ 1]), nullptr,
+                    P<float>(ctx->body_w32) + (size_t)l * wb, P<float>(ctx->body_b) + l * kWidth, s, C, ctx->den_act,
+                    1, 0, ctx->num_cus, st);
+      check_launch(ctx, "conv32_body");
+    }
+    {
+      ProfScope ps(ctx, "conv32_tail", st);
+      launch_conv32(2, P<float>(ctx->act32[cur]), xo, xin, P<float>(ctx->tail_w32), P<float>(ctx->tail_b), s, C,
+                    ctx->den_act, ctx->den_residual, ctx->den_clamp, ctx->num_cus, st);
+      check_launch(ctx, "conv32_tail");
+    }
+  }
+}
+
 // Denoiser forward over B images: u16 (padded NHWC4) + u32 (NCHW, residual input) -> xout.
 void run_denoiser(pnp_ctx* ctx, const half_t* u16, const float* u32, float* xout, DevBuf (&act)[2], int B, int H,
                   int W, hipStream_t st) {
   if (!ctx->den_ready) fail(ctx, PNP_E_STATE, "denoiser not set (pnp_set_denoiser)");
+  if (ctx->prec == PNP_PREC_FP32) {
+    run_denoiser32(ctx, u32, xout, B, H, W, st);
+    return;
+  }
   const int m = denoise_chunk(ctx, B, H, W);
   ensure_act(ctx, act, m, H, W, st);
   const int C = ctx->den_C;
@@ -272,28 +318,10 @@ void run_denoiser(pnp_ctx* ctx, const half_t* u16, const float* u32, float* xout
     for (int l = 0; l < nbody;) {
       const char* wl = (const char*)ctx->body_w.p + (size_t)l * kBodyWBytes;
       const float* bl = P<float>(ctx->body_b) + l * kWidth;
-      if (ctx->body_fused && l + 1 < nbody) {      // layers l+1, l+2 of simple_CNN in one launch
-        ProfScope ps(ctx, "conv_body2", st);
-        launch_conv_body2(P<half_t>(act[cur]), P<half_t>(act[cur ^ 1]), wl, bl, wl + kBodyWBytes, bl + kWidth, s,
-                          ctx->den_act, ctx->num_cus, st);
-        check_launch(ctx, "conv_body2");
-        l += 2;
-      } else if (ctx->body_wg && !ctx->ablate) {
-        ProfScope ps(ctx, "conv_body", st);
-        launch_conv_body_wg(P<half_t>(act[cur]), P<half_t>(act[cur ^ 1]),
-                            (const char*)ctx->body_wwg.p + (size_t)l * kBodyWgBytes, bl, s, ctx->den_act, ctx->num_cus, st);
-        check_launch(ctx, "conv_body");
-        l += 1;
-      } else if (ctx->body_mf16 && !ctx->ablate) {
-        ProfScope ps(ctx, "conv_body", st);
-        launch_conv_body16(P<half_t>(act[cur]), P<half_t>(act[cur ^ 1]),
-                           (const char*)ctx->body_w16.p + (size_t)l * kBodyWBytes, bl, s, ctx->den_act, ctx->num_cus, st);
-        check_launch(ctx, "conv_body");
-        l += 1;
-      } else {
+      {
         ProfScope ps(ctx, "conv_body", st);
         launch_conv_body(P<half_t>(act[cur]), P<half_t>(act[cur ^ 1]), wl, bl, s, ctx->den_act, ctx->num_cus,
-                         ctx->ablate ? ctx->ablate : (ctx->body_stagger ? 8 : 0), st);
+                         ctx->ablate, st);
         check_launch(ctx, "conv_body");
         l += 1;
       }
@@ -597,6 +625,10 @@ void solver_setup(pnp_ctx* ctx, int method, const pnp_params* params, int B, int
   if (ctx->op_kind == PNP_OP_BLUR && (ctx->op_R > H || ctx->op_R > W))
     fail(ctx, PNP_E_ARG, "blur kernel radius %d larger than the image", ctx->op_R);
   if (params->gamma2 == 0.0) fail(ctx, PNP_E_ARG, "gamma2 must be non-zero");
+  if ((size_t)C * H * W >= kMaxL1Elems && (method == PNP_METHOD_B || method == PNP_METHOD_ADMM_B2 ||
+                                            method == PNP_METHOD_B_HTV || method == PNP_METHOD_B_RED ||
+                                            method == PNP_METHOD_B_PNPFBS))
+    fail(ctx, PNP_E_UNSUPPORTED, "l1-ball methods need C*H*W < 2^29 per image");
   ctx->method = method;
   ctx->prm = *params;
   ctx->B = B; ctx->C = C; ctx->H = H; ctx->W = W;
@@ -630,6 +662,9 @@ void solver_setup(pnp_ctx* ctx, int method, const pnp_params* params, int B, int
 }
 
 void solver_reset_state(pnp_ctx* ctx) {
+  check_operator_shape(ctx, ctx->H, ctx->W);
+  if (ctx->op_kind == PNP_OP_BLUR && (ctx->op_R > ctx->H || ctx->op_R > ctx->W))
+    fail(ctx, PNP_E_ARG, "blur kernel radius %d larger than the image", ctx->op_R);
   const size_t fb = (size_t)ctx->B * ctx->C * ctx->H * ctx->W * sizeof(float);
   HIPCHK(ctx, hipMemsetAsync(ctx->y.p, 0, fb, ctx->stream));          // iteration.py:24
   HIPCHK(ctx, hipMemsetAsync(ctx->s.p, 0, fb, ctx->stream));          // iteration.py:27
@@ -682,6 +717,11 @@ extern "C" {
 
 int pnp_abi_version(void) { return PNP_ABI_VERSION; }
 
+#ifndef PNP_SRC_HASH
+#define PNP_SRC_HASH "unknown"
+#endif
+const char* pnp_build_id(void) { return PNP_SRC_HASH; }
+
 int pnp_device_count(int* count) {
   return guarded(nullptr, [&] {
     if (!count) fail(nullptr, PNP_E_ARG, "count is NULL");
@@ -713,6 +753,7 @@ int pnp_create(int device, pnp_ctx** out) {
       ctx->num_cus = prop.multiProcessorCount;
       HIPCHK(ctx, hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
       HIPCHK(ctx, conv_kernels_init());
+      HIPCHK(ctx, conv32_kernels_init());
     } catch (const PnpError&) {
       g_thread_err = ctx->err;
       delete ctx;
@@ -726,14 +767,15 @@ int pnp_destroy(pnp_ctx* ctx) {
   if (!ctx) return PNP_OK;
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-  DevBuf* bufs[] = {&ctx->head_w, &ctx->head_b, &ctx->body_w, &ctx->body_w16, &ctx->body_wwg, &ctx->body_b, &ctx->tail_w, &ctx->tail_b,
+  DevBuf* bufs[] = {&ctx->head_w, &ctx->head_b, &ctx->body_w, &ctx->body_b, &ctx->tail_w, &ctx->tail_b,
                     &ctx->taps_fwd, &ctx->taps_adj, &ctx->mask, &ctx->x[0], &ctx->x[1], &ctx->y, &ctx->s,
                     &ctx->w, &ctx->xobs, &ctx->xtrue, &ctx->u32, &ctx->u16, &ctx->act[0], &ctx->act[1],
                     &ctx->partials, &ctx->metrics, &ctx->theta, &ctx->scr_u32, &ctx->scr_u16,
                     &ctx->scr_act[0], &ctx->scr_act[1], &ctx->scr_part, &ctx->scr_theta,
                     &ctx->z, &ctx->p, &ctx->t, &ctx->dense_fwd, &ctx->dense_adj, &ctx->ssim_scr,
                     &ctx->taps64, &ctx->y1, &ctx->d, &ctx->c1, &ctx->dg_words, &ctx->dg_flag, &ctx->dg_rank, &ctx->dg_scan, &ctx->dg_noise,
-                    &ctx->dg_img, &ctx->dg_draws, &ctx->dg_first, &ctx->dg_status};
+                    &ctx->dg_img, &ctx->dg_draws, &ctx->dg_first, &ctx->dg_status,
+                    &ctx->head_w32, &ctx->body_w32, &ctx->tail_w32, &ctx->act32[0], &ctx->act32[1]};
   for (DevBuf* b : bufs) release(*b);
   for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -756,21 +798,12 @@ int pnp_set_tuning(pnp_ctx* ctx, int key, int value) {
       ctx->den_chunk = value;
       return;
     }
-    if (key == PNP_TUNE_BODY_VARIANT) {
-      if (value < 0 || value > 4)
-        fail(ctx, PNP_E_ARG,
-             "body variant must be 0 (one layer/launch), 1 (two), 2 (one, staggered), 3 (one, 16x16x32) or 4 (one, "
-             "row Winograd F(2,3))");
-      ctx->body_fused = value == 1;
-      ctx->body_stagger = value == 2;
-      ctx->body_mf16 = value == 3;
-      ctx->body_wg = value == 4;
-      return;
-    }
-    if (key == PNP_TUNE_ABLATE) {          // profiling only
+#ifdef PNP_PROFILING
+    if (key == kTuneAblate) {              // profiling build only
       ctx->ablate = value;
       return;
     }
+#endif
     fail(ctx, PNP_E_UNSUPPORTED, "tuning key %d", key);
   });
 }
@@ -778,7 +811,9 @@ int pnp_set_tuning(pnp_ctx* ctx, int key, int value) {
 int pnp_set_precision(pnp_ctx* ctx, int precision) {
   if (!ctx) return PNP_E_ARG;
   return guarded(ctx, [&] {
-    if (precision != PNP_PREC_FP16) fail(ctx, PNP_E_UNSUPPORTED, "precision %d not supported", precision);
+    if (precision != PNP_PREC_FP16 && precision != PNP_PREC_FP32)
+      fail(ctx, PNP_E_UNSUPPORTED, "precision %d not supported", precision);
+    ctx->prec = precision;
   });
 }
 
@@ -799,33 +834,42 @@ int pnp_set_denoiser(pnp_ctx* ctx, int channels, int depth, int width, const flo
       fail(ctx, PNP_E_ARG, "expected %zu parameters for C=%d depth=%d, got %zu", expect, channels, depth, n_params);
     const float* p = params;
     std::vector<uint16_t> hw(kHeadWBytes / 2), bw((size_t)(depth - 2) * kBodyWBytes / 2), tw(kTailWBytes / 2);
-    std::vector<uint16_t> bw16(bw.size()), bwg((size_t)(depth - 2) * kBodyWgBytes / 2);
     std::vector<float> hb(kWidth), bb((size_t)(depth - 2) * kWidth), tb(kMaxC, 0.f);
     pack_head_weights(p, channels, hw.data());
     std::memcpy(hb.data(), p + kWidth * channels * 9, kWidth * sizeof(float));
     p += n_head;
     for (int l = 0; l < depth - 2; ++l) {
       pack_body_weights(p, bw.data() + (size_t)l * kBodyWBytes / 2);
-      pack_body_weights16(p, bw16.data() + (size_t)l * kBodyWBytes / 2);
-      pack_body_weights_wg(p, bwg.data() + (size_t)l * kBodyWgBytes / 2);
       std::memcpy(bb.data() + (size_t)l * kWidth, p + kWidth * kWidth * 9, kWidth * sizeof(float));
       p += n_body;
     }
     pack_tail_weights(p, channels, tw.data());
+    {                                        // fp32 fragments for PNP_PREC_FP32
+      std::vector<float> h32(conv32_weight_floats(0)), b32(conv32_weight_floats(1) * (depth - 2)),
+          t32(conv32_weight_floats(2));
+      const float* q = params;
+      pack_conv32_weights(q, 0, channels, kWidth, h32.data());
+      q += n_head;
+      for (int l = 0; l < depth - 2; ++l, q += n_body)
+        pack_conv32_weights(q, 1, kWidth, kWidth, b32.data() + (size_t)l * conv32_weight_floats(1));
+      pack_conv32_weights(q, 2, kWidth, channels, t32.data());
+      ensure(ctx, ctx->head_w32, h32.size() * 4);
+      ensure(ctx, ctx->body_w32, b32.size() * 4);
+      ensure(ctx, ctx->tail_w32, t32.size() * 4);
+      HIPCHK(ctx, hipMemcpy(ctx->head_w32.p, h32.data(), h32.size() * 4, hipMemcpyHostToDevice));
+      HIPCHK(ctx, hipMemcpy(ctx->body_w32.p, b32.data(), b32.size() * 4, hipMemcpyHostToDevice));
+      HIPCHK(ctx, hipMemcpy(ctx->tail_w32.p, t32.data(), t32.size() * 4, hipMemcpyHostToDevice));
+    }
     std::memcpy(tb.data(), p + channels * kWidth * 9, channels * sizeof(float));
     ensure(ctx, ctx->head_w, hw.size() * 2);
     ensure(ctx, ctx->head_b, hb.size() * 4);
     ensure(ctx, ctx->body_w, bw.size() * 2);
-    ensure(ctx, ctx->body_w16, bw16.size() * 2);
-    ensure(ctx, ctx->body_wwg, bwg.size() * 2);
     ensure(ctx, ctx->body_b, bb.size() * 4);
     ensure(ctx, ctx->tail_w, tw.size() * 2);
     ensure(ctx, ctx->tail_b, tb.size() * 4);
     HIPCHK(ctx, hipMemcpy(ctx->head_w.p, hw.data(), hw.size() * 2, hipMemcpyHostToDevice));
     HIPCHK(ctx, hipMemcpy(ctx->head_b.p, hb.data(), hb.size() * 4, hipMemcpyHostToDevice));
     HIPCHK(ctx, hipMemcpy(ctx->body_w.p, bw.data(), bw.size() * 2, hipMemcpyHostToDevice));
-    HIPCHK(ctx, hipMemcpy(ctx->body_w16.p, bw16.data(), bw16.size() * 2, hipMemcpyHostToDevice));
-    HIPCHK(ctx, hipMemcpy(ctx->body_wwg.p, bwg.data(), bwg.size() * 2, hipMemcpyHostToDevice));
     HIPCHK(ctx, hipMemcpy(ctx->body_b.p, bb.data(), bb.size() * 4, hipMemcpyHostToDevice));
     HIPCHK(ctx, hipMemcpy(ctx->tail_w.p, tw.data(), tw.size() * 2, hipMemcpyHostToDevice));
     HIPCHK(ctx, hipMemcpy(ctx->tail_b.p, tb.data(), tb.size() * 4, hipMemcpyHostToDevice));
@@ -842,6 +886,9 @@ int pnp_set_operator(pnp_ctx* ctx, int kind, const double* h, int kh, int kw, co
                      int W) {
   if (!ctx) return PNP_E_ARG;
   return guarded(ctx, [&] {
+    // the loaded solver state depends on the operator (the Poisson-ADMM c1 = Phi^T 1 and the
+    // shape checks of solver_setup): a new operator needs pnp_solver_load / pnp_run again
+    ctx->loaded = false;
     if (kind == PNP_OP_ID) {
       ctx->op_kind = kind;
       return;
@@ -1087,6 +1134,8 @@ int pnp_op_proj_l1_ball(pnp_ctx* ctx, const float* x, float* out, int B, int64_t
   if (!ctx) return PNP_E_ARG;
   return guarded(ctx, [&] {
     if (!x || !out || B < 1 || n < 1) fail(ctx, PNP_E_ARG, "bad arguments");
+    if ((size_t)n >= kMaxL1Elems) fail(ctx, PNP_E_UNSUPPORTED, "l1-ball projection of %lld >= 2^29 elements per image",
+                                      (long long)n);
     ensure(ctx, ctx->scr_theta, (size_t)B * sizeof(float));
     const double eta = alpha_s * (double)n * sp_nl * r * 0.5;    // operators.py:96
     hipStream_t st = pick_stream(ctx, stream);

@@ -1,0 +1,211 @@
+// fp32-operand denoiser (PNP_PREC_FP32): the parity fallback of SURVEY.md §7 hard part 2.
+//
+// Reference: models/denoiser.py:34-46 runs simple_CNN (basic_models.py:25-38) in fp32;
+// KAIR DnCNN (network_dncnn.py:42-77) likewise.  The default path (conv.hip) rounds the
+// MFMA operands to fp16; this one keeps every operand fp32 on v_mfma_f32_32x32x2_f32,
+// which is an exact fp32 FMA chain (MI355X_MICROARCH.md, Matrix cores), at the fp32
+// matrix rate (157 TF, 1/16 of fp16).
+//
+// Activations: fp32 [B][H+2][W+2][64] ("padded NHWC64", 256 B per pixel, one-pixel zero
+// border).  Head input: the fp32 NCHW u32 image K1 writes (clamped denoiser input), read
+// with bounds checks.  Tail output: x+ in fp32 NCHW, with the residual (+x / x - n) and clamp.
+//
+// One kernel template for the three layer kinds.  Tile: 8 output rows x 32 columns, all
+// output channels; 4 waves, wave w owns tile rows 2w and 2w+1 (two 32-pixel N-tiles) and
+// every 32-channel M-tile.  The 10 x 34 input halo is staged in LDS with a pixel pitch of
+// CIN + 1 floats, so the 32 lanes of a ds_read_b32 (32 consecutive pixels, one channel)
+// hit 32 distinct banks.  The A fragments (weights, [k-step][M-tile][lane] fp32, 147 KB per
+// body layer, L2-resident) are loaded per tap, one tap ahead of the MFMAs that use them.
+// GEMM view per tap: K = CIN input channels in steps of 2 (one MFMA K-step).
+#include "kernels.h"
+
+namespace pnp {
+
+constexpr int kC32Pitch64 = kWidth + 1;   // LDS floats per halo pixel (64-channel input)
+constexpr int kC32Pitch4 = kMaxC + 1;     // (head: C <= 4 channels)
+constexpr int kC32Lds = kHaloPix * kC32Pitch64 * 4;   // 88400 B
+
+template <int MODE>   // 0 = head (C -> 64), 1 = body (64 -> 64), 2 = tail (64 -> C)
+struct C32Traits {
+  static constexpr int CIN = MODE == 0 ? kMaxC : kWidth;
+  static constexpr int PITCH = CIN + 1;
+  static constexpr int CP = CIN / 2;            // MFMA K-steps per tap
+  static constexpr int NM = MODE == 2 ? 1 : 2;  // 32-channel M-tiles
+  static constexpr int KS = 9 * CP;             // K-steps per layer
+};
+
+size_t conv32_weight_floats(int mode) {
+  return mode == 0 ? (size_t)C32Traits<0>::KS * C32Traits<0>::NM * 64
+       : mode == 1 ? (size_t)C32Traits<1>::KS * C32Traits<1>::NM * 64
+                   : (size_t)C32Traits<2>::KS * C32Traits<2>::NM * 64;
+}
+
+// PyTorch layout W[cout][cin][3][3] -> [ks][m][lane]: lane l holds A[row l&31][k l>>5] of
+// M-tile m at k-step ks = tap * CP + cp, i.e. input channel 2cp + (l>>5) of tap ks / CP.  Row i
+// is output channel 32m + mfma32_row_to_channel(i) (64-channel outputs: accumulator register r
+// of lane-half h = channel 16h + r) or channel i (tail: the C rows are registers 0..C-1 of
+// lane-half 0); rows and input channels past the layer's are zero.
+void pack_conv32_weights(const float* W, int mode, int cin, int cout, float* out) {
+  const int CP = mode == 0 ? kMaxC / 2 : kWidth / 2, NM = mode == 2 ? 1 : 2;
+  for (int ks = 0; ks < 9 * CP; ++ks) {
+    const int tap = ks / CP, cp = ks % CP;
+    for (int m = 0; m < NM; ++m)
+      for (int l = 0; l < 64; ++l) {
+        const int i = l & 31, ci = 2 * cp + (l >> 5);
+        const int co = mode == 2 ? i : 32 * m + mfma32_row_to_channel(i);
+        float v = 0.f;
+        if (co < cout && ci < cin) v = W[((size_t)co * cin + ci) * 9 + tap];
+        out[((size_t)ks * NM + m) * 64 + l] = v;
+      }
+  }
+}
+
+template <int MODE, int ACT>
+__global__ __launch_bounds__(256, 1) void conv32_kernel(const float* __restrict__ in, float* __restrict__ out,
+                                                        const float* __restrict__ xin,
+                                                        const float* __restrict__ wpk,
+                                                        const float* __restrict__ bias, ConvShape s, int C,
+                                                        int residual_sign, int clamp_out) {
+  using T = C32Traits<MODE>;
+  extern __shared__ float hl[];            // [kHaloPix][PITCH]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int col = lane & 31, kk = lane >> 5;
+  const int Hp = s.H + 2, Wp = s.W + 2;    // fp32 activations: one-pixel border
+  float bias_r[T::NM][16];
+#pragma unroll
+  for (int m = 0; m < T::NM; ++m)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int co = MODE == 2 ? r : 32 * m + 16 * kk + r;
+      bias_r[m][r] = (MODE == 2 ? (co < C && kk == 0) : true) ? bias[co] : 0.f;
+    }
+
+  for (int t = blockIdx.x; t < s.tiles; t += gridDim.x) {
+    int b, ty0, tx0;
+    {
+      const int per_img = s.tiles_x * s.tiles_y;
+      b = t / per_img;
+      const int r = t - b * per_img, ty = r / s.tiles_x;
+      ty0 = ty * kTileH;
+      tx0 = (r - ty * s.tiles_x) * kTileW;
+    }
+    __syncthreads();                       // previous tile's readers are done with the halo
+    if (MODE == 0) {                       // gather C channels of the NCHW input, zero outside
+      for (int i = tid; i < kHaloPix * kMaxC; i += 256) {
+        const int p = i / kMaxC, c = i - p * kMaxC;
+        const int pr = p / kHaloW, pc = p - pr * kHaloW;
+        const int y = ty0 - 1 + pr, x = tx0 - 1 + pc;
+        float v = 0.f;
+        if (c < C && y >= 0 && y < s.H && x >= 0 && x < s.W) v = in[(((size_t)b * C + c) * s.H + y) * s.W + x];
+        hl[p * T::PITCH + c] = v;
+      }
+    } else {                               // padded NHWC64: 16 float4 per pixel
+      for (int i = tid; i < kHaloPix * 16; i += 256) {
+        const int p = i >> 4, q = i & 15;
+        const int pr = p / kHaloW, pc = p - pr * kHaloW;
+        const int yp = ty0 + pr, xp = tx0 + pc;   // padded coordinates of the halo origin (ty0 - 1, tx0 - 1)
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (yp < Hp && xp < Wp) v = *reinterpret_cast<const float4*>(in + (((size_t)b * Hp + yp) * Wp + xp) * kWidth + 4 * q);
+        float* d = hl + p * T::PITCH + 4 * q;
+        d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+      }
+    }
+    __syncthreads();
+
+    floatx16 acc[T::NM][2];
+#pragma unroll
+    for (int m = 0; m < T::NM; ++m) acc[m][0] = acc[m][1] = floatx16{};
+    float wc[T::CP * T::NM], wn[T::CP * T::NM];
+#pragma unroll
+    for (int j = 0; j < T::CP * T::NM; ++j) wc[j] = wpk[j * 64 + lane];
+    for (int tap = 0; tap < 9; ++tap) {
+      if (tap + 1 < 9) {                  // next tap's A fragments, in flight during this tap
+#pragma unroll
+        for (int j = 0; j < T::CP * T::NM; ++j) wn[j] = wpk[((tap + 1) * T::CP * T::NM + j) * 64 + lane];
+      }
+      const int dy = tap / 3, dx = tap - 3 * dy;
+      const float* h0 = hl + ((2 * wave + dy) * kHaloW + col + dx) * T::PITCH + kk;
+      const float* h1 = h0 + kHaloW * T::PITCH;
+#pragma unroll
+      for (int cp = 0; cp < T::CP; ++cp) {
+        const float b0 = h0[2 * cp], b1 = h1[2 * cp];
+#pragma unroll
+        for (int m = 0; m < T::NM; ++m) {
+          acc[m][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(wc[cp * T::NM + m], b0, acc[m][0], 0, 0, 0);
+          acc[m][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(wc[cp * T::NM + m], b1, acc[m][1], 0, 0, 0);
+        }
+      }
+      if (tap + 1 < 9) {
+#pragma unroll
+        for (int j = 0; j < T::CP * T::NM; ++j) wc[j] = wn[j];
+      }
+    }
+
+    // epilogue: lane (col, kk), register r of M-tile m = channel 32m + 16kk + r (tail: channel r, kk = 0)
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+      const int y = ty0 + 2 * wave + n, x = tx0 + col;
+      if (y >= s.H || x >= s.W) continue;
+      if (MODE == 2) {
+        if (kk != 0) continue;
+#pragma unroll
+        for (int c = 0; c < kMaxC; ++c) {
+          if (c >= C) break;
+          const size_t o = (((size_t)b * C + c) * s.H + y) * s.W + x;
+          const float net = acc[0][n][c] + bias_r[0][c];
+          float v = residual_sign > 0 ? net + xin[o] : xin[o] - net;
+          if (clamp_out) v = fminf(fmaxf(v, 0.f), 1.f);
+          out[o] = v;
+        }
+      } else {
+        float* o = out + (((size_t)b * Hp + y + 1) * Wp + x + 1) * kWidth + 16 * kk;
+#pragma unroll
+        for (int m = 0; m < T::NM; ++m)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            float4 v;
+            v.x = act_fn(acc[m][n][4 * q + 0] + bias_r[m][4 * q + 0], ACT);
+            v.y = act_fn(acc[m][n][4 * q + 1] + bias_r[m][4 * q + 1], ACT);
+            v.z = act_fn(acc[m][n][4 * q + 2] + bias_r[m][4 * q + 2], ACT);
+            v.w = act_fn(acc[m][n][4 * q + 3] + bias_r[m][4 * q + 3], ACT);
+            *reinterpret_cast<float4*>(o + 32 * m + 4 * q) = v;
+          }
+      }
+    }
+  }
+}
+
+hipError_t conv32_kernels_init() {
+  for (const void* k : {(const void*)conv32_kernel<0, 0>, (const void*)conv32_kernel<0, 1>,
+                        (const void*)conv32_kernel<1, 0>, (const void*)conv32_kernel<1, 1>,
+                        (const void*)conv32_kernel<2, 0>}) {
+    const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kC32Lds);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+size_t act32_bytes(int B, int H, int W) {
+  return (size_t)B * (H + 2) * (W + 2) * kWidth * sizeof(float);
+}
+
+void launch_conv32(int mode, const float* in, float* out, const float* xin, const float* w, const float* bias,
+                   const ConvShape& s, int C, int act, int residual_sign, int clamp_out, int num_cus,
+                   hipStream_t st) {
+  const int cap = mode == 0 ? 4 * num_cus : num_cus;   // body/tail: 88 KB of LDS, one workgroup per CU
+  const int grid = s.tiles < cap ? s.tiles : cap;
+  const size_t lds = mode == 0 ? (size_t)kHaloPix * kC32Pitch4 * 4 : (size_t)kC32Lds;
+#define C32(M, A) hipLaunchKernelGGL((conv32_kernel<M, A>), dim3(grid), dim3(256), lds, st, in, out, xin, w, bias, s, \
+                                     C, residual_sign, clamp_out)
+  if (mode == 0) {
+    if (act == 0) C32(0, 0); else C32(0, 1);
+  } else if (mode == 1) {
+    if (act == 0) C32(1, 0); else C32(1, 1);
+  } else {
+    C32(2, 0);
+  }
+#undef C32
+}
+
+}  // namespace pnp

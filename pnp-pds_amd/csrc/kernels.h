@@ -16,27 +16,27 @@ struct ConvShape {
 ConvShape make_conv_shape(int B, int H, int W);
 hipError_t conv_kernels_init();
 void pack_body_weights(const float* W, uint16_t* out);
-void pack_body_weights16(const float* W, uint16_t* out);   // conv_body_v4 (16x16x32) order, same size
-void pack_body_weights_wg(const float* W, uint16_t* out);  // conv_body_wg (row Winograd F(2,3)), kBodyWgBytes
-constexpr int kBodyWgBytes = 3 * 4 * 64 * 64 * 2;           // 98304: U[a][j][co][ci] fp16
 void pack_head_weights(const float* W, int C, uint16_t* out);
 void pack_tail_weights(const float* W, int C, uint16_t* out);
 void launch_conv_head(const half_t* in4, half_t* out, const void* w, const float* bias, const ConvShape& s,
                       int act, int num_cus, int blocks_per_cu, hipStream_t st);
-// one 64 -> 64 layer (variant kept for the tuning ABI; one kernel)
+// one 64 -> 64 layer; ablate != 0 only in the PNP_PROFILING build (profiling, results wrong)
 void launch_conv_body(const half_t* in, half_t* out, const void* w, const float* bias, const ConvShape& s,
-                      int act, int num_cus, int variant, hipStream_t st);
-// one 64 -> 64 layer on 16x16x32 MFMAs (weights packed by pack_body_weights16)
-void launch_conv_body16(const half_t* in, half_t* out, const void* w16, const float* bias, const ConvShape& s,
-                        int act, int num_cus, hipStream_t st);
-// one 64 -> 64 layer as a row-wise Winograd F(2,3) (weights packed by pack_body_weights_wg)
-void launch_conv_body_wg(const half_t* in, half_t* out, const void* wwg, const float* bias, const ConvShape& s,
-                         int act, int num_cus, hipStream_t st);
-// two 64 -> 64 layers in one launch (the intermediate stays in LDS); in needs pad >= 2
-void launch_conv_body2(const half_t* in, half_t* out, const void* w1, const float* b1, const void* w2,
-                       const float* b2, const ConvShape& s, int act, int num_cus, hipStream_t st);
+                      int act, int num_cus, int ablate, hipStream_t st);
+#ifdef PNP_PROFILING
+constexpr int kTuneAblate = 3;   // pnp_set_tuning key of the profiling build (not in include/pnppds.h)
+#endif
 void launch_conv_tail(const half_t* in, const float* xin, float* xout, const void* w, const float* bias,
                       const ConvShape& s, int C, int residual_sign, int clamp_out, int num_cus, hipStream_t st);
+// fp32-operand denoiser (conv32.hip, PNP_PREC_FP32): mode 0 = head (NCHW fp32 in), 1 = body,
+// 2 = tail (NCHW fp32 out + residual + clamp); activations fp32 padded NHWC64, pad 1.
+hipError_t conv32_kernels_init();
+size_t conv32_weight_floats(int mode);
+void pack_conv32_weights(const float* W, int mode, int cin, int cout, float* out);
+size_t act32_bytes(int B, int H, int W);
+void launch_conv32(int mode, const float* in, float* out, const float* xin, const float* w, const float* bias,
+                   const ConvShape& s, int C, int act, int residual_sign, int clamp_out, int num_cus,
+                   hipStream_t st);
 
 // ---- operators / proxes (ops.hip) ----------------------------------------------------
 enum { OP_ID = 0, OP_BLUR = 1, OP_MASK = 2 };
@@ -75,6 +75,8 @@ void launch_k3(int method, float* y, const float* xobs, const double* partials, 
 int partial_tiles(int H, int W);
 int k2_partials(const OpDesc& op, int C, int H, int W);   // partial-sum entries per image written by launch_k2
 int chunk_count(size_t n);
+// theta per image; n < kMaxL1Elems keeps the radix select's bin sums exact (ops.hip sel_bin_sum)
+constexpr size_t kMaxL1Elems = (size_t)1 << 29;
 void launch_l1_select(const float* v, float* theta, int B, size_t n, double eta, hipStream_t st);
 // out = Phi(x) (or Phi^T x) [+ add]
 void launch_op_phi(int kind, int adj, const float* x, float* out, const OpDesc& op, int BC, int H, int W,

@@ -482,7 +482,7 @@ __global__ __launch_bounds__(256) void k3_metrics(const double* __restrict__ par
 // =====================================================================================
 // l1-ball threshold (operators.py:94-100).  The reference sorts |v| and takes
 // theta = max(0, max_k (S_k - eta)/k); equivalently theta is the root of
-// f(t) = sum max(|v|-t, 0) - eta.  One 1024-thread workgroup per image runs a 3-level
+// f(t) = sum max(|v|-t, 0) - eta.  One 512-thread workgroup per image runs a 3-level
 // radix select on the float bit patterns of |v| (11 + 11 + 9 bits): each level builds
 // an LDS histogram (count, sum) of the candidates, finds the highest bin whose lower
 // edge still has f >= 0, and descends into it.  A final exact pass gives
@@ -490,7 +490,7 @@ __global__ __launch_bounds__(256) void k3_metrics(const double* __restrict__ par
 // =====================================================================================
 constexpr int kSelThreads = 512;
 
-__device__ __forceinline__ double block_sum1024(double v, double* scratch) {
+__device__ __forceinline__ double block_sum_sel(double v, double* scratch) {
   return block_sum<double, kSelThreads>(v, scratch);
 }
 
@@ -508,7 +508,9 @@ __device__ __forceinline__ unsigned sel_significand(unsigned u) {
 template <int SH>
 __device__ __forceinline__ double sel_bin_sum(const unsigned long long* sm, unsigned prefix, int j) {
   const int e = (int)(((prefix | ((unsigned)j << SH)) >> 23) & 0xffu);
-  return ldexp((double)sm[j], e ? e - 150 : -149);   // exact: the sum has < 48 significant bits
+  // exact while n < 2^29 (a bin's significand sum < n * 2^24 <= 2^53); launch_l1_select's
+  // callers reject larger images (kMaxL1Elems)
+  return ldexp((double)sm[j], e ? e - 150 : -149);
 }
 
 template <int SH, int NBITS>
@@ -586,7 +588,7 @@ __global__ __launch_bounds__(kSelThreads) void l1_select_kernel(const float* __r
   }
   double tot = 0;
   for (size_t i = threadIdx.x; i < n; i += kSelThreads) tot += (double)__uint_as_float(vb[i] & 0x7fffffffu);
-  tot = block_sum1024(tot, red);
+  tot = block_sum_sel(tot, red);
   if (tot <= eta) {                            // already inside the ball: theta = 0
     if (threadIdx.x == 0) theta[b] = 0.f;
     return;
@@ -602,8 +604,8 @@ __global__ __launch_bounds__(kSelThreads) void l1_select_kernel(const float* __r
     const unsigned u = vb[i] & 0x7fffffffu;
     if (u > prefix) { K += 1.0; S += (double)__uint_as_float(u); }
   }
-  K = block_sum1024(K, red);
-  S = block_sum1024(S, red);
+  K = block_sum_sel(K, red);
+  S = block_sum_sel(S, red);
   if (threadIdx.x == 0) {
     const double th = K > 0 ? (S - eta) / K : (double)__uint_as_float(prefix);
     theta[b] = (float)(th > 0 ? th : 0.0);

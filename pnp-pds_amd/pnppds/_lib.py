@@ -23,9 +23,10 @@ METHOD_A, METHOD_B, METHOD_C, METHOD_ADMM_B2 = 0, 1, 2, 3
  METHOD_C_PNPADMM, METHOD_C_RED) = range(4, 13)
 TV_METHODS = (METHOD_A_PDS_TV, METHOD_A_FBS_TV, METHOD_B_HTV)   # no denoiser
 OP_ID, OP_BLUR, OP_RANDOM_SAMPLING = 0, 1, 2
+PREC_FP16, PREC_FP32 = 0, 1
+PRECISIONS = {"fp16": PREC_FP16, "fp32": PREC_FP32}
 TUNE_DENOISE_CHUNK = 1
-TUNE_BODY_VARIANT = 2
-TUNE_ABLATE = 3
+TUNE_ABLATE = 3          # profiling build only (make PROFILING=1, lib_prof/): not in include/pnppds.h
 
 
 class PnpError(RuntimeError):
@@ -42,7 +43,7 @@ class pnp_params(C.Structure):
                 ("record_ssim", C.c_int32)]
 
 
-ABI_VERSION = 2   # include/pnppds.h PNP_ABI_VERSION
+ABI_VERSION = 3   # include/pnppds.h PNP_ABI_VERSION
 class pnp_degrade_params(C.Structure):
     _fields_ = [("gaussian_nl", C.c_double), ("sp_nl", C.c_double), ("poisson_alpha", C.c_double),
                 ("poisson_noise", C.c_int32), ("seed", C.c_uint32)]
@@ -56,6 +57,7 @@ _F = C.POINTER(C.c_float)
 _D = C.POINTER(C.c_double)
 _SIGS = {
     "pnp_abi_version": ([], C.c_int),
+    "pnp_build_id": ([], C.c_char_p),
     "pnp_device_count": ([C.POINTER(C.c_int)], C.c_int),
     "pnp_create": ([C.c_int, C.POINTER(_P)], C.c_int),
     "pnp_destroy": ([_P], C.c_int),
@@ -92,8 +94,41 @@ _SIGS = {
 }
 
 
+_PKG = os.path.dirname(_HERE)
+
+
+def source_hash() -> str | None:
+    """The build id libpnppds.so must carry: SHA-256 prefix of the sources listed in the
+    Makefile's SRC and HDR (sorted, concatenated), as the Makefile computes it.  None if the
+    sources are not in the tree."""
+    import hashlib
+    try:
+        with open(os.path.join(_PKG, "Makefile")) as f:
+            mk = f.read()
+    except OSError:
+        return None
+    files = []
+    for line in mk.splitlines():
+        key, _, val = line.partition("=")
+        if key.strip() in ("SRC", "HDR") and not line.startswith((" ", "\t")):
+            files += val.split()
+    h = hashlib.sha256()
+    for rel in sorted(set(files)):
+        try:
+            with open(os.path.join(_PKG, rel), "rb") as f:
+                h.update(f.read())
+        except OSError:
+            return None
+    return h.hexdigest()[:16]
+
+
+def build_id() -> str:
+    return load_library().pnp_build_id().decode()
+
+
 def load_library(path: str = LIB_PATH):
-    """Load libpnppds.so (raises if absent — there is no fallback path)."""
+    """Load libpnppds.so (raises if absent — there is no fallback path — or if it was built
+    from other sources than the tree's: a stale prebuilt library must not pass for this one)."""
     global _lib
     with _lock:
         if _lib is None:
@@ -111,6 +146,10 @@ def load_library(path: str = LIB_PATH):
                 fn.restype = res
             if lib.pnp_abi_version() != ABI_VERSION:
                 raise RuntimeError("libpnppds ABI mismatch")
+            want, got = source_hash(), lib.pnp_build_id().decode()
+            if want is not None and got != want and path == os.path.join(_PKG, "lib", "libpnppds.so"):
+                raise RuntimeError(f"{path} was built from other sources (build id {got}, tree {want}); "
+                                   "rebuild with `make -C pnp-pds_amd`")
             _lib = lib
     return _lib
 
@@ -180,21 +219,21 @@ class Context:
                                               weights.clamp_io))
         self._denoiser_key = key
 
+    def set_precision(self, precision):
+        """Denoiser operands: 'fp16' (default; fp32 accumulation) or 'fp32' (the reference's own
+        precision, models/denoiser.py:37; about a tenth of the throughput)."""
+        code = PRECISIONS[precision] if isinstance(precision, str) else int(precision)
+        self._check(self.lib.pnp_set_precision(self.h, code))
+
     def set_denoise_chunk(self, images: int):
         """Images per denoiser pass (0 = auto).  Performance only."""
         self._check(self.lib.pnp_set_tuning(self.h, TUNE_DENOISE_CHUNK, int(images)))
 
     def set_ablate(self, bits: int):
-        """Profiling only (results wrong): skip parts of the one-layer body kernel
-        (1 = halo DMA, 2 = stores, 4 = MFMA K-loop)."""
+        """Profiling build only (make PROFILING=1, PNP_LIB_PATH=.../lib_prof/libpnppds.so;
+        results wrong): skip parts of the one-layer body kernel (1 = halo DMA, 2 = stores,
+        4 = MFMA K-loop).  The product library rejects the key (PNP_E_UNSUPPORTED)."""
         self._check(self.lib.pnp_set_tuning(self.h, TUNE_ABLATE, int(bits)))
-
-    def set_body_variant(self, variant: int):
-        """Body layers per launch: 0 = one (default), 1 = two fused layers, 2 = one with the
-        staggered epilogue, 3 = one on 16x16x32 MFMAs (not bit-identical: another summation
-        order), 4 = one as a row-wise Winograd F(2,3) (fp16-rounded transformed operands;
-        within the fp16 tolerance).  Performance only."""
-        self._check(self.lib.pnp_set_tuning(self.h, TUNE_BODY_VARIANT, int(variant)))
 
     def set_operator(self, kind: int, h=None, mask=None, key=None):
         if key is not None and key == self._operator_key:

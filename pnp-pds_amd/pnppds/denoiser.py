@@ -15,9 +15,10 @@ from .weights import DenoiserWeights, resolve_weights
 
 
 class Denoiser:
-    def __init__(self, file_name, ch=3, weights: DenoiserWeights | None = None):
+    def __init__(self, file_name, ch=3, weights: DenoiserWeights | None = None, precision="fp16"):
         self.weights = weights if weights is not None else resolve_weights(file_name, ch)
         self.ch = ch
+        self.precision = precision   # 'fp16' MFMA operands (default) or 'fp32' (the reference's)
         self.key = ("den", self.weights.name, file_name, id(weights) if weights is not None else 0)
         self.cost = 0
 
@@ -30,6 +31,7 @@ class Denoiser:
         B, Cc, H, W = x.shape
         ctx = get_ctx()
         self.configure(ctx)
+        ctx.set_precision(self.precision)
         dx = to_device(x)
         dy = to_device(np.empty(x.shape, np.float32))
         ctx.op_denoise(dx.data_ptr(), dy.data_ptr(), B, Cc, H, W)

@@ -13,7 +13,8 @@ Differences from the reference, by design:
   * ``phi``/``adj_phi`` must come from pnppds.operators.get_observation_operators (opaque
     Python closures cannot run on the device; there is no host fallback).
   * state is fp32 on the device (the reference mixes fp32 x and fp64 y); denoiser
-    operands are fp16 with fp32 accumulation.  Tolerances: DESIGN.md §Parity.
+    operands are fp16 with fp32 accumulation, except for the Poisson methods, which run fp32
+    operands (``precision='auto'``; FP32_METHODS below).  Tolerances: DESIGN.md §Parity.
   * ``ssim`` is computed on the device every iteration (utils_eval.eval_ssim restated;
     skimage is absent here, so its parity is unpinned).
   * comparisonB-4 / comparisonB-5 run with the DnCNN denoiser their text uses; the
@@ -59,6 +60,23 @@ def make_params(gamma1, gamma2, alpha_s, alpha_n, myLambda, m1, m2, gammaInADMMS
 
 BM3D_METHODS = ("A-PnPPDS-BM3D", "A-PnPFBS-BM3D", "comparisonB-1", "C-PnPPDS-BM3D")
 
+# Denoiser operand precision per method when precision="auto" (the default).  Measured against
+# the reference's own trajectories (tests/test_gpu_long.py): with fp16 operands
+# ours-A stays within 0.0043 dB over the 1200 iterations of a blur experiment and ours-B within
+# 0.0006 dB over 300, but the Poisson method drifts (ours-C, random sampling, gamma1 = 0.00035:
+# 0.008 dB at 300 iterations, 0.19 dB at the 3000 that main.py:136-139 runs), because its tiny
+# primal steps integrate the fp16 denoiser's deterministic error through the dual.  fp32
+# operands hold every case to <= 0.00013 dB, so the Poisson-family methods default to them.
+FP32_METHODS = (_lib.METHOD_C, _lib.METHOD_C_PNPADMM, _lib.METHOD_C_RED)
+
+
+def resolve_precision(precision, method_code: int) -> str:
+    if precision == "auto":
+        return "fp32" if method_code in FP32_METHODS else "fp16"
+    if precision not in _lib.PRECISIONS:
+        raise ValueError(f"precision must be 'auto', 'fp16' or 'fp32', not {precision!r}")
+    return precision
+
 
 def resolve_method(method: str) -> int:
     if method in BM3D_METHODS:
@@ -86,11 +104,14 @@ def _check_ops(phi, adj_phi):
 
 def test_iter_batch(x_0, x_obsrv, x_true, phi, adj_phi, gamma1, gamma2, alpha_s, alpha_n, myLambda, m1, m2,
                     gammaInADMMStep1, gaussian_nl, sp_nl, poisson_alpha, path_prox, max_iter,
-                    method="A-Proposed", ch=3, r=1, record_metrics=True, record_ssim=True, ctx=None):
+                    method="A-Proposed", ch=3, r=1, record_metrics=True, record_ssim=True, ctx=None,
+                    precision="auto"):
     """Batched test_iter over B independent images: arrays are [B, C, H, W].
     Returns (x[B,C,H,W] f32, s+0.5 [B,C,H,W] f32, c[B,max_iter], psnr[B,max_iter], ssim[B,max_iter],
     avg_time).  ssim is computed on the device each iteration (iteration.py:189) when record_ssim;
-    C == 1 batches are scored as the reference's (H, W) grayscale arrays."""
+    C == 1 batches are scored as the reference's (H, W) grayscale arrays.  precision: the
+    denoiser's MFMA operands, 'fp16', 'fp32' (the reference's, about 10x slower) or 'auto'
+    (default: fp32 for the Poisson methods, fp16 otherwise; FP32_METHODS)."""
     m = resolve_method(method)
     _check_ops(phi, adj_phi)
     x0 = np.asarray(x_0)
@@ -100,6 +121,7 @@ def test_iter_batch(x_0, x_obsrv, x_true, phi, adj_phi, gamma1, gamma2, alpha_s,
     if Cc != ch:
         raise ValueError(f"ch={ch} but images have {Cc} channels")
     ctx = ctx or get_ctx()
+    ctx.set_precision(resolve_precision(precision, m))
     if m not in _lib.TV_METHODS:                       # the TV methods use no denoiser
         den = _resolve_denoiser(path_prox, ch)
         den.configure(ctx)
@@ -114,8 +136,9 @@ def test_iter_batch(x_0, x_obsrv, x_true, phi, adj_phi, gamma1, gamma2, alpha_s,
 
 def test_iter(x_0, x_obsrv, x_true, phi, adj_phi, gamma1, gamma2, alpha_s, alpha_n, myLambda, m1, m2,
               gammaInADMMStep1, gaussian_nl, sp_nl, poisson_alpha, path_prox, max_iter, method="A-Proposed",
-              ch=3, r=1):
-    """iteration.py:10 signature; x_0 etc. are (C,H,W) (RGB) or (H,W) (gray)."""
+              ch=3, r=1, *, precision="auto"):
+    """iteration.py:10 signature; x_0 etc. are (C,H,W) (RGB) or (H,W) (gray).  Keyword-only
+    extension: precision ('auto' default, 'fp16', 'fp32'; see test_iter_batch)."""
     x0 = np.asarray(x_0)
     shp = x0.shape
     to4 = (lambda a: np.asarray(a).reshape((1, 1) + shp)) if x0.ndim == 2 else \
@@ -123,5 +146,5 @@ def test_iter(x_0, x_obsrv, x_true, phi, adj_phi, gamma1, gamma2, alpha_s, alpha
     x, s, c, psnr, ssim, t = test_iter_batch(to4(x0), to4(x_obsrv), None if x_true is None else to4(x_true),
                                              phi, adj_phi, gamma1, gamma2, alpha_s, alpha_n, myLambda, m1, m2,
                                              gammaInADMMStep1, gaussian_nl, sp_nl, poisson_alpha, path_prox,
-                                             max_iter, method, ch, r)
+                                             max_iter, method, ch, r, precision=precision)
     return x.reshape(shp), s.reshape(shp).astype(np.float64), c[0], psnr[0], ssim[0], t

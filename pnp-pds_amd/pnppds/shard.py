@@ -4,7 +4,7 @@ Every image's PnP-PDS state (x, y, s, x_obs, metrics) is independent and every r
 in test_iter (l2 norm, l1 threshold, c_n, PSNR) is per image, so the batch
 is split into contiguous shards with no collective on the data path.  torch.distributed
 (RCCL over xGMI on the GPU box, gloo in the CPU tests) is used only
-  * to gather the per-shard results on every rank after the run (off the timed path), and
+  * to gather the per-shard results on rank 0 after the run (off the timed path), and
   * for the max-over-ranks wall time of the benchmark.
 
 The reference runs its images one after another in one process (main.py:36-69); a batch
@@ -47,11 +47,19 @@ def max_over_ranks(value: float, device=None) -> float:
     return float(t.item())
 
 
-def test_iter_sharded(x_0, x_obsrv, x_true, *args, runner=None, **kwargs):
+def test_iter_sharded(x_0, x_obsrv, x_true, *args, runner=None, gather="rank0", **kwargs):
     """Batched test_iter ([B, C, H, W] arrays) over the ranks of the default process group:
-    each rank solves images shard_bounds(B, world, rank) on its own GPU, then the results
-    are gathered on every rank.  `runner` defaults to pnppds.iteration.test_iter_batch
-    (the device solver); tests substitute the CPU oracle to check the sharding alone."""
+    each rank solves images shard_bounds(B, world, rank) on its own GPU.  x_obsrv / x_true
+    may be shared (C, H, W) arrays, broadcast to every image as in test_iter_batch.
+
+    gather="rank0" (default): rank 0 returns the whole batch's results, the other ranks
+    None (one gather to one host: at cfg5 the whole batch's x and s are 13 GB, which must
+    not be replicated on every rank).  gather="none": every rank returns
+    (its shard's results, (lo, hi)) and nothing crosses ranks.  `runner` defaults to
+    pnppds.iteration.test_iter_batch (the device solver); tests substitute the CPU oracle
+    to check the sharding alone."""
+    if gather not in ("rank0", "none"):
+        raise ValueError(f"gather must be 'rank0' or 'none', not {gather!r}")
     if runner is None:
         from .iteration import test_iter_batch as runner
     rank, world = dist_info()
@@ -59,16 +67,18 @@ def test_iter_sharded(x_0, x_obsrv, x_true, *args, runner=None, **kwargs):
     B = x0.shape[0]
     lo, hi = shard_bounds(B, world, rank)
     sl = slice(lo, hi)
-    xt = None if x_true is None else np.asarray(x_true)[sl]
-    if hi > lo:
-        parts = tuple(runner(x0[sl], np.asarray(x_obsrv)[sl], xt, *args, **kwargs))
-    else:
-        parts = None
+    xo = np.broadcast_to(np.asarray(x_obsrv), x0.shape)
+    xt = None if x_true is None else np.broadcast_to(np.asarray(x_true), x0.shape)[sl]
+    parts = tuple(runner(x0[sl], xo[sl], xt, *args, **kwargs)) if hi > lo else None
+    if gather == "none":
+        return parts, (lo, hi)
     if world == 1:
         return parts
     import torch.distributed as dist
-    allp = [None] * world
-    dist.all_gather_object(allp, parts)
+    allp = [None] * world if rank == 0 else None
+    dist.gather_object(parts, allp, dst=0)
+    if rank != 0:
+        return None
     allp = [p for p in allp if p is not None]
     out = []
     for k in range(len(allp[0])):

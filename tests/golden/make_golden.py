@@ -266,7 +266,51 @@ def make_cmp_golden(ref_root="/root/reference"):
         print(f"iter_cmp_{name}.npz  psnr {ps[0]:.3f} -> {ps[-1]:.3f}  ({time.perf_counter()-t:.1f}s)")
 
 
+LONG_CASES = [
+    # name,          method,       deg_op,            ch, size, sigma, sp,  pois,  g1,      g2,          a_n,  a_s,  lam, r,   iters
+    ("A_blur_1200",  "A-Proposed", "blur",            3, 256, 0.01, 0.0, False, 0.99,    0.99,        0.95, 1.0,  1.0, 0.8, 1200),
+    ("B_blur_300",   "B-Proposed", "blur",            3, 128, 0.01, 0.1, False, 1.0,     0.49,        0.95, 0.95, 1.0, 0.8, 300),
+    ("C_rs_300",     "C-Proposed", "random_sampling", 3, 128, 0.0,  0.0, True,  0.00035, 1 / 0.00035, 1.0,  1.0,  1.0, 0.5, 300),
+    # random-sampling experiments run 3000 iterations (main.py:136-139)
+    ("C_rs_3000",    "C-Proposed", "random_sampling", 3, 128, 0.0,  0.0, True,  0.00035, 1 / 0.00035, 1.0,  1.0,  1.0, 0.5, 3000),
+]
+
+
+def make_long_golden(ref_root="/root/reference", only=None):
+    """Long trajectories at the lengths the experiments run (main.py:136-139: 1200 iterations
+    for blur), so the 0.01 dB PSNR bound is checked over every iteration rather than
+    extrapolated from 120: ours-A 3x256^2 blur for 1200 iterations (the metric's method,
+    operator and image size), ours-B blur + salt-and-pepper and ours-C random sampling + Poisson
+    at 3x128^2 for 300.  Stored: inputs, the per-iteration c and PSNR, the final x in fp16."""
+    install_shims(ref_root)
+    import operators as op
+    import iteration
+    path_kernel = os.path.join(ref_root, "blur_models", "blur_1.mat")
+    nn_dir = os.path.join(ref_root, "nn")
+    for (name, method, deg, ch, n, sig, sp, pois, g1, g2, an, as_, lam, r, iters) in LONG_CASES:
+        if only and name not in only:
+            continue
+        phi, adj = op.get_observation_operators(deg, path_kernel, r)
+        Id, _ = op.get_observation_operators("Id", path_kernel, r)
+        xt = synthetic_image(ch, n, n, seed=7 if n == 256 else 500 + len(name))
+        obs, x0 = degrade(xt, phi, Id, deg, sig, sp, pois, 300)
+        arch = f"DnCNN_nobn_nch_{ch}_nlev_0.01"
+        t = time.perf_counter()
+        res = iteration.test_iter(x0, obs, xt, phi, adj, g1, g2, as_, an, lam, 15, 15, 0.1, sig, sp, 300,
+                                  os.path.join(nn_dir, arch + ".pth"), iters, method, ch, r)
+        xs, ss, c, ps, _ssim, _t = res
+        small = (lambda a: np.asarray(a, np.float32)) if n >= 256 else np.asarray   # fixture size
+        np.savez_compressed(os.path.join(HERE, f"long_{name}.npz"), x_true=xt, x_obs=small(obs),
+                            x_0=small(x0), x_out=np.asarray(xs).astype(np.float16), c=c, psnr=ps,
+                            params=np.array([g1, g2, as_, an, lam, 15, 15, 0.1, sig, sp, 300, iters, ch, r]),
+                            method=np.array(method), deg_op=np.array(deg), arch=np.array(arch))
+        print(f"long_{name}.npz psnr {ps[0]:.3f} -> {ps[-1]:.3f} ({time.perf_counter()-t:.1f}s)", flush=True)
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "--long":
+        make_long_golden(only=sys.argv[2:] or None)
+        sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "--cmp":
         make_cmp_golden(*sys.argv[2:])
         sys.exit(0)

@@ -56,48 +56,48 @@ def test_denoiser_ragged_batched(gpu_ctx, B, C, H, W):
     np.testing.assert_array_equal(one[0], out[B - 1])
 
 
-@pytest.mark.parametrize("name,B,C,H,W", [("DnCNN_nobn_nch_3_nlev_0.01", 3, 3, 50, 70),
-                                          ("DnCNN_nobn_nch_3_nlev_0.01", 2, 3, 256, 256),
-                                          ("dncnn_15", 2, 1, 37, 45), ("DnCNN_nobn_nch_1_nlev_0.01", 1, 1, 8, 32)])
-def test_body_variants_bit_identical(gpu_ctx, name, B, C, H, W):
-    """One layer per launch (plain and staggered epilogue) and two fused layers per launch run
-    the same MFMA K-sequence per output (and the fused intermediate is the same fp16 image):
-    same bits."""
-    rng = np.random.default_rng(11)
-    w = DenoiserWeights.load_npz(os.path.join(WEIGHTS_DIR, name + ".npz"))
-    x = rng.uniform(0, 1, (B, C, H, W)).astype(np.float32)
-    outs = []
-    for v in (0, 1, 2):
-        gpu_ctx.set_body_variant(v)
-        outs.append(run_denoise(gpu_ctx, w, x))
-    gpu_ctx.set_body_variant(0)
-    for o in outs[1:]:
-        np.testing.assert_array_equal(outs[0], o)
+# fp32 operands (PNP_PREC_FP32, v_mfma_f32_32x32x2_f32: exact fp32 FMA chains) vs the
+# reference's fp32 conv: only the summation order differs.
+TOL_FP32 = 1e-5
 
 
-@pytest.mark.parametrize("variant", [3, 4])
-@pytest.mark.parametrize("name,B,C,H,W", [("DnCNN_nobn_nch_3_nlev_0.01", 3, 3, 50, 70),
-                                          ("DnCNN_nobn_nch_3_nlev_0.01", 2, 3, 256, 256),
-                                          ("dncnn_15", 2, 1, 37, 45)])
-def test_body_variant_mfma16(gpu_ctx, variant, name, B, C, H, W):
-    """Variant 3 (16x16x32 MFMAs, planar halo) sums each output's 576 products in another
-    order than the 32x32x16 kernels, and variant 4 (row Winograd F(2,3)) rounds transformed
-    operands to fp16 instead of the plain ones, so they match the fp16-emulating oracle to
-    the same tolerance rather than variant 0 bit for bit."""
-    rng = np.random.default_rng(12)
+@pytest.mark.parametrize("name", ["DnCNN_nobn_nch_3_nlev_0.01", "DnCNN_nobn_nch_1_nlev_0.01",
+                                  "dncnn_color_blind", "dncnn_15"])
+def test_denoiser_fp32_golden(gpu_ctx, golden_denoiser, name):
+    """The fp32-operand path against the reference's own denoiser outputs (denoiser.npz,
+    made by the imported reference) and the fp32 oracle."""
     w = DenoiserWeights.load_npz(os.path.join(WEIGHTS_DIR, name + ".npz"))
-    x = rng.uniform(0, 1, (B, C, H, W)).astype(np.float32)
-    gpu_ctx.set_body_variant(variant)
+    xin = golden_denoiser[f"in_{name}"]
+    x4 = xin.reshape((1, 1) + xin.shape) if xin.ndim == 2 else xin[None]
+    gpu_ctx.set_precision("fp32")
+    try:
+        out = run_denoise(gpu_ctx, w, x4).reshape(xin.shape)
+    finally:
+        gpu_ctx.set_precision("fp16")
+    ref = golden_denoiser[f"out_{name}"]
+    scale = max(1.0, float(np.abs(ref).max()))
+    err = float(np.abs(out - ref).max())
+    print(f"{name}: fp32 path max|d| vs reference = {err:.2e}")
+    assert err <= TOL_FP32 * scale
+    o32 = O.OracleDenoiser(w).forward_batch(x4).reshape(xin.shape)
+    assert np.abs(out - o32).max() <= TOL_FP32 * scale
+
+
+@pytest.mark.parametrize("B,C,H,W", [(3, 3, 50, 70), (2, 1, 33, 31), (1, 3, 8, 32), (2, 3, 256, 256)])
+def test_denoiser_fp32_ragged_batched(gpu_ctx, B, C, H, W):
+    """fp32 path: partial tiles, tiny images, several images per launch; batch vs single bits."""
+    rng = np.random.default_rng(B * 100 + H + 7)
+    w = random_weights(C, depth=6, seed=H, scale=0.9)
+    x = rng.uniform(-0.1, 1.1, (B, C, H, W)).astype(np.float32)
+    gpu_ctx.set_precision("fp32")
     try:
         out = run_denoise(gpu_ctx, w, x)
         one = run_denoise(gpu_ctx, w, x[B - 1:B])
     finally:
-        gpu_ctx.set_body_variant(0)
-    emu = O.OracleDenoiser(w, emulate_fp16=True).forward_batch(x[:1])
-    np.testing.assert_allclose(out[:1], emu, atol=TOL_VS_FP16_EMU)
-    base = run_denoise(gpu_ctx, w, x)
-    assert np.abs(out - base).max() <= TOL_VS_FP16_EMU
-    np.testing.assert_array_equal(one[0], out[B - 1])        # images independent: same bits alone
+        gpu_ctx.set_precision("fp16")
+    ref = O.OracleDenoiser(w).forward_batch(x)
+    np.testing.assert_allclose(out, ref, atol=TOL_FP32)
+    np.testing.assert_array_equal(one[0], out[B - 1])
 
 
 def test_denoiser_full_size_rgb(gpu_ctx):

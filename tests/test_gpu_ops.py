@@ -155,6 +155,47 @@ def test_l1_ball_deterministic(gpu_ctx, torch_cuda):
         np.testing.assert_array_equal(host(torch_cuda, one, gpu_ctx)[0], outs[0][b])
 
 
+@pytest.mark.parametrize("kind", ["exponents", "ties"])
+def test_l1_ball_exact_bins_edge_cases(gpu_ctx, torch_cuda, kind):
+    """The exact-bin radix select on data that exercises its edge paths: magnitudes spread
+    over 140 binary exponents including subnormals (the e == 0 significand branch and bins
+    at exponent boundaries), and many exactly repeated values at / near the threshold.
+    Bits batch vs one-image launch; values against the oracle's sort-based projection."""
+    rng = np.random.default_rng(5 if kind == "exponents" else 6)
+    B, n = 4, 3 * 96 * 96
+    if kind == "exponents":
+        mag = np.ldexp(rng.uniform(1, 2, (B, n)), rng.integers(-140, 3, (B, n)))
+        mag[:, :64] = np.ldexp(rng.integers(1, 1 << 20, (B, 64)).astype(np.float64), -149)   # subnormals
+        mag[:, 64:96] = np.ldexp(1.0, rng.integers(-126, 2, (B, 32)))                         # exact powers of 2
+    else:
+        mag = rng.uniform(0, 0.3, (B, n))
+        mag[:, : n // 3] = 0.125                                     # a third of the entries tie
+        mag[:, n // 3: n // 3 + 500] = np.nextafter(np.float32(0.125), np.float32(1))
+        mag[:, n // 3 + 500: n // 3 + 1000] = np.nextafter(np.float32(0.125), np.float32(0))
+    v = (mag * rng.choice([-1.0, 1.0], (B, n))).astype(np.float32)
+    assert (np.abs(v[:, :64]) < np.finfo(np.float32).tiny).all() or kind == "ties"
+    dx = dev(torch_cuda, v)
+    out = torch_cuda.empty_like(dx)
+    gpu_ctx.op_proj_l1_ball(dx.data_ptr(), out.data_ptr(), B, n, 0.95, 0.1, 0.8)
+    got = host(torch_cuda, out, gpu_ctx)
+    eta = 0.95 * n * 0.1 * 0.8 * 0.5
+    for b in range(B):
+        ref = O.proj_l1_ball(v[b].astype(np.float64), 0.95, 0.1, 0.8)
+        np.testing.assert_allclose(got[b], ref, atol=2e-6 * max(1.0, float(np.abs(v[b]).max())))
+        if np.abs(v[b].astype(np.float64)).sum() > eta:
+            assert abs(np.abs(got[b].astype(np.float64)).sum() - eta) <= 1e-4 * eta
+        one = torch_cuda.empty_like(dx[b:b + 1])
+        gpu_ctx.op_proj_l1_ball(dx[b:b + 1].data_ptr(), one.data_ptr(), 1, n, 0.95, 0.1, 0.8)
+        np.testing.assert_array_equal(host(torch_cuda, one, gpu_ctx)[0], got[b])
+
+
+def test_l1_ball_rejects_oversized_images(gpu_ctx):
+    """Above 2^29 elements per image the bin sums would no longer be exact: rejected."""
+    from pnppds._lib import PnpError
+    with pytest.raises(PnpError):
+        gpu_ctx.op_proj_l1_ball(16, 16, 1, 1 << 29, 0.95, 0.1, 0.8)
+
+
 def test_prox_gkl(gpu_ctx, torch_cuda, golden_ops):
     g = golden_ops
     v, x0 = g["prox_v"] * 10, np.round(g["prox_x0"] * 300)

@@ -49,9 +49,17 @@ def _worker(rank, world, port, out_dir, method):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         xt, xo = _inputs()
-        x, s, c, p, t = shard.test_iter_sharded(xo, xo, xt, method, ITERS, runner=oracle_batch_runner)
+        res = shard.test_iter_sharded(xo, xo, xt, method, ITERS, runner=oracle_batch_runner)
+        local, (lo, hi) = shard.test_iter_sharded(xo, xo, xt, method, ITERS, runner=oracle_batch_runner,
+                                                  gather="none")
         tmax = shard.max_over_ranks(float(rank + 1))
-        np.savez(os.path.join(out_dir, f"r{rank}.npz"), x=x, s=s, c=c, p=p, tmax=tmax)
+        if rank == 0:
+            x, s, c, p, t = res
+            np.savez(os.path.join(out_dir, "gathered.npz"), x=x, s=s, c=c, p=p)
+        else:
+            assert res is None                    # results are gathered on rank 0 only
+        np.savez(os.path.join(out_dir, f"r{rank}.npz"), lo=lo, hi=hi, tmax=tmax,
+                 x=local[0] if local is not None else np.zeros((0, C, H, W), np.float32))
     finally:
         dist.destroy_process_group()
 
@@ -74,10 +82,28 @@ def test_sharded_equals_single_process(world, method):
     ref = oracle_batch_runner(xo, xo, xt, method, ITERS)
     with tempfile.TemporaryDirectory() as d:
         mp.spawn(_worker, args=(world, _free_port(), d, method), nprocs=world, join=True)
+        got = np.load(os.path.join(d, "gathered.npz"))
+        np.testing.assert_array_equal(got["x"], ref[0])
+        np.testing.assert_array_equal(got["s"], ref[1])
+        np.testing.assert_array_equal(got["c"], ref[2])
+        np.testing.assert_array_equal(got["p"], ref[3])
         for r in range(world):
-            got = np.load(os.path.join(d, f"r{r}.npz"))
-            np.testing.assert_array_equal(got["x"], ref[0])
-            np.testing.assert_array_equal(got["s"], ref[1])
-            np.testing.assert_array_equal(got["c"], ref[2])
-            np.testing.assert_array_equal(got["p"], ref[3])
-            assert float(got["tmax"]) == float(world)   # max over ranks of rank+1
+            loc = np.load(os.path.join(d, f"r{r}.npz"))
+            lo, hi = int(loc["lo"]), int(loc["hi"])
+            assert (lo, hi) == shard.shard_bounds(B, world, r)
+            np.testing.assert_array_equal(loc["x"], ref[0][lo:hi])   # gather="none": the local shard only
+            assert float(loc["tmax"]) == float(world)   # max over ranks of rank+1
+
+
+def test_shared_observation_is_broadcast():
+    """A shared (C, H, W) x_obsrv / x_true is broadcast to every image before slicing (as in
+    test_iter_batch), not sliced along the channel axis."""
+    xt, xo = _inputs()
+    seen = []
+
+    def runner(x0, xo_, xt_, *a, **k):
+        seen.append((xo_.shape, xt_.shape))
+        return (x0,)
+    out = shard.test_iter_sharded(xo, xo[0], xt[1], runner=runner)
+    assert seen == [((B, C, H, W), (B, C, H, W))]
+    np.testing.assert_array_equal(out[0], xo)

@@ -19,9 +19,10 @@ def main():
     ap.add_argument("--size", type=int, default=256)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--chunk", type=int, default=0)
-    ap.add_argument("--variant", type=int, default=0)
     ap.add_argument("--random", action="store_true", help="uniform-random input instead of structured images")
-    ap.add_argument("--ablate", type=int, default=0, help="profiling only: 1 DMA, 2 stores, 4 MFMA skipped")
+    ap.add_argument("--ablate", type=int, default=0,
+                    help="profiling build only (PNP_LIB_PATH=.../lib_prof/libpnppds.so): 1 DMA, 2 stores, 4 MFMA skipped")
+    ap.add_argument("--precision", default="fp16", choices=["fp16", "fp32"])
     a = ap.parse_args()
     import torch
     from pnppds import _lib
@@ -29,8 +30,9 @@ def main():
     ctx = _lib.Context(0)
     ctx.set_denoiser(resolve_weights("DnCNN_nobn_nch_3_nlev_0.01", 3))
     ctx.set_denoise_chunk(a.chunk)
-    ctx.set_body_variant(a.variant)
-    ctx.set_ablate(a.ablate)
+    ctx.set_precision(a.precision)
+    if a.ablate:
+        ctx.set_ablate(a.ablate)
     B, C, H, W = a.batch, 3, a.size, a.size
     if a.random:
         x = torch.rand((B, C, H, W), device="cuda:0")
