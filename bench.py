@@ -139,7 +139,7 @@ def prox_bytes(method, B, C, H, W):
                 "k3_dual": 4 * n * 3}                      # read v, xobs; write y
     if method == "B-Proposed":
         return {"k1_primal_pre": 4 * n * 5 + 8 * npx,      # read x, y, s; write u32, w; write u16
-                "l1_select": 4 * n * 5,                    # |w| total + 3 radix levels + exact pass
+                "l1_select": 4 * n * 3,                    # 3 radix-level histogram passes over w
                 "k2_dual": 4 * n * 9,                      # read x+, x, y, xobs, xtrue, s, w; write v, s+
                 "k3_dual": 4 * n * 3}
     if method == "C-Proposed":

@@ -78,6 +78,7 @@ struct pnp_ctx {
   // scratch for single ops
   DevBuf scr_u32, scr_u16, scr_act[2], scr_part, scr_theta;
   DevBuf act32[2];   // fp32 hidden activations (PNP_PREC_FP32), shared by the solver and pnp_op_denoise
+  DevBuf l1_scr;     // l1-ball select histograms + per-image state (launch_l1_select)
 
   // profiling
   bool prof = false;
@@ -336,6 +337,13 @@ void run_denoiser(pnp_ctx* ctx, const half_t* u16, const float* u32, float* xout
   }
 }
 
+// l1-ball threshold per image into theta (scratch grown and zeroed on demand)
+void l1_select(pnp_ctx* ctx, const float* v, float* theta, int B, size_t n, double eta, hipStream_t st) {
+  const size_t need = l1_select_scratch_bytes(B);
+  if (!ctx->l1_scr.p || ctx->l1_scr.bytes < need) ensure(ctx, ctx->l1_scr, need, true);
+  launch_l1_select(v, theta, ctx->l1_scr.p, B, n, eta, st);
+}
+
 // -------- one solver iteration -------------------------------------------------------
 double l2_eps(pnp_ctx* ctx, size_t n) {
   const pnp_params& p = ctx->prm;
@@ -372,7 +380,7 @@ void solver_iteration(pnp_ctx* ctx) {
   if (mb) {
     ProfScope ps(ctx, "l1_select", st);
     const double eta = p.alpha_s * (double)n * p.sp_nl * p.r * 0.5;   // operators.py:96
-    launch_l1_select(P<float>(ctx->w), P<float>(ctx->theta), B, n, eta, st);
+    l1_select(ctx, P<float>(ctx->w), P<float>(ctx->theta), B, n, eta, st);
     check_launch(ctx, "l1_select");
   }
   run_denoiser(ctx, P<half_t>(ctx->u16), P<float>(ctx->u32), xn, ctx->act, B, H, W, st);
@@ -434,7 +442,7 @@ void solver_iteration_admm(pnp_ctx* ctx) {
     const double eta = p.alpha_s * (double)n * p.sp_nl * 0.5;               // operators.py:96, r = 1
     for (int i = 0; i < p.m2; ++i) {
       launch_lincomb(w, 0.0, sv, 1.0 - g, pp, -g, y, -g, z, g, N, st);       // s - (Phi x + s - z + y) / g1
-      launch_l1_select(w, P<float>(ctx->theta), B, n, eta, st);
+      l1_select(ctx, w, P<float>(ctx->theta), B, n, eta, st);
       launch_shrink(w, sv, P<float>(ctx->theta), B, n, st);
     }
     check_launch(ctx, "admm_s_step");
@@ -487,7 +495,7 @@ void solver_iteration_cmp(pnp_ctx* ctx) {
   const double eta = p.alpha_s * (double)n * p.sp_nl * 0.5;                         // proj_l1_ball, r = 1
   const double eps = std::sqrt((double)n * (1.0 - p.sp_nl)) * p.alpha_n * p.gaussian_nl;  // proj_l2_ball, r = 1
   auto l1proj = [&](const float* in, float* out) {
-    launch_l1_select(in, P<float>(ctx->theta), B, n, eta, st);
+    l1_select(ctx, in, P<float>(ctx->theta), B, n, eta, st);
     launch_shrink(in, out, P<float>(ctx->theta), B, n, st);
   };
   auto metrics = [&] {
@@ -548,7 +556,7 @@ void solver_iteration_cmp(pnp_ctx* ctx) {
       const int mb = m == PNP_METHOD_B_HTV;
       if (mb) {
         lin(w, 0.0, sv, 1.0, y, -p.gamma1);
-        launch_l1_select(w, P<float>(ctx->theta), B, n, eta, st);
+        l1_select(ctx, w, P<float>(ctx->theta), B, n, eta, st);
       }
       launch_tv_dual(xn, xo, y1, p.gamma2, B, C, H, W, st);
       launch_k2(od.kind, mb ? PNP_METHOD_B : PNP_METHOD_A, xn, xo, y, xobs, xt, sv, w, P<float>(ctx->theta),
@@ -775,7 +783,7 @@ int pnp_destroy(pnp_ctx* ctx) {
                     &ctx->z, &ctx->p, &ctx->t, &ctx->dense_fwd, &ctx->dense_adj, &ctx->ssim_scr,
                     &ctx->taps64, &ctx->y1, &ctx->d, &ctx->c1, &ctx->dg_words, &ctx->dg_flag, &ctx->dg_rank, &ctx->dg_scan, &ctx->dg_noise,
                     &ctx->dg_img, &ctx->dg_draws, &ctx->dg_first, &ctx->dg_status,
-                    &ctx->head_w32, &ctx->body_w32, &ctx->tail_w32, &ctx->act32[0], &ctx->act32[1]};
+                    &ctx->head_w32, &ctx->body_w32, &ctx->tail_w32, &ctx->act32[0], &ctx->act32[1], &ctx->l1_scr};
   for (DevBuf* b : bufs) release(*b);
   for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -1139,7 +1147,7 @@ int pnp_op_proj_l1_ball(pnp_ctx* ctx, const float* x, float* out, int B, int64_t
     ensure(ctx, ctx->scr_theta, (size_t)B * sizeof(float));
     const double eta = alpha_s * (double)n * sp_nl * r * 0.5;    // operators.py:96
     hipStream_t st = pick_stream(ctx, stream);
-    launch_l1_select(x, P<float>(ctx->scr_theta), B, (size_t)n, eta, st);
+    l1_select(ctx, x, P<float>(ctx->scr_theta), B, (size_t)n, eta, st);
     check_launch(ctx, "l1_select");
     launch_shrink(x, out, P<float>(ctx->scr_theta), B, (size_t)n, st);
     check_launch(ctx, "shrink");

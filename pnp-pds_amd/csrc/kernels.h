@@ -75,9 +75,11 @@ void launch_k3(int method, float* y, const float* xobs, const double* partials, 
 int partial_tiles(int H, int W);
 int k2_partials(const OpDesc& op, int C, int H, int W);   // partial-sum entries per image written by launch_k2
 int chunk_count(size_t n);
-// theta per image; n < kMaxL1Elems keeps the radix select's bin sums exact (ops.hip sel_bin_sum)
+// theta per image; n < kMaxL1Elems keeps the radix select's bin sums exact (ops.hip sel_bin_sum).
+// scratch: l1_select_scratch_bytes(B), zeroed once at allocation (the launches leave it clean).
 constexpr size_t kMaxL1Elems = (size_t)1 << 29;
-void launch_l1_select(const float* v, float* theta, int B, size_t n, double eta, hipStream_t st);
+size_t l1_select_scratch_bytes(int B);
+void launch_l1_select(const float* v, float* theta, void* scratch, int B, size_t n, double eta, hipStream_t st);
 // out = Phi(x) (or Phi^T x) [+ add]
 void launch_op_phi(int kind, int adj, const float* x, float* out, const OpDesc& op, int BC, int H, int W,
                    hipStream_t st, const float* add = nullptr);

@@ -482,25 +482,36 @@ __global__ __launch_bounds__(256) void k3_metrics(const double* __restrict__ par
 // =====================================================================================
 // l1-ball threshold (operators.py:94-100).  The reference sorts |v| and takes
 // theta = max(0, max_k (S_k - eta)/k); equivalently theta is the root of
-// f(t) = sum max(|v|-t, 0) - eta.  One 512-thread workgroup per image runs a 3-level
-// radix select on the float bit patterns of |v| (11 + 11 + 9 bits): each level builds
-// an LDS histogram (count, sum) of the candidates, finds the highest bin whose lower
-// edge still has f >= 0, and descends into it.  A final exact pass gives
-// K = #{|v| > t*}, S = sum of those (fp64, fixed order), theta = (S - eta) / K.
-// =====================================================================================
-constexpr int kSelThreads = 512;
-
-__device__ __forceinline__ double block_sum_sel(double v, double* scratch) {
-  return block_sum<double, kSelThreads>(v, scratch);
-}
-
-// One radix level: histogram of candidates whose bits above this level equal `prefix`,
-// then the highest bin j with f(lo_j) >= 0.  Updates prefix / (Khi, Shi).
+// f(t) = sum max(|v|-t, 0) - eta.  A 3-level radix select on the float bit patterns of |v|
+// (11 + 11 + 9 bits): each level builds a histogram (count, sum) of the candidates, finds the
+// highest bin whose lower edge still has f >= 0, and descends into it.  After the last level
+// every candidate bin is one float value t*, and the counts / sums strictly above it are
+// K = #{|v| > t*} and S = sum of those, so theta = (S - eta) / K with no extra pass.
+//
+// Work split (MI355X: a whole chip of CUs, few images): each level is a histogram launch
+// over G workgroups per image (B x G >= 512, slices of >= 16K elements, 16-B loads; each
+// workgroup bins its slice in LDS and adds its non-empty bins to the image's histogram in
+// HBM with integer atomics) and a pick launch (one wave per image) that scans the bins and
+// updates the image's state {prefix, K above, S above}.  Level 1 also yields sum |v|
+// (all values are its candidates), which decides the "inside the ball" case.
 // Bin sums are kept exactly: every value of a bin shares its float exponent (the bins split
 // the bit pattern below the 8 exponent bits), so a bin's sum is (sum of 24-bit significands,
-// a uint64 that LDS atomics add in any order to the same result) x 2^(exponent - 150).
-// fp32 atomic adds here made theta depend on the atomics' order: a batch and a one-image run
-// could pick another bin near the threshold (a batch-vs-single mismatch seen once in ~20 runs).
+// a uint64 that atomics add in any order to the same result) x 2^(exponent - 150); every
+// launch split therefore gives the same theta bits (batch vs single image, sharding).
+// =====================================================================================
+constexpr int kSelBins = 2048;
+constexpr int kSelHistThreads = 256;
+struct L1State {
+  unsigned prefix;
+  unsigned done;          // theta already decided (eta <= 0, inside the ball, or last level)
+  double Khi, Shi;        // count / sum of |v| strictly above the current candidate range
+};
+struct L1Scratch {        // per image, in HBM
+  L1State st;
+  unsigned cnt[kSelBins];
+  unsigned long long sm[kSelBins];
+};
+
 __device__ __forceinline__ unsigned sel_significand(unsigned u) {
   const unsigned e = u >> 23, m = u & 0x7fffffu;
   return e ? (m | 0x800000u) : m;
@@ -508,109 +519,143 @@ __device__ __forceinline__ unsigned sel_significand(unsigned u) {
 template <int SH>
 __device__ __forceinline__ double sel_bin_sum(const unsigned long long* sm, unsigned prefix, int j) {
   const int e = (int)(((prefix | ((unsigned)j << SH)) >> 23) & 0xffu);
-  // exact while n < 2^29 (a bin's significand sum < n * 2^24 <= 2^53); launch_l1_select's
-  // callers reject larger images (kMaxL1Elems)
+  // exact while n < 2^29 (a bin's significand sum < n * 2^24 <= 2^53); the callers of
+  // launch_l1_select reject larger images (kMaxL1Elems)
   return ldexp((double)sm[j], e ? e - 150 : -149);
 }
 
 template <int SH, int NBITS>
-__device__ __forceinline__ void select_level(const unsigned* __restrict__ vb, size_t n, double eta,
-                                             unsigned& prefix, double& Khi, double& Shi, unsigned* cnt,
-                                             unsigned long long* sm, int* s_j, double* s_KS) {
+__global__ __launch_bounds__(kSelHistThreads) void l1_hist_kernel(const float* __restrict__ v, size_t n, size_t chunk,
+                                                                  L1Scratch* __restrict__ scr, double eta) {
   constexpr int nb = 1 << NBITS;
   constexpr unsigned hi_mask = (SH + NBITS >= 31) ? 0u : (0x7fffffffu & ~((1u << (SH + NBITS)) - 1u));
-  for (int j = threadIdx.x; j < nb; j += kSelThreads) { cnt[j] = 0; sm[j] = 0ull; }
+  __shared__ unsigned cnt[nb];
+  __shared__ unsigned long long sm[nb];
+  const int b = blockIdx.y;
+  L1Scratch* sc = scr + b;
+  if (!(eta > 0.0) || sc->st.done) return;
+  const unsigned prefix = sc->st.prefix;
+  for (int j = threadIdx.x; j < nb; j += kSelHistThreads) { cnt[j] = 0; sm[j] = 0ull; }
   __syncthreads();
-  for (size_t i = threadIdx.x; i < n; i += kSelThreads) {
-    const unsigned u = vb[i] & 0x7fffffffu;
+  const size_t lo = (size_t)blockIdx.x * chunk, hi = min(n, lo + chunk);
+  const unsigned* vb = reinterpret_cast<const unsigned*>(v + (size_t)b * n);
+  auto bin = [&](unsigned u) {
+    u &= 0x7fffffffu;
     if ((u & hi_mask) == prefix) {
       const unsigned j = (u >> SH) & (unsigned)(nb - 1);
       atomicAdd(&cnt[j], 1u);
       atomicAdd(&sm[j], (unsigned long long)sel_significand(u));   // exact, so order-independent
     }
-  }
-  __syncthreads();
-  if (threadIdx.x < 64) {                      // wave 0: suffix scan over the bins from the top
-    constexpr int per = nb / 64;
-    const int lane = threadIdx.x;
-    double kc = 0, sc = 0;
-    for (int q = 0; q < per; ++q) { kc += cnt[lane * per + q]; sc += sel_bin_sum<SH>(sm, prefix, lane * per + q); }
-    double ks = kc, ss = sc;                   // inclusive suffix over lanes lane..63
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const double tk = __shfl_down(ks, off, 64), ts = __shfl_down(ss, off, 64);
-      if (lane + off < 64) { ks += tk; ss += ts; }
+  };
+  size_t i = lo;
+  if ((((uintptr_t)(vb + lo)) & 15) == 0) {     // 16-B loads over the aligned body of the slice
+    typedef unsigned u4v_t __attribute__((ext_vector_type(4)));
+    const u4v_t* v4 = reinterpret_cast<const u4v_t*>(vb + lo);
+    const size_t n4 = (hi - lo) / 4;
+    for (size_t k = threadIdx.x; k < n4; k += kSelHistThreads) {
+      const u4v_t q = __builtin_nontemporal_load(v4 + k);
+      bin(q.x); bin(q.y); bin(q.z); bin(q.w);
     }
-    double K = Khi + ks - kc, S = Shi + ss - sc;   // strictly above this lane's bins
-    int found = -1;
-    double fK = 0, fS = 0;
-    for (int q = per - 1; q >= 0; --q) {
-      const int j = lane * per + q;
-      const double K2 = K + cnt[j], S2 = S + sel_bin_sum<SH>(sm, prefix, j);
-      const double lo = (double)__uint_as_float(prefix | ((unsigned)j << SH));
-      if (S2 - K2 * lo - eta >= 0.0) { found = j; fK = K; fS = S; break; }
-      K = K2; S = S2;
-    }
-    int best = found;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) best = max(best, __shfl_xor(best, off, 64));
-    if (best >= 0 && found == best) { *s_j = best; s_KS[0] = fK; s_KS[1] = fS; }
-    if (best < 0 && lane == 0) {               // approximate sums missed: take bin 0
-      *s_j = 0;
-      s_KS[0] = K; s_KS[1] = S;                // lane 0's K/S after its loop = all bins >= 1 ... plus bin 0
-    }
+    i = lo + 4 * n4;
   }
+  for (size_t k = i + threadIdx.x; k < hi; k += kSelHistThreads) bin(vb[k]);
   __syncthreads();
-  if (*s_j == 0 && threadIdx.x == 0) {         // "above bin 0" = Khi + all bins >= 1, exactly
-    double K = Khi, S = Shi;
-    for (int j = nb - 1; j >= 1; --j) { K += cnt[j]; S += sel_bin_sum<SH>(sm, prefix, j); }
-    s_KS[0] = K; s_KS[1] = S;
-  }
-  __syncthreads();
-  prefix |= (unsigned)(*s_j) << SH;
-  Khi = s_KS[0];
-  Shi = s_KS[1];
-  __syncthreads();
+  for (int j = threadIdx.x; j < nb; j += kSelHistThreads)
+    if (cnt[j]) {
+      atomicAdd(&sc->cnt[j], cnt[j]);
+      atomicAdd(&sc->sm[j], sm[j]);
+    }
 }
 
-__global__ __launch_bounds__(kSelThreads) void l1_select_kernel(const float* __restrict__ v, float* __restrict__ theta,
-                                                                 size_t n, double eta) {
-  __shared__ unsigned cnt[2048];
-  __shared__ unsigned long long sm[2048];
-  __shared__ double red[8];
-  __shared__ int s_j;
-  __shared__ double s_KS[2];
-  const int b = blockIdx.x;
-  const unsigned* vb = reinterpret_cast<const unsigned*>(v + (size_t)b * n);
-  if (!(eta > 0.0)) {                         // eta == 0: projection onto {0}
-    if (threadIdx.x == 0) theta[b] = __builtin_inff();
-    return;
+// One wave per image: scan the level's bins from the top, keep the highest bin whose lower
+// edge has f >= 0, clear the bins for the next level.  Level 1 (FIRST) first decides
+// eta <= 0 (projection onto {0}: theta = inf) and sum |v| <= eta (inside: theta = 0); the
+// last level writes theta.
+template <int SH, int NBITS, bool FIRST, bool LAST>
+__global__ __launch_bounds__(64) void l1_pick_kernel(L1Scratch* __restrict__ scr, float* __restrict__ theta,
+                                                     double eta) {
+  constexpr int nb = 1 << NBITS, per = nb / 64;
+  const int b = blockIdx.x, lane = threadIdx.x;
+  L1Scratch* sc = scr + b;
+  if (sc->st.done) return;
+  const unsigned prefix = sc->st.prefix;
+  const double Khi = sc->st.Khi, Shi = sc->st.Shi;
+  unsigned* cnt = sc->cnt;
+  const unsigned long long* sm = sc->sm;
+  double kc = 0, sc_ = 0;
+  unsigned c[per];
+  double sv[per];
+#pragma unroll
+  for (int q = 0; q < per; ++q) {
+    c[q] = cnt[lane * per + q];
+    sv[q] = sel_bin_sum<SH>(sm, prefix, lane * per + q);
+    kc += c[q];
+    sc_ += sv[q];
   }
-  double tot = 0;
-  for (size_t i = threadIdx.x; i < n; i += kSelThreads) tot += (double)__uint_as_float(vb[i] & 0x7fffffffu);
-  tot = block_sum_sel(tot, red);
-  if (tot <= eta) {                            // already inside the ball: theta = 0
-    if (threadIdx.x == 0) theta[b] = 0.f;
-    return;
+  if (FIRST) {
+    double tot = sc_;                           // fixed-order sum of exact bin sums
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) tot += __shfl_xor(tot, off, 64);
+    const bool zero_ball = !(eta > 0.0), inside = tot <= eta;
+    if (zero_ball || inside) {
+      for (int q = 0; q < per; ++q) { cnt[lane * per + q] = 0; sc->sm[lane * per + q] = 0ull; }
+      if (lane == 0) {
+        theta[b] = zero_ball ? __builtin_inff() : 0.f;
+        sc->st.done = 1;
+      }
+      return;
+    }
   }
-  unsigned prefix = 0;
-  double Khi = 0, Shi = 0;                     // candidates strictly above the current range
-  select_level<20, 11>(vb, n, eta, prefix, Khi, Shi, cnt, sm, &s_j, s_KS);
-  select_level<9, 11>(vb, n, eta, prefix, Khi, Shi, cnt, sm, &s_j, s_KS);
-  select_level<0, 9>(vb, n, eta, prefix, Khi, Shi, cnt, sm, &s_j, s_KS);
-  // exact pass: elements strictly greater than the selected float value `prefix`
-  double K = 0, S = 0;
-  for (size_t i = threadIdx.x; i < n; i += kSelThreads) {
-    const unsigned u = vb[i] & 0x7fffffffu;
-    if (u > prefix) { K += 1.0; S += (double)__uint_as_float(u); }
+  double ks = kc, ss = sc_;                     // inclusive suffix over lanes lane..63
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const double tk = __shfl_down(ks, off, 64), ts = __shfl_down(ss, off, 64);
+    if (lane + off < 64) { ks += tk; ss += ts; }
   }
-  K = block_sum_sel(K, red);
-  S = block_sum_sel(S, red);
-  if (threadIdx.x == 0) {
-    const double th = K > 0 ? (S - eta) / K : (double)__uint_as_float(prefix);
-    theta[b] = (float)(th > 0 ? th : 0.0);
+  double K = Khi + ks - kc, S = Shi + ss - sc_;   // strictly above this lane's bins
+  int found = -1;
+  double fK = 0, fS = 0;
+  for (int q = per - 1; q >= 0; --q) {
+    const int j = lane * per + q;
+    const double K2 = K + c[q], S2 = S + sv[q];
+    const double lo = (double)__uint_as_float(prefix | ((unsigned)j << SH));
+    if (S2 - K2 * lo - eta >= 0.0) { found = j; fK = K; fS = S; break; }
+    K = K2; S = S2;
+  }
+  int best = found;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) best = max(best, __shfl_xor(best, off, 64));
+  // bin 0 as the fallback (exact sums make it unreachable: the parent bin had f(lo) >= 0):
+  // "above bin 0" = Khi + all bins >= 1, summed in the same fixed order as the scan
+  const int own = best >= 0 ? (found == best) : (lane == 0);
+  double nK = fK, nS = fS;
+  if (best < 0 && lane == 0) {
+    nK = Khi; nS = Shi;
+    for (int j = nb - 1; j >= 1; --j) { nK += cnt[j]; nS += sel_bin_sum<SH>(sm, prefix, j); }
+  }
+  const int jsel = best >= 0 ? best : 0;
+  __syncthreads();                              // every lane has read its bins
+  for (int q = 0; q < per; ++q) { cnt[lane * per + q] = 0; sc->sm[lane * per + q] = 0ull; }
+  if (own) {
+    const unsigned np = prefix | ((unsigned)jsel << SH);
+    if (LAST) {
+      const double th = nK > 0 ? (nS - eta) / nK : (double)__uint_as_float(np);
+      theta[b] = (float)(th > 0 ? th : 0.0);
+      sc->st.done = 1;
+    } else {
+      sc->st.prefix = np;
+      sc->st.Khi = nK;
+      sc->st.Shi = nS;
+    }
   }
 }
+
+__global__ void l1_reset_kernel(L1Scratch* __restrict__ scr, int B) {
+  const int b = blockIdx.x * 64 + threadIdx.x;
+  if (b < B) scr[b].st = L1State{0u, 0u, 0.0, 0.0};
+}
+
+size_t l1_select_scratch_bytes(int B) { return (size_t)B * sizeof(L1Scratch); }
 
 // =====================================================================================
 // Standalone operators (pnp_op_*): stencil, l2 projection, shrink, GKL, PSNR, packing.
@@ -1519,8 +1564,25 @@ void launch_k3(int method, float* y, const float* xobs, const double* partials, 
                      metrics, it, cap, record, has_true);
 }
 
-void launch_l1_select(const float* v, float* theta, int B, size_t n, double eta, hipStream_t st) {
-  hipLaunchKernelGGL(l1_select_kernel, dim3(B), dim3(kSelThreads), 0, st, v, theta, n, eta);
+void launch_l1_select(const float* v, float* theta, void* scratch, int B, size_t n, double eta, hipStream_t st) {
+  L1Scratch* scr = reinterpret_cast<L1Scratch*>(scratch);
+  // per-image state reset (the bins are left cleared by every pick launch; zeroed at allocation)
+  hipLaunchKernelGGL(l1_reset_kernel, dim3((B + 63) / 64), dim3(64), 0, st, scr, B);
+  // workgroups per image: B x G >= 512 (two per CU), slices of >= 16K elements, 16-B aligned
+  int G = (512 + B - 1) / B;
+  const int gmax = (int)((n + 16383) / 16384);
+  G = G < gmax ? G : gmax;
+  G = G > 0 ? G : 1;
+  size_t chunk = (n + G - 1) / G;
+  chunk = (chunk + 3) & ~(size_t)3;
+  G = (int)((n + chunk - 1) / chunk);
+  const dim3 hg(G, B);
+  hipLaunchKernelGGL((l1_hist_kernel<20, 11>), hg, dim3(kSelHistThreads), 0, st, v, n, chunk, scr, eta);
+  hipLaunchKernelGGL((l1_pick_kernel<20, 11, true, false>), dim3(B), dim3(64), 0, st, scr, theta, eta);
+  hipLaunchKernelGGL((l1_hist_kernel<9, 11>), hg, dim3(kSelHistThreads), 0, st, v, n, chunk, scr, eta);
+  hipLaunchKernelGGL((l1_pick_kernel<9, 11, false, false>), dim3(B), dim3(64), 0, st, scr, theta, eta);
+  hipLaunchKernelGGL((l1_hist_kernel<0, 9>), hg, dim3(kSelHistThreads), 0, st, v, n, chunk, scr, eta);
+  hipLaunchKernelGGL((l1_pick_kernel<0, 9, false, true>), dim3(B), dim3(64), 0, st, scr, theta, eta);
 }
 
 void launch_op_phi(int kind, int adj, const float* x, float* out, const OpDesc& op, int BC, int H, int W,
