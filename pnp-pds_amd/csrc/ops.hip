@@ -948,14 +948,31 @@ __device__ __forceinline__ void st2g(float* __restrict__ p, size_t idx, const f2
 }
 constexpr int kRbBatch = 2;                   // epilogue rows whose loads are in flight together (2: 0.351 ms K2, 4: 0.366, 1 per pixel before: 0.392)
 
+// Epilogue rows of a thread: rows i0 + 8ty + r, columns j, j + 1 (nv(r) valid of 2); the
+// per-row index and count are recomputed (two registers live instead of sixteen).
+struct RbRows {
+  size_t base;        // plane_base + row0 * W + j
+  int rows_left, ncol, W;
+  __device__ __forceinline__ void init(size_t plane_base, int i0, int j, int H, int W_) {
+    const int row0 = i0 + (threadIdx.x >> 5) * kRbRows;
+    W = W_;
+    ncol = j < W ? min(2, W - j) : 0;
+    rows_left = H - row0;
+    base = plane_base + (size_t)row0 * W + j;
+  }
+  __device__ __forceinline__ int nv(int r) const { return r < rows_left ? ncol : 0; }
+  __device__ __forceinline__ size_t ix(int r) const { return base + (size_t)(r < rows_left ? r : 0) * W; }
+};
+
 // K1: u = [clamp](x - g1 Phi^T y) -> u32 and its channel of the NHWC4 fp16 denoiser input
-// u16 (2-byte stores); B: w = s - g1 y.  Block = one (plane, 64 x 64 tile).
-template <class T>
+// u16 (2-byte stores); B (MB): w = s - g1 y.  Block = one (plane, 64 x 64 tile).  B's y comes
+// from the halo in LDS (it is the stencil's input), so K1 reads y once.
+template <class T, bool MB>
 __global__ __launch_bounds__(256) void k1_blur_rb(const float* __restrict__ x, const float* __restrict__ y,
                                                    const float* __restrict__ s, float* __restrict__ u32,
                                                    half_t* __restrict__ u16, float* __restrict__ w,
                                                    const f2_t* __restrict__ wd_adj, int C, int H, int W, int tiles_x,
-                                                   int tiles, float gamma1, int clamp_in, int method_b) {
+                                                   int tiles, float gamma1, int clamp_in) {
   using G = TapGeom<T>;
   __shared__ float lds[G::N];
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
@@ -964,53 +981,107 @@ __global__ __launch_bounds__(256) void k1_blur_rb(const float* __restrict__ x, c
   rb_tile_origin(blockIdx.x - bc * tiles, tiles_x, i0, j0);
   const int j = j0 + 2 * tx;
   const size_t pb = (size_t)bc * H * W;
+  const bool al = (W & 1) == 0;              // column pairs 8-B aligned
+  RbRows rw;
+  rw.init(pb, i0, j, H, W);
   const float* yp = y + pb;
   rb_fill_batch<G, 0>(lds, i0, j0, H, W, [&](int k) { return yp[k]; }, [](int) { return 0.f; },
                       [](float a, float) { return a; });
   __syncthreads();
   f2_t g[kRbRows];
   rb_stencil<T>(lds, wd_adj, g);
-  const int ncol = j < W ? min(2, W - j) : 0;
-  const bool al = (W & 1) == 0;              // column pairs 8-B aligned
+  const float* yc = lds + (ty * kRbRows + G::R) * G::LW + 2 * tx + G::R - G::kOff;   // y at (row 0, col j)
 #pragma unroll
-  for (int rb = 0; rb < kRbRows; rb += kRbBatch) {   // batched loads, as in k2_blur_rb
-    f2_t xv[kRbBatch], sv[kRbBatch], yv[kRbBatch];
-    int nv[kRbBatch];
-    size_t ix[kRbBatch];
+  for (int rb = 0; rb < kRbRows; rb += kRbBatch) {   // the loads of kRbBatch rows in flight together
+    f2_t xv[kRbBatch], sv[kRbBatch];
 #pragma unroll
     for (int k = 0; k < kRbBatch; ++k) {
-      const int i = i0 + ty * kRbRows + rb + k;
-      nv[k] = i < H ? ncol : 0;
-      ix[k] = pb + (size_t)min(i, H - 1) * W + j;
-      const bool vec = al && nv[k] == 2;
-      xv[k] = ld2g(x, ix[k], nv[k], vec);
-      if (method_b) {
-        sv[k] = ld2g(s, ix[k], nv[k], vec);
-        yv[k] = ld2g(y, ix[k], nv[k], vec);
-      }
+      const bool vec = al && rw.nv(rb + k) == 2;
+      xv[k] = ld2g(x, rw.ix(rb + k), rw.nv(rb + k), vec);
+      if (MB) sv[k] = ld2g(s, rw.ix(rb + k), rw.nv(rb + k), vec);
     }
 #pragma unroll
     for (int k = 0; k < kRbBatch; ++k) {
-      const int i = i0 + ty * kRbRows + rb + k;
+      const int r = rb + k, i = i0 + ty * kRbRows + r;
       f2_t uo, wo;
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
-        float uu = xv[k][q] - gamma1 * g[rb + k][q];
+        float uu = xv[k][q] - gamma1 * g[r][q];
         if (clamp_in) uu = fminf(fmaxf(uu, 0.f), 1.f);
         uo[q] = uu;
-        if (q < nv[k]) u16[(((size_t)b * (H + 2) + i + 1) * (W + 2) + j + q + 1) * 4 + c] = (half_t)uu;
-        wo[q] = sv[k][q] - gamma1 * yv[k][q];
+        if (q < rw.nv(r)) u16[(((size_t)b * (H + 2) + i + 1) * (W + 2) + j + q + 1) * 4 + c] = (half_t)uu;
+        if (MB) wo[q] = sv[k][q] - gamma1 * yc[r * G::LW + q];
       }
-      const bool vec = al && nv[k] == 2;
-      st2g(u32, ix[k], uo, nv[k], vec);
-      if (method_b) st2g(w, ix[k], wo, nv[k], vec);
+      const bool vec = al && rw.nv(r) == 2;
+      st2g(u32, rw.ix(r), uo, rw.nv(r), vec);
+      if (MB) st2g(w, rw.ix(r), wo, rw.nv(r), vec);
     }
   }
 }
 
+// K2 halo fill of 2 xn - xo (Phi's argument) that also accumulates the metric sums of the
+// tile's own pixels from the same loads: e2 = sum (xn - xo)^2, n2 = sum xo^2 (c_n,
+// iteration.py:187) and t2 = sum (xt - xn)^2 (PSNR, :188; x_true loaded for those pixels
+// only).  Each batch's <= kRbFill terms are summed in fp32, then added once into fp64.
+template <class G, int K0 = 0>
+__device__ __forceinline__ void rb_fill_k2(float* lds, int i0, int j0, int H, int W, const float* xnp,
+                                           const float* xop, const float* xtp, bool record, double& e2, double& n2,
+                                           double& t2) {
+  constexpr int K1 = K0 + kRbFill < G::NF ? K0 + kRbFill : G::NF;
+  const int tid = threadIdx.x;
+  const int ly0 = tid / G::LW, lx0 = tid - ly0 * G::LW;
+  const int ci = i0 - G::R, cj = j0 - G::R + G::kOff;
+  const int ie = min(i0 + kRbH, H), je = min(j0 + kRbW, W);
+  float a[kRbFill], bb[kRbFill], t[kRbFill];
+  bool in[kRbFill];
+#pragma unroll
+  for (int k = K0; k < K1; ++k) {
+    const int dy = (256 * k) / G::LW, dx = (256 * k) % G::LW;
+    int lx = lx0 + dx, ly = ly0 + dy;
+    const bool carry = lx >= G::LW;
+    lx = carry ? lx - G::LW : lx;
+    ly = carry ? ly + 1 : ly;
+    const bool valid = G::N % 256 == 0 || tid + 256 * k < G::N;
+    ly = min(ly, G::LH - 1);
+    const int ui = ci + ly, uj = cj + lx;      // unwrapped image coordinates
+    int gi = ui, gj = uj;
+    gi += gi < 0 ? H : 0;
+    gi -= gi >= H ? H : 0;
+    gj += gj < 0 ? W : 0;
+    gj -= gj >= W ? W : 0;
+    gi = min(max(gi, 0), H - 1);
+    gj = min(max(gj, 0), W - 1);
+    const int idx = gi * W + gj;
+    a[k - K0] = xnp[idx];
+    bb[k - K0] = xop[idx];
+    in[k - K0] = record && valid && ui >= i0 && ui < ie && uj >= j0 && uj < je;
+    t[k - K0] = (in[k - K0] && xtp) ? xtp[idx] : 0.f;
+  }
+  float be = 0.f, bn = 0.f, bt = 0.f;
+#pragma unroll
+  for (int k = K0; k < K1; ++k) {
+    const int q = tid + 256 * k;
+    const float av = a[k - K0], bv = bb[k - K0];
+    if (G::N % 256 == 0 || q < G::N) lds[q] = 2.f * av - bv;
+    const float d = in[k - K0] ? av - bv : 0.f, o = in[k - K0] ? bv : 0.f;
+    const float tt = in[k - K0] ? t[k - K0] - av : 0.f;
+    be = fmaf(d, d, be);
+    bn = fmaf(o, o, bn);
+    bt = fmaf(tt, tt, bt);
+  }
+  e2 += be;
+  n2 += bn;
+  t2 += bt;
+  if constexpr (K1 < G::NF) rb_fill_k2<G, K1>(lds, i0, j0, H, W, xnp, xop, xtp, record, e2, n2, t2);
+}
+
 // K2: v = y + g2 (Phi(2x+ - x) [+ 2 s+ - s]), s+ = shrink(w, theta) (B), the GKL prox (C),
-// per-cell partial sums.  Block = one (plane, 64 x 64 tile).  partials: [B][cells][C][4]
-// (per 32 x 32 cell and channel), reduced by k3 in that order.
+// per-cell partial sums.  Block = one (plane, 64 x 64 tile).  The metric sums come from the
+// fill's own loads of xn / xo (plus x_true for the tile's pixels) and are reduced before the
+// barrier (no fill value stays live through the stencil), so the epilogue reads only y and
+// x_obs (and B's s, w) and nothing is read twice.  partials: [B][cells][C][4] (per 32 x 32
+// cell and channel), reduced by k3 in that order: d2 per cell, e2 / n2 / t2 per tile in the
+// tile's first cell (zeros in the others).
 template <class T, int METHOD>
 __global__ __launch_bounds__(256) void k2_blur_rb(const float* __restrict__ xn, const float* __restrict__ xo,
                                                    float* __restrict__ y, const float* __restrict__ xobs,
@@ -1022,60 +1093,57 @@ __global__ __launch_bounds__(256) void k2_blur_rb(const float* __restrict__ xn, 
                                                    int record) {
   using G = TapGeom<T>;
   __shared__ float lds[G::N];
-  __shared__ double red[8][2][4];
-  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  __shared__ double red[4][2];
+  __shared__ double redm[4][3];
+  const int tx = threadIdx.x & 31;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int bc = blockIdx.x / tiles, b = bc / C, c = bc - b * C;
   int i0, j0;
   rb_tile_origin(blockIdx.x - bc * tiles, tiles_x, i0, j0);
   const size_t plane = (size_t)H * W;
+  const int j = j0 + 2 * tx;
+  const bool al = (W & 1) == 0;              // column pairs 8-B aligned
+  RbRows rw;
+  rw.init((size_t)bc * plane, i0, j, H, W);
   {
-    const float* xnp = xn + (size_t)bc * plane;
-    const float* xop = xo + (size_t)bc * plane;
-    rb_fill_batch<G, 0>(lds, i0, j0, H, W, [&](int k) { return xnp[k]; }, [&](int k) { return xop[k]; },
-                        [](float a, float b) { return 2.f * a - b; });   // Phi(2x+ - x)'s argument
+    double e2 = 0, n2 = 0, t2 = 0;
+    rb_fill_k2<G>(lds, i0, j0, H, W, xn + (size_t)bc * plane, xo + (size_t)bc * plane,
+                  xtrue ? xtrue + (size_t)bc * plane : nullptr, record != 0, e2, n2, t2);
+    if (record) {                            // reduced here, so no fill value stays live past the fill
+      e2 = wave_sum(e2);
+      n2 = wave_sum(n2);
+      t2 = wave_sum(t2);
+      if (lane == 0) { redm[wave][0] = e2; redm[wave][1] = n2; redm[wave][2] = t2; }
+    }
   }
   __syncthreads();
   f2_t g[kRbRows];
   rb_stencil<T>(lds, wd_fwd, g);
+  double d2 = 0;
   {
-    double d2 = 0, e2 = 0, n2 = 0, t2 = 0;
     const float th = METHOD == M_B ? theta[b] : 0.f;
-    const int j = j0 + 2 * tx;
-    const int ncol = j < W ? min(2, W - j) : 0;
-    const bool al = (W & 1) == 0;            // column pairs 8-B aligned
-    // kRbBatch rows at a time: every stream's loads of the batch are issued before the first
-    // use (the per-pixel form waited on each load in turn: y is read and written).
+    // kRbBatch rows at a time: every stream's loads of the batch are issued before the first use
 #pragma unroll
     for (int rb = 0; rb < kRbRows; rb += kRbBatch) {
-      f2_t yv[kRbBatch], bv[kRbBatch], av[kRbBatch], ov[kRbBatch], tv[kRbBatch], sv[kRbBatch], wv[kRbBatch];
-      int nv[kRbBatch];
-      size_t ix[kRbBatch];
+      f2_t yv[kRbBatch], bv[kRbBatch], sv[kRbBatch], wv[kRbBatch];
 #pragma unroll
       for (int k = 0; k < kRbBatch; ++k) {
-        const int i = i0 + ty * kRbRows + rb + k;
-        nv[k] = i < H ? ncol : 0;
-        ix[k] = (size_t)bc * plane + (size_t)min(i, H - 1) * W + j;
-        const bool vec = al && nv[k] == 2;
-        yv[k] = ld2g(y, ix[k], nv[k], vec);
-        bv[k] = ld2g(xobs, ix[k], nv[k], vec);
+        const bool vec = al && rw.nv(rb + k) == 2;
+        yv[k] = ld2g(y, rw.ix(rb + k), rw.nv(rb + k), vec);
+        bv[k] = ld2g(xobs, rw.ix(rb + k), rw.nv(rb + k), vec);
         if (METHOD == M_B) {
-          sv[k] = ld2g(s, ix[k], nv[k], vec);
-          wv[k] = ld2g(w, ix[k], nv[k], vec);
-        }
-        if (record) {
-          av[k] = ld2g(xn, ix[k], nv[k], vec);
-          ov[k] = ld2g(xo, ix[k], nv[k], vec);
-          tv[k] = xtrue ? ld2g(xtrue, ix[k], nv[k], vec) : f2_t{0.f, 0.f};
+          sv[k] = ld2g(s, rw.ix(rb + k), rw.nv(rb + k), vec);
+          wv[k] = ld2g(w, rw.ix(rb + k), rw.nv(rb + k), vec);
         }
       }
 #pragma unroll
       for (int k = 0; k < kRbBatch; ++k) {
+        const int r = rb + k;
         f2_t yo = yv[k], so = {0.f, 0.f};
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
-          if (q >= nv[k]) break;
-          double gv = g[rb + k][q];
+          if (q >= rw.nv(r)) break;
+          double gv = g[r][q];
           if (METHOD == M_B) {
             const float wq = wv[k][q];
             const float sp = copysignf(fmaxf(fabsf(wq) - th, 0.f), wq);   // operators.py:98
@@ -1093,46 +1161,33 @@ __global__ __launch_bounds__(256) void k2_blur_rb(const float* __restrict__ xn, 
             const double dd = v * inv_g2 - ob;
             d2 += dd * dd;
           }
-          if (record) {
-            const double a = av[k][q], o = ov[k][q];
-            e2 += (a - o) * (a - o);
-            n2 += o * o;
-            if (xtrue) {
-              const double qv = (double)tv[k][q] - a;
-              t2 += qv * qv;
-            }
-          }
         }
-        const bool vec = al && nv[k] == 2;
-        st2g(y, ix[k], yo, nv[k], vec);
-        if (METHOD == M_B) st2g(s, ix[k], so, nv[k], vec);
+        const bool vec = al && rw.nv(r) == 2;
+        st2g(y, rw.ix(r), yo, rw.nv(r), vec);
+        if (METHOD == M_B) st2g(s, rw.ix(r), so, rw.nv(r), vec);
       }
     }
-    // 32 x 32 cell = 16 threads (tx) x 4 thread rows (ty) = two half-cells of two waves:
-    // reduce each half in its wave (lanes {c, c+32}: xor 32, then xor 8..1), then combine
-    // the two waves' halves through LDS in a fixed order.
-    auto half_sum = [](double v) {
-      v += __shfl_xor(v, 32, 64);
+  }
+  // d2: 32 x 32 cell = 16 threads (tx) x 4 thread rows (ty) = two half-cells of two waves:
+  // reduce each half in its wave (lanes {c, c+32}: xor 32, then xor 8..1), then combine the
+  // two waves' halves through LDS in a fixed order.  e2 / n2 / t2: whole tile, fixed order.
+  auto half_sum = [](double v) {
+    v += __shfl_xor(v, 32, 64);
 #pragma unroll
-      for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-      return v;
-    };
-    d2 = half_sum(d2);
-    e2 = half_sum(e2);
-    n2 = half_sum(n2);
-    t2 = half_sum(t2);
-    if ((lane & 47) == 0) {                              // lanes 0 and 16: the wave's two half-cells
-      double* q = red[wave][lane >> 4];
-      q[0] = d2; q[1] = e2; q[2] = n2; q[3] = t2;
-    }
-    __syncthreads();
-    if (threadIdx.x < 16) {                              // 2 x 2 cells x 4 sums
-      const int cell = threadIdx.x >> 2, k = threadIdx.x & 3, cy = cell >> 1, cx = cell & 1;
-      const int gy = i0 / 32 + cy, gx = j0 / 32 + cx;
-      if (gy * 32 < H && gx < cells_x)
-        partials[(((size_t)b * cells + (size_t)gy * cells_x + gx) * C + c) * 4 + k] =
-            red[2 * cy][cx][k] + red[2 * cy + 1][cx][k];
-    }
+    for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+  };
+  d2 = half_sum(d2);
+  if ((lane & 47) == 0) red[wave][lane >> 4] = d2;   // lanes 0 / 16: the wave's two half-cells
+  __syncthreads();
+  if (threadIdx.x < 16) {                              // 2 x 2 cells x 4 sums
+    const int cell = threadIdx.x >> 2, k = threadIdx.x & 3, cy = cell >> 1, cx = cell & 1;
+    const int gy = i0 / 32 + cy, gx = j0 / 32 + cx;
+    double v = 0.0;
+    if (k == 0) v = red[2 * cy][cx] + red[2 * cy + 1][cx];
+    else if (record && cell == 0) v = ((redm[0][k - 1] + redm[1][k - 1]) + redm[2][k - 1]) + redm[3][k - 1];
+    if (gy * 32 < H && gx < cells_x)
+      partials[(((size_t)b * cells + (size_t)gy * cells_x + gx) * C + c) * 4 + k] = v;
   }
 }
 
@@ -1412,8 +1467,12 @@ static void launch_k1_rb(hipStream_t st, const float* x, const float* y, const f
                          float* w, const OpDesc& op, int B, int C, int H, int W, float gamma1, int clamp_in,
                          int method_b) {
   const int tx = (W + kRbW - 1) / kRbW, tiles = tx * ((H + kRbH - 1) / kRbH);
-  hipLaunchKernelGGL((k1_blur_rb<T>), dim3(B * C * tiles), dim3(256), 0, st, x, y, s, u32, u16, w,
-                     reinterpret_cast<const f2_t*>(op.dense_adj), C, H, W, tx, tiles, gamma1, clamp_in, method_b);
+  if (method_b)
+    hipLaunchKernelGGL((k1_blur_rb<T, true>), dim3(B * C * tiles), dim3(256), 0, st, x, y, s, u32, u16, w,
+                       reinterpret_cast<const f2_t*>(op.dense_adj), C, H, W, tx, tiles, gamma1, clamp_in);
+  else
+    hipLaunchKernelGGL((k1_blur_rb<T, false>), dim3(B * C * tiles), dim3(256), 0, st, x, y, s, u32, u16, w,
+                       reinterpret_cast<const f2_t*>(op.dense_adj), C, H, W, tx, tiles, gamma1, clamp_in);
 }
 
 void launch_k1(int kind, const float* x, const float* y, const float* s, float* u32, half_t* u16, float* w,
