@@ -906,7 +906,10 @@ __device__ __forceinline__ void rb_gather(int i0, int j0, int H, int W, F&& load
 // Halo fill: batches of kRbFill elements per thread (the loads of a batch in flight
 // together, then their LDS stores), so few registers are live and 6 blocks fit per CU.  val(a, b) combines the values of the two source
 // planes (b is unused for one-plane fills).
-constexpr int kRbFill = 8;
+#ifndef PNP_RB_FILL
+#define PNP_RB_FILL 8        // A/B builds only
+#endif
+constexpr int kRbFill = PNP_RB_FILL;
 template <class G, int K0, class FA, class FB, class FV>
 __device__ __forceinline__ void rb_fill_batch(float* lds, int i0, int j0, int H, int W, FA&& la, FB&& lb, FV&& val) {
   constexpr int K1 = K0 + kRbFill < G::NF ? K0 + kRbFill : G::NF;
@@ -946,7 +949,10 @@ __device__ __forceinline__ void st2g(float* __restrict__ p, size_t idx, const f2
   if (nv > 0) p[idx] = v.x;
   if (nv > 1) p[idx + 1] = v.y;
 }
-constexpr int kRbBatch = 2;                   // epilogue rows whose loads are in flight together (2: 0.351 ms K2, 4: 0.366, 1 per pixel before: 0.392)
+#ifndef PNP_RB_BATCH
+#define PNP_RB_BATCH 2       // A/B builds only
+#endif
+constexpr int kRbBatch = PNP_RB_BATCH;                   // epilogue rows whose loads are in flight together (2: 0.351 ms K2, 4: 0.366, 1 per pixel before: 0.392)
 
 // Epilogue rows of a thread: rows i0 + 8ty + r, columns j, j + 1 (nv(r) valid of 2); the
 // per-row index and count are recomputed (two registers live instead of sixteen).

@@ -307,7 +307,37 @@ def make_long_golden(ref_root="/root/reference", only=None):
         print(f"long_{name}.npz psnr {ps[0]:.3f} -> {ps[-1]:.3f} ({time.perf_counter()-t:.1f}s)", flush=True)
 
 
+def make_weights_pin(ref_root="/root/reference"):
+    """Pin of the simple_CNN weight conversion (tests/golden/weights_pin.json): the reference
+    loads a checkpoint with a strict load_state_dict into simple_CNN(depth=20)
+    (models/denoiser.py:18-30), so the checkpoint's parameter names, order and shapes are the
+    module's state_dict.  Recorded here: that state_dict (names + shapes, from the reference's
+    own class), and per layer the SHA-256 of our data-only reader's arrays straight from the
+    .pth; tests/test_weights_pin.py checks the shipped npz layers against both."""
+    import hashlib
+    import json
+    sys.path.insert(0, ref_root)
+    from models.basic_models import simple_CNN
+    from pnppds.weights import read_legacy_checkpoint
+    out = {}
+    for ch, name in ((3, "DnCNN_nobn_nch_3_nlev_0.01"), (1, "DnCNN_nobn_nch_1_nlev_0.01"),
+                     (1, "DnCNN_nobn_nch_1_nlev_0.009")):
+        net = simple_CNN(n_ch_in=ch, n_ch_out=ch, n_ch=64, nl_type="relu", depth=20, bn=False)
+        keys = [(k, list(v.shape)) for k, v in net.state_dict().items()]
+        raw = read_legacy_checkpoint(os.path.join(ref_root, "nn", name + ".pth"))
+        out[name] = {"module_state_dict": keys,
+                     "reader_keys": list(raw.keys()),
+                     "sha256": {k: hashlib.sha256(np.ascontiguousarray(v, np.float32).tobytes()).hexdigest()
+                                for k, v in raw.items()}}
+    with open(os.path.join(HERE, "weights_pin.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    print("weights_pin.json")
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "--weights-pin":
+        make_weights_pin(*sys.argv[2:])
+        sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "--long":
         make_long_golden(only=sys.argv[2:] or None)
         sys.exit(0)
