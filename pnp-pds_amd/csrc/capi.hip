@@ -69,6 +69,7 @@ struct pnp_ctx {
   DevBuf z, p, t;   // comparisonB-2 and the other comparison methods
   DevBuf y1, d, c1; // TV dual [B][2C][H][W]; Poisson-ADMM d and Phi^T 1
   DevBuf ssim_scr;  // SSIM partials (record_ssim)
+  DevBuf ssim_mm;   // x+ (min, max) partials written by K2 for SSIM's data_range
 
   // observation pipeline (pnp_degrade)
   DevBuf dg_words, dg_flag, dg_rank, dg_scan, dg_noise, dg_img, dg_draws, dg_first, dg_status;
@@ -352,12 +353,17 @@ double l2_eps(pnp_ctx* ctx, size_t n) {
 }
 
 // iteration.py:189: ssim_data[i] = eval_ssim(x_true, x_n), only when asked (record_ssim)
-void record_ssim(pnp_ctx* ctx, const float* xn, hipStream_t st) {
+bool want_ssim(pnp_ctx* ctx) {
   const pnp_params& p = ctx->prm;
-  if (!(p.record_metrics && p.record_ssim && ctx->has_true && ctx->it < ctx->cap)) return;
+  return p.record_metrics && p.record_ssim && ctx->has_true && ctx->it < ctx->cap;
+}
+
+// mm_chunks > 0: K2 already wrote x+'s (min, max) partials to ctx->ssim_mm
+void record_ssim(pnp_ctx* ctx, const float* xn, hipStream_t st, int mm_chunks = 0) {
+  if (!want_ssim(ctx)) return;
   ProfScope ps(ctx, "ssim", st);
   launch_ssim(P<float>(ctx->xtrue), xn, ctx->ssim_scr.p, P<double>(ctx->metrics), ctx->B, ctx->C, ctx->H, ctx->W,
-              ctx->it, ctx->cap, st);
+              ctx->it, ctx->cap, st, mm_chunks > 0 ? P<float>(ctx->ssim_mm) : nullptr, mm_chunks);
   check_launch(ctx, "ssim");
 }
 
@@ -384,13 +390,14 @@ void solver_iteration(pnp_ctx* ctx) {
     check_launch(ctx, "l1_select");
   }
   run_denoiser(ctx, P<half_t>(ctx->u16), P<float>(ctx->u32), xn, ctx->act, B, H, W, st);
+  int mm_chunks = 0;
   {
     ProfScope ps(ctx, "k2_dual", st);
     const double gkl_gamma = p.my_lambda / p.gamma2;   // iteration.py:63
-    launch_k2(od.kind, ctx->method, xn, xo, P<float>(ctx->y), P<float>(ctx->xobs),
-              ctx->has_true ? P<float>(ctx->xtrue) : nullptr, P<float>(ctx->s), P<float>(ctx->w),
-              P<float>(ctx->theta), P<double>(ctx->partials), od, B, C, H, W, p.gamma2, gkl_gamma,
-              p.poisson_alpha, record, st);
+    mm_chunks = launch_k2(od.kind, ctx->method, xn, xo, P<float>(ctx->y), P<float>(ctx->xobs),
+                          ctx->has_true ? P<float>(ctx->xtrue) : nullptr, P<float>(ctx->s), P<float>(ctx->w),
+                          P<float>(ctx->theta), P<double>(ctx->partials), od, B, C, H, W, p.gamma2, gkl_gamma,
+                          p.poisson_alpha, record, want_ssim(ctx) ? P<float>(ctx->ssim_mm) : nullptr, st);
     check_launch(ctx, "k2");
   }
   {
@@ -399,7 +406,7 @@ void solver_iteration(pnp_ctx* ctx) {
               l2_eps(ctx, n), P<double>(ctx->metrics), ctx->it, ctx->cap, record, ctx->has_true, st);
     check_launch(ctx, "k3");
   }
-  record_ssim(ctx, xn, st);
+  record_ssim(ctx, xn, st, mm_chunks);
   ctx->cur ^= 1;
   ctx->it += 1;
 }
@@ -560,7 +567,7 @@ void solver_iteration_cmp(pnp_ctx* ctx) {
       }
       launch_tv_dual(xn, xo, y1, p.gamma2, B, C, H, W, st);
       launch_k2(od.kind, mb ? PNP_METHOD_B : PNP_METHOD_A, xn, xo, y, xobs, xt, sv, w, P<float>(ctx->theta),
-                P<double>(ctx->partials), od, B, C, H, W, p.gamma2, 0.0, p.poisson_alpha, record, st);
+                P<double>(ctx->partials), od, B, C, H, W, p.gamma2, 0.0, p.poisson_alpha, record, nullptr, st);
       launch_k3(mb ? PNP_METHOD_B : PNP_METHOD_A, y, xobs, P<double>(ctx->partials), od, B, C, H, W, p.gamma2, eps,
                 P<double>(ctx->metrics), ctx->it, ctx->cap, record, ctx->has_true, st);
       break;
@@ -663,7 +670,10 @@ void solver_setup(pnp_ctx* ctx, int method, const pnp_params* params, int B, int
   ensure(ctx, ctx->partials,
          (size_t)B * std::max(partial_tiles(H, W) * C, chunk_count((size_t)C * H * W)) * 4 * sizeof(double));
   ensure(ctx, ctx->metrics, (size_t)B * std::max(ctx->cap, 1) * kMetrics * sizeof(double));
-  if (params->record_ssim) ensure(ctx, ctx->ssim_scr, ssim_scratch_bytes(B, C, H, W));
+  if (params->record_ssim) {
+    ensure(ctx, ctx->ssim_scr, ssim_scratch_bytes(B, C, H, W));
+    ensure(ctx, ctx->ssim_mm, (size_t)B * k2_minmax_chunks(C, H, W) * 2 * sizeof(float));
+  }
   ensure(ctx, ctx->theta, (size_t)B * sizeof(float));
   ctx->loaded = false;
   ctx->it = 0;
@@ -783,7 +793,7 @@ int pnp_destroy(pnp_ctx* ctx) {
                     &ctx->z, &ctx->p, &ctx->t, &ctx->dense_fwd, &ctx->dense_adj, &ctx->ssim_scr,
                     &ctx->taps64, &ctx->y1, &ctx->d, &ctx->c1, &ctx->dg_words, &ctx->dg_flag, &ctx->dg_rank, &ctx->dg_scan, &ctx->dg_noise,
                     &ctx->dg_img, &ctx->dg_draws, &ctx->dg_first, &ctx->dg_status,
-                    &ctx->head_w32, &ctx->body_w32, &ctx->tail_w32, &ctx->act32[0], &ctx->act32[1], &ctx->l1_scr};
+                    &ctx->head_w32, &ctx->body_w32, &ctx->tail_w32, &ctx->act32[0], &ctx->act32[1], &ctx->l1_scr, &ctx->ssim_mm};
   for (DevBuf* b : bufs) release(*b);
   for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);

@@ -64,10 +64,14 @@ void pack_tap_pairs(int Rd, const float* W, float* out);
 void launch_k1(int kind, const float* x, const float* y, const float* s, float* u32, half_t* u16, float* w,
                const OpDesc& op, int B, int C, int H, int W, float gamma1, int clamp_in, int method_b,
                hipStream_t st);
-void launch_k2(int kind, int method, const float* xn, const float* xo, float* y, const float* xobs,
-               const float* xtrue, float* s, const float* w, const float* theta, double* partials,
-               const OpDesc& op, int B, int C, int H, int W, double gamma2, double gkl_gamma, double gkl_alpha,
-               int record, hipStream_t st);
+// Returns the number of per-image (min, max) partials of xn it wrote to mm ([B][chunks][2]
+// floats, SSIM's data_range; mm may be null), 0 when this path does not produce them.
+int launch_k2(int kind, int method, const float* xn, const float* xo, float* y, const float* xobs,
+              const float* xtrue, float* s, const float* w, const float* theta, double* partials,
+              const OpDesc& op, int B, int C, int H, int W, double gamma2, double gkl_gamma, double gkl_alpha,
+              int record, float* mm, hipStream_t st);
+// the largest chunk count launch_k2 writes to mm
+int k2_minmax_chunks(int C, int H, int W);
 void launch_k3(int method, float* y, const float* xobs, const double* partials, const OpDesc& op, int B, int C,
                int H, int W,
                double gamma2, double eps, double* metrics, int it, int cap, int record, int has_true,
@@ -128,8 +132,9 @@ void launch_admm_poisson_step(float* x, const float* g, const float* c1, const f
 constexpr int kMetrics = 3;
 // SSIM of x against xt (utils_eval.py:9-12) into metrics[b][it][2]; scratch >= ssim_scratch_bytes
 size_t ssim_scratch_bytes(int B, int C, int H, int W);
+// mm_ext / mm_chunks: x's (min, max) partials from launch_k2, or null (then computed here)
 void launch_ssim(const float* xt, const float* x, void* scratch, double* metrics, int B, int C, int H, int W,
-                 int it, int cap, hipStream_t st);
+                 int it, int cap, hipStream_t st, const float* mm_ext = nullptr, int mm_chunks = 0);
 // comparisonB-2: out = k + ca*a + cb*b + cc*c + cd*d (null inputs skipped), fp64 arithmetic
 void launch_lincomb(float* out, double k, const float* a, double ca, const float* b, double cb, const float* c,
                     double cc, const float* d, double cd, size_t count, hipStream_t st);

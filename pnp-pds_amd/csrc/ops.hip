@@ -335,7 +335,8 @@ __global__ __launch_bounds__(256) void k2_elem(const float* __restrict__ xn, con
                                                 const float* __restrict__ w, const float* __restrict__ theta,
                                                 double* __restrict__ partials, const uint8_t* __restrict__ mask,
                                                 int Crt, int H, int W, int tiles_x, int tiles, double gamma2,
-                                                double inv_g2, double gkl_gamma, double gkl_alpha, int record) {
+                                                double inv_g2, double gkl_gamma, double gkl_alpha, int record,
+                                                float* __restrict__ mm) {
   constexpr int CM = NC ? NC : kMaxC;
   const int C = NC ? NC : Crt;
   __shared__ double red[4][4];
@@ -343,6 +344,7 @@ __global__ __launch_bounds__(256) void k2_elem(const float* __restrict__ xn, con
   const int ty = tile / tiles_x;
   const int i = ty * kST + (threadIdx.x >> 3), j = (tile - ty * tiles_x) * kST + 4 * (threadIdx.x & 7);
   double d2 = 0, e2 = 0, n2 = 0, t2 = 0;
+  float lo = __builtin_inff(), hi = -__builtin_inff();   // x+ range for SSIM's data_range
   if (i < H && j < W) {
     const int nv = min(4, W - j);
     const bool vec = (W & 3) == 0 && nv == 4;
@@ -395,6 +397,8 @@ __global__ __launch_bounds__(256) void k2_elem(const float* __restrict__ xn, con
           }
           (k == 0 ? yo.x : k == 1 ? yo.y : k == 2 ? yo.z : yo.w) = yk;
           if (record && k < nv) {
+            lo = fminf(lo, f4get(a4[c], k));
+            hi = fmaxf(hi, f4get(a4[c], k));
             const double a = f4get(a4[c], k), oo = f4get(o4[c], k);
             e2 += (a - oo) * (a - oo);
             n2 += oo * oo;
@@ -421,11 +425,26 @@ __global__ __launch_bounds__(256) void k2_elem(const float* __restrict__ xn, con
   n2 = wave_sum(n2);
   t2 = wave_sum(t2);
   const int wv = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) { red[wv][0] = d2; red[wv][1] = e2; red[wv][2] = n2; red[wv][3] = t2; }
+  __shared__ float redr[4][2];
+  if (record && mm) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      lo = fminf(lo, __shfl_xor(lo, o, 64));
+      hi = fmaxf(hi, __shfl_xor(hi, o, 64));
+    }
+  }
+  if ((threadIdx.x & 63) == 0) {
+    red[wv][0] = d2; red[wv][1] = e2; red[wv][2] = n2; red[wv][3] = t2;
+    redr[wv][0] = lo; redr[wv][1] = hi;
+  }
   __syncthreads();
   if (threadIdx.x < 4)
     partials[((size_t)b * tiles + tile) * 4 + threadIdx.x] =
         ((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x];
+  if (record && mm && threadIdx.x == 0) {    // per (image, tile): [B][tiles][2]
+    mm[((size_t)b * tiles + tile) * 2 + 0] = fminf(fminf(redr[0][0], redr[1][0]), fminf(redr[2][0], redr[3][0]));
+    mm[((size_t)b * tiles + tile) * 2 + 1] = fmaxf(fmaxf(redr[0][1], redr[1][1]), fmaxf(redr[2][1], redr[3][1]));
+  }
 }
 
 // Deterministic reduction of one image's tile partials (fixed order) in a 256-block.
@@ -1032,7 +1051,7 @@ __global__ __launch_bounds__(256) void k1_blur_rb(const float* __restrict__ x, c
 template <class G, int K0 = 0>
 __device__ __forceinline__ void rb_fill_k2(float* lds, int i0, int j0, int H, int W, const float* xnp,
                                            const float* xop, const float* xtp, bool record, double& e2, double& n2,
-                                           double& t2) {
+                                           double& t2, float& lo, float& hi) {
   constexpr int K1 = K0 + kRbFill < G::NF ? K0 + kRbFill : G::NF;
   const int tid = threadIdx.x;
   const int ly0 = tid / G::LW, lx0 = tid - ly0 * G::LW;
@@ -1074,11 +1093,13 @@ __device__ __forceinline__ void rb_fill_k2(float* lds, int i0, int j0, int H, in
     be = fmaf(d, d, be);
     bn = fmaf(o, o, bn);
     bt = fmaf(tt, tt, bt);
+    lo = in[k - K0] ? fminf(lo, av) : lo;    // x+ range for SSIM's data_range (utils_eval.py:11)
+    hi = in[k - K0] ? fmaxf(hi, av) : hi;
   }
   e2 += be;
   n2 += bn;
   t2 += bt;
-  if constexpr (K1 < G::NF) rb_fill_k2<G, K1>(lds, i0, j0, H, W, xnp, xop, xtp, record, e2, n2, t2);
+  if constexpr (K1 < G::NF) rb_fill_k2<G, K1>(lds, i0, j0, H, W, xnp, xop, xtp, record, e2, n2, t2, lo, hi);
 }
 
 // K2: v = y + g2 (Phi(2x+ - x) [+ 2 s+ - s]), s+ = shrink(w, theta) (B), the GKL prox (C),
@@ -1096,7 +1117,7 @@ __global__ __launch_bounds__(256) void k2_blur_rb(const float* __restrict__ xn, 
                                                    double* __restrict__ partials, const f2_t* __restrict__ wd_fwd,
                                                    int C, int H, int W, int tiles_x, int tiles, int cells_x, int cells,
                                                    double gamma2, double inv_g2, double gkl_gamma, double gkl_alpha,
-                                                   int record) {
+                                                   int record, float* __restrict__ mm) {
   using G = TapGeom<T>;
   __shared__ float lds[G::N];
   __shared__ double red[4][2];
@@ -1111,18 +1132,33 @@ __global__ __launch_bounds__(256) void k2_blur_rb(const float* __restrict__ xn, 
   const bool al = (W & 1) == 0;              // column pairs 8-B aligned
   RbRows rw;
   rw.init((size_t)bc * plane, i0, j, H, W);
+  __shared__ float redr[4][2];
   {
     double e2 = 0, n2 = 0, t2 = 0;
+    float lo = __builtin_inff(), hi = -__builtin_inff();
     rb_fill_k2<G>(lds, i0, j0, H, W, xn + (size_t)bc * plane, xo + (size_t)bc * plane,
-                  xtrue ? xtrue + (size_t)bc * plane : nullptr, record != 0, e2, n2, t2);
+                  xtrue ? xtrue + (size_t)bc * plane : nullptr, record != 0, e2, n2, t2, lo, hi);
     if (record) {                            // reduced here, so no fill value stays live past the fill
       e2 = wave_sum(e2);
       n2 = wave_sum(n2);
       t2 = wave_sum(t2);
       if (lane == 0) { redm[wave][0] = e2; redm[wave][1] = n2; redm[wave][2] = t2; }
+      if (mm) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+          lo = fminf(lo, __shfl_xor(lo, o, 64));
+          hi = fmaxf(hi, __shfl_xor(hi, o, 64));
+        }
+        if (lane == 0) { redr[wave][0] = lo; redr[wave][1] = hi; }
+      }
     }
   }
   __syncthreads();
+  if (record && mm && threadIdx.x == 0) {    // per (image, channel, tile): [B][C * tiles][2]
+    const size_t chunk = (size_t)b * C * tiles + (size_t)c * tiles + (blockIdx.x - bc * tiles);
+    mm[chunk * 2 + 0] = fminf(fminf(redr[0][0], redr[1][0]), fminf(redr[2][0], redr[3][0]));
+    mm[chunk * 2 + 1] = fmaxf(fmaxf(redr[0][1], redr[1][1]), fmaxf(redr[2][1], redr[3][1]));
+  }
   f2_t g[kRbRows];
   rb_stencil<T>(lds, wd_fwd, g);
   double d2 = 0;
@@ -1326,8 +1362,10 @@ __global__ __launch_bounds__(256) void ssim_rgb_kernel(const float* __restrict__
     }
   }
   __syncthreads();
-  // ---- horizontal + SSIM map: row r = t / 8, columns 8*(t % 8) .. +8 (segments 0..6) ----
-  const int r = threadIdx.x >> 3, c0 = (threadIdx.x & 7) * 8;
+  // ---- horizontal + SSIM map: row r = t % 32, columns 8*(t / 32) .. +8 (segments 0..6): the
+  // 32 lanes of a ds_read_b32 group read one column of 32 rows, stride 63 = -1 mod 32 banks,
+  // conflict-free (rows-within-a-lane-group mapping t / 8 had every bank hit twice) ----
+  const int r = threadIdx.x & 31, c0 = (threadIdx.x >> 5) * 8;
   const int i = i0 + r;
   const float C1 = cst[0], C2 = cst[1];
   double acc = 0;
@@ -1515,11 +1553,11 @@ template <int KIND>
 static void launch_k2_kind(int method, dim3 grid, hipStream_t st, const float* xn, const float* xo, float* y,
                            const float* xobs, const float* xtrue, float* s, const float* w, const float* theta,
                            double* partials, const OpDesc& op, int C, int H, int W, int tiles_x, int tiles,
-                           double gamma2, double gkl_gamma, double gkl_alpha, int record) {
+                           double gamma2, double gkl_gamma, double gkl_alpha, int record, float* mm) {
 #define K2_ARGS xn, xo, y, xobs, xtrue, s, w, theta, partials, op, C, H, W, tiles_x, tiles, gamma2, gkl_gamma, \
                 gkl_alpha, record
 #define K2E_ARGS xn, xo, y, xobs, xtrue, s, w, theta, partials, op.mask, C, H, W, tiles_x, tiles, gamma2, \
-                 1.0 / gamma2, gkl_gamma, gkl_alpha, record
+                 1.0 / gamma2, gkl_gamma, gkl_alpha, record, mm
   if constexpr (KIND == OP_BLUR) {
     if (method == M_A) hipLaunchKernelGGL((k2_dual<KIND, M_A>), grid, dim3(256), 0, st, K2_ARGS);
     else if (method == M_B) hipLaunchKernelGGL((k2_dual<KIND, M_B>), grid, dim3(256), 0, st, K2_ARGS);
@@ -1542,25 +1580,26 @@ template <class T>
 static void launch_k2_rb(int method, hipStream_t st, const float* xn, const float* xo, float* y, const float* xobs,
                          const float* xtrue, float* s, const float* w, const float* theta, double* partials,
                          const OpDesc& op, int B, int C, int H, int W, int cells_x, int cells, double gamma2,
-                         double gkl_gamma, double gkl_alpha, int record) {
+                         double gkl_gamma, double gkl_alpha, int record, float* mm) {
   const int tx = (W + kRbW - 1) / kRbW, tiles = tx * ((H + kRbH - 1) / kRbH);
   const dim3 grid(B * C * tiles);
 #define K2RB_ARGS xn, xo, y, xobs, xtrue, s, w, theta, partials, reinterpret_cast<const f2_t*>(op.dense_fwd), C, H, W, \
-                  tx, tiles, cells_x, cells, gamma2, 1.0 / gamma2, gkl_gamma, gkl_alpha, record
+                  tx, tiles, cells_x, cells, gamma2, 1.0 / gamma2, gkl_gamma, gkl_alpha, record, mm
   if (method == M_A) hipLaunchKernelGGL((k2_blur_rb<T, M_A>), grid, dim3(256), 0, st, K2RB_ARGS);
   else if (method == M_B) hipLaunchKernelGGL((k2_blur_rb<T, M_B>), grid, dim3(256), 0, st, K2RB_ARGS);
   else hipLaunchKernelGGL((k2_blur_rb<T, M_C>), grid, dim3(256), 0, st, K2RB_ARGS);
 #undef K2RB_ARGS
 }
 
-void launch_k2(int kind, int method, const float* xn, const float* xo, float* y, const float* xobs,
-               const float* xtrue, float* s, const float* w, const float* theta, double* partials,
-               const OpDesc& op, int B, int C, int H, int W, double gamma2, double gkl_gamma, double gkl_alpha,
-               int record, hipStream_t st) {
+int launch_k2(int kind, int method, const float* xn, const float* xo, float* y, const float* xobs,
+              const float* xtrue, float* s, const float* w, const float* theta, double* partials,
+              const OpDesc& op, int B, int C, int H, int W, double gamma2, double gkl_gamma, double gkl_alpha,
+              int record, float* mm, hipStream_t st) {
   const TileGrid g = tile_grid(H, W);
+  if (!record) mm = nullptr;
   if (kind == OP_BLUR && rb_ok(op, C)) {
 #define K2RB(TT) launch_k2_rb<TT>(method, st, xn, xo, y, xobs, xtrue, s, w, theta, partials, op, B, C, H, W, \
-                                  g.tiles_x, g.tiles, gamma2, gkl_gamma, gkl_alpha, record)
+                                  g.tiles_x, g.tiles, gamma2, gkl_gamma, gkl_alpha, record, mm)
     switch (op.taps_id) {
       case TAPS_BLUR_1: K2RB(Taps_blur_1_Fwd); break;
       case TAPS_SQUARE_MINI: K2RB(Taps_square_mini_Fwd); break;
@@ -1568,21 +1607,30 @@ void launch_k2(int kind, int method, const float* xn, const float* xo, float* y,
         switch (op.Rd) { case 2: K2RB(DenseTaps<2>); break; case 4: K2RB(DenseTaps<4>); break; default: K2RB(DenseTaps<8>); }
     }
 #undef K2RB
-    return;
+    return mm ? C * ((W + kRbW - 1) / kRbW) * ((H + kRbH - 1) / kRbH) : 0;
   }
   dim3 grid(g.tiles, B);
-  if (kind == OP_BLUR)
+  if (kind == OP_BLUR) {      // generic stencil path: no x+ range (SSIM computes its own)
     launch_k2_kind<OP_BLUR>(method, grid, st, xn, xo, y, xobs, xtrue, s, w, theta, partials, op, C, H, W,
-                            g.tiles_x, g.tiles, gamma2, gkl_gamma, gkl_alpha, record);
-  else if (kind == OP_MASK)
+                            g.tiles_x, g.tiles, gamma2, gkl_gamma, gkl_alpha, record, nullptr);
+    return 0;
+  }
+  if (kind == OP_MASK)
     launch_k2_kind<OP_MASK>(method, grid, st, xn, xo, y, xobs, xtrue, s, w, theta, partials, op, C, H, W,
-                            g.tiles_x, g.tiles, gamma2, gkl_gamma, gkl_alpha, record);
+                            g.tiles_x, g.tiles, gamma2, gkl_gamma, gkl_alpha, record, mm);
   else
     launch_k2_kind<OP_ID>(method, grid, st, xn, xo, y, xobs, xtrue, s, w, theta, partials, op, C, H, W,
-                          g.tiles_x, g.tiles, gamma2, gkl_gamma, gkl_alpha, record);
+                          g.tiles_x, g.tiles, gamma2, gkl_gamma, gkl_alpha, record, mm);
+  return mm ? g.tiles : 0;
 }
 
 int partial_tiles(int H, int W) { return tile_grid(H, W).tiles; }
+
+int k2_minmax_chunks(int C, int H, int W) {
+  const int rb = C * ((W + kRbW - 1) / kRbW) * ((H + kRbH - 1) / kRbH);
+  const int el = tile_grid(H, W).tiles;
+  return rb > el ? rb : el;
+}
 
 template <class TF, class TA>
 static bool taps_match(int Rd, const uint32_t* fwd_cols, const uint32_t* adj_cols) {
@@ -1735,15 +1783,20 @@ size_t ssim_scratch_bytes(int B, int C, int H, int W) {
 }
 
 void launch_ssim(const float* xt, const float* x, void* scratch, double* metrics, int B, int C, int H, int W,
-                 int it, int cap, hipStream_t st) {
+                 int it, int cap, hipStream_t st, const float* mm_ext, int mm_chunks) {
   const size_t n = (size_t)C * H * W;
-  const int chunks = chunk_count(n);
+  int chunks = chunk_count(n);
   const int tx = (W + kSsTW - 1) / kSsTW, tiles = tx * ((H + kSsTH - 1) / kSsTH);
   float* mm = static_cast<float*>(scratch);
   double* ps = reinterpret_cast<double*>(
       (reinterpret_cast<uintptr_t>(mm + (size_t)B * chunks * 2) + 255) & ~(uintptr_t)255);
   float* rows = reinterpret_cast<float*>(ps + (size_t)B * C * tiles);
-  hipLaunchKernelGGL(ssim_minmax_kernel, dim3(chunks, B), dim3(256), 0, st, x, mm, n, chunks);
+  if (mm_ext && mm_chunks > 0) {          // x+'s range came from K2 (one pass over x+ fewer)
+    mm = const_cast<float*>(mm_ext);
+    chunks = mm_chunks;
+  } else {
+    hipLaunchKernelGGL(ssim_minmax_kernel, dim3(chunks, B), dim3(256), 0, st, x, mm, n, chunks);
+  }
   const int gray = C == 1;
   if (gray)
     hipLaunchKernelGGL(ssim_gray_kernel, dim3((H + 3) / 4, B), dim3(256), 0, st, xt, x, mm, rows, H, W, chunks);
