@@ -226,7 +226,7 @@ def main():
     ap.add_argument("--size", type=int, default=0, help="image side (0 = the config's)")
     ap.add_argument("--op", default="", choices=["", "blur", "Id", "random_sampling"],
                     help="override the config's degradation operator (profiling the elementwise K1/K2)")
-    ap.add_argument("--precision", default="auto", choices=["auto", "fp16", "fp32"],
+    ap.add_argument("--precision", default="auto", choices=["auto", "fp16", "fp16w2", "fp32"],
                     help="denoiser operands: auto = the solver's policy (fp32 for the Poisson methods, "
                          "fp16 otherwise; pnppds.iteration.FP32_METHODS)")
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU-baseline work")
@@ -328,7 +328,8 @@ def main():
             "n_gpus": world, "steps": K, "warmup": Wm,
             "ms_per_step": round(1e3 * t_el / K, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "fp16-mfma/fp32-acc+state" if args.precision == "fp16" else "fp32-mfma/fp32-state",
+            "dtype": {"fp16": "fp16-mfma/fp32-acc+state", "fp16w2": "fp16-mfma(split fp16 hi+lo weights)/fp32-acc+state",
+                      "fp32": "fp32-mfma/fp32-state"}[args.precision],
             "data": f"synthetic structured images, x_obs from the device observation pipeline (main.py:49-64: "
                     f"{cfg['op']}, sigma={cfg['sigma']}, sp={cfg['sp']}, poisson={cfg['poisson']}, "
                     f"np.random.seed(1234) streams); real {arch} weights",
@@ -344,7 +345,7 @@ def main():
             line["kernel_ms"] = kt
             line["kernel_calls_per_step"] = {k: round(v[1] / K, 2) for k, v in prof.items()}
             fp32 = args.precision == "fp32"
-            kname = "conv32_body" if fp32 else "conv_body"
+            kname = {"fp32": "conv32_body", "fp16w2": "conv_body_w2"}.get(args.precision, "conv_body")
             if kname in prof:
                 body_ms = prof[kname][0]
                 m = images_per_launch(B, H, W, args.chunk, fp32)
@@ -357,6 +358,12 @@ def main():
                     line["roofline"] = {"kernel": "conv32_body (64->64 3x3, fp32 MFMA 32x32x2)", "bound": "mfma",
                                         "achieved": round(tfl, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                                         "frac": round(tfl / FP32_PEAK_TFLOPS, 4), "traffic": None,
+                                        "bytes_per_launch": by, "flops_per_launch": fl, "hbm_gbs": round(gbs, 1)}
+                elif args.precision == "fp16w2":   # 2 MFMAs per product: 576 MFMA-FLOP/B, MFMA roof
+                    line["roofline"] = {"kernel": "conv_body_w2 (64->64 3x3, fp16 MFMA, split hi+lo weights)",
+                                        "bound": "mfma", "achieved": round(2 * tfl, 1), "peak": FP16_PEAK_TFLOPS,
+                                        "unit": "TFLOP/s (MFMA work, 2x algorithmic)",
+                                        "frac": round(2 * tfl / FP16_PEAK_TFLOPS, 4), "traffic": None,
                                         "bytes_per_launch": by, "flops_per_launch": fl, "hbm_gbs": round(gbs, 1)}
                 else:      # 288 FLOP/B, below the 2500 / 8 = 312 FLOP/B ridge: HBM roof
                     line["roofline"] = {"kernel": "conv_body (64->64 3x3 implicit GEMM, fp16 MFMA)", "bound": "hbm",

@@ -81,9 +81,11 @@ enum pnp_activation { PNP_ACT_LEAKY_RELU = 0 /* slope 0.01 */, PNP_ACT_RELU = 1 
 
 enum pnp_precision {
   PNP_PREC_FP16 = 0, /* fp16 MFMA operands, fp32 accumulation (default)            */
-  PNP_PREC_FP32 = 1  /* fp32 operands and accumulation (v_mfma_f32_32x32x2_f32): the
+  PNP_PREC_FP32 = 1, /* fp32 operands and accumulation (v_mfma_f32_32x32x2_f32): the
                         reference denoiser's own precision (models/denoiser.py:37), the
                         parity fallback; about 1/10 of the fp16 path's throughput     */
+  PNP_PREC_FP16W2 = 2 /* fp16 activations, weights split into fp16 hi + lo halves (two
+                        MFMAs per product, ~22-bit weights), fp32 accumulation         */
 };
 
 /* Scalar parameters of iteration.test_iter (iteration.py:10), same names/meaning. */

@@ -225,15 +225,19 @@ class OracleDenoiser:
     """Forward of the conv stack on torch-CPU in float32.
 
     ``emulate_fp16=True`` rounds every conv's input activations and weights to fp16
-    (fp32 accumulation, fp16 storage of hidden activations) — the device numerics.
+    (fp32 accumulation, fp16 storage of hidden activations) — the device numerics of
+    PNP_PREC_FP16.  ``emulate_fp16="w2"``: activations rounded to fp16, weights as the sum of
+    their fp16 high half and the fp16 rounding of the remainder (PNP_PREC_FP16W2).
     """
 
-    def __init__(self, weights, emulate_fp16: bool = False):
+    def __init__(self, weights, emulate_fp16=False):
         self.w = weights
-        self.emulate_fp16 = emulate_fp16
+        self.emulate_fp16 = bool(emulate_fp16)
         self.tw = [torch.from_numpy(np.ascontiguousarray(a, np.float32)) for a in weights.weights]
         self.tb = [torch.from_numpy(np.ascontiguousarray(b, np.float32)) for b in weights.biases]
-        if emulate_fp16:
+        if emulate_fp16 == "w2":
+            self.tw = [t.half().float() + (t - t.half().float()).half().float() for t in self.tw]
+        elif emulate_fp16:
             self.tw = [t.half().float() for t in self.tw]
 
     @torch.no_grad()

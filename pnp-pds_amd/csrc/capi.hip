@@ -53,6 +53,7 @@ struct pnp_ctx {
   int prec = PNP_PREC_FP16;   // pnp_set_precision: fp16 MFMA operands (conv.hip) or fp32 (conv32.hip)
   DevBuf head_w, head_b, body_w, body_b, tail_w, tail_b;
   DevBuf head_w32, body_w32, tail_w32;   // fp32 MFMA fragments (PNP_PREC_FP32)
+  DevBuf head_wlo, body_wlo, tail_wlo;   // fp16 low halves W - fp16(W) (PNP_PREC_FP16W2)
 
   // operator
   int op_kind = PNP_OP_ID;
@@ -309,10 +310,11 @@ void run_denoiser(pnp_ctx* ctx, const half_t* u16, const float* u32, float* xout
     const half_t* in4 = u16 + (size_t)b0 * (H + 2) * (W + 2) * 4;
     const float* xin = u32 + (size_t)b0 * C * H * W;
     float* xo = xout + (size_t)b0 * C * H * W;
+    const bool w2 = ctx->prec == PNP_PREC_FP16W2;
     {
       ProfScope ps(ctx, "conv_head", st);
-      launch_conv_head(in4, P<half_t>(act[0]), ctx->head_w.p, P<float>(ctx->head_b), s, ctx->den_act,
-                       ctx->num_cus, ctx->ablate >= 100 ? ctx->ablate - 100 : 4, st);
+      launch_conv_head(in4, P<half_t>(act[0]), ctx->head_w.p, w2 ? ctx->head_wlo.p : nullptr, P<float>(ctx->head_b),
+                       s, ctx->den_act, ctx->num_cus, 4, st);
       check_launch(ctx, "conv_head");
     }
     int cur = 0;
@@ -320,19 +322,25 @@ void run_denoiser(pnp_ctx* ctx, const half_t* u16, const float* u32, float* xout
     for (int l = 0; l < nbody;) {
       const char* wl = (const char*)ctx->body_w.p + (size_t)l * kBodyWBytes;
       const float* bl = P<float>(ctx->body_b) + l * kWidth;
-      {
+      if (w2) {
+        ProfScope ps(ctx, "conv_body_w2", st);
+        launch_conv_body_w2(P<half_t>(act[cur]), P<half_t>(act[cur ^ 1]), wl,
+                            (const char*)ctx->body_wlo.p + (size_t)l * kBodyWBytes, bl, s, ctx->den_act, ctx->num_cus,
+                            st);
+        check_launch(ctx, "conv_body_w2");
+      } else {
         ProfScope ps(ctx, "conv_body", st);
         launch_conv_body(P<half_t>(act[cur]), P<half_t>(act[cur ^ 1]), wl, bl, s, ctx->den_act, ctx->num_cus,
                          ctx->ablate, st);
         check_launch(ctx, "conv_body");
-        l += 1;
       }
+      l += 1;
       cur ^= 1;
     }
     {
       ProfScope ps(ctx, "conv_tail", st);
-      launch_conv_tail(P<half_t>(act[cur]), xin, xo, ctx->tail_w.p, P<float>(ctx->tail_b), s, C, ctx->den_residual,
-                       ctx->den_clamp, ctx->num_cus, st);
+      launch_conv_tail(P<half_t>(act[cur]), xin, xo, ctx->tail_w.p, w2 ? ctx->tail_wlo.p : nullptr,
+                       P<float>(ctx->tail_b), s, C, ctx->den_residual, ctx->den_clamp, ctx->num_cus, st);
       check_launch(ctx, "conv_tail");
     }
   }
@@ -793,7 +801,7 @@ int pnp_destroy(pnp_ctx* ctx) {
                     &ctx->z, &ctx->p, &ctx->t, &ctx->dense_fwd, &ctx->dense_adj, &ctx->ssim_scr,
                     &ctx->taps64, &ctx->y1, &ctx->d, &ctx->c1, &ctx->dg_words, &ctx->dg_flag, &ctx->dg_rank, &ctx->dg_scan, &ctx->dg_noise,
                     &ctx->dg_img, &ctx->dg_draws, &ctx->dg_first, &ctx->dg_status,
-                    &ctx->head_w32, &ctx->body_w32, &ctx->tail_w32, &ctx->act32[0], &ctx->act32[1], &ctx->l1_scr, &ctx->ssim_mm};
+                    &ctx->head_w32, &ctx->body_w32, &ctx->tail_w32, &ctx->act32[0], &ctx->act32[1], &ctx->l1_scr, &ctx->ssim_mm, &ctx->head_wlo, &ctx->body_wlo, &ctx->tail_wlo};
   for (DevBuf* b : bufs) release(*b);
   for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -829,7 +837,7 @@ int pnp_set_tuning(pnp_ctx* ctx, int key, int value) {
 int pnp_set_precision(pnp_ctx* ctx, int precision) {
   if (!ctx) return PNP_E_ARG;
   return guarded(ctx, [&] {
-    if (precision != PNP_PREC_FP16 && precision != PNP_PREC_FP32)
+    if (precision != PNP_PREC_FP16 && precision != PNP_PREC_FP32 && precision != PNP_PREC_FP16W2)
       fail(ctx, PNP_E_UNSUPPORTED, "precision %d not supported", precision);
     ctx->prec = precision;
   });
@@ -862,6 +870,26 @@ int pnp_set_denoiser(pnp_ctx* ctx, int channels, int depth, int width, const flo
       p += n_body;
     }
     pack_tail_weights(p, channels, tw.data());
+    {                                        // low halves W - fp16(W) for PNP_PREC_FP16W2, packed like W
+      auto lo_of = [](const float* w, size_t n) {
+        std::vector<float> lo(n);
+        for (size_t i = 0; i < n; ++i) lo[i] = w[i] - (float)(_Float16)w[i];
+        return lo;
+      };
+      std::vector<uint16_t> hl(hw.size()), bl(bw.size()), tl(tw.size());
+      const float* q = params;
+      pack_head_weights(lo_of(q, (size_t)kWidth * channels * 9).data(), channels, hl.data());
+      q += n_head;
+      for (int l = 0; l < depth - 2; ++l, q += n_body)
+        pack_body_weights(lo_of(q, (size_t)kWidth * kWidth * 9).data(), bl.data() + (size_t)l * kBodyWBytes / 2);
+      pack_tail_weights(lo_of(q, (size_t)channels * kWidth * 9).data(), channels, tl.data());
+      ensure(ctx, ctx->head_wlo, hl.size() * 2);
+      ensure(ctx, ctx->body_wlo, bl.size() * 2);
+      ensure(ctx, ctx->tail_wlo, tl.size() * 2);
+      HIPCHK(ctx, hipMemcpy(ctx->head_wlo.p, hl.data(), hl.size() * 2, hipMemcpyHostToDevice));
+      HIPCHK(ctx, hipMemcpy(ctx->body_wlo.p, bl.data(), bl.size() * 2, hipMemcpyHostToDevice));
+      HIPCHK(ctx, hipMemcpy(ctx->tail_wlo.p, tl.data(), tl.size() * 2, hipMemcpyHostToDevice));
+    }
     {                                        // fp32 fragments for PNP_PREC_FP32
       std::vector<float> h32(conv32_weight_floats(0)), b32(conv32_weight_floats(1) * (depth - 2)),
           t32(conv32_weight_floats(2));

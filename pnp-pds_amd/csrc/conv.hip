@@ -297,21 +297,138 @@ PNP_V3_INST(6, 0)
 #undef PNP_V3_INST
 
 // ------------------------------------------------------------------------------------
+// Body layer with split weights (PNP_PREC_FP16W2): W = W_hi + W_lo, both fp16 (W_lo =
+// fp16(W - W_hi), subnormals kept: the f16 MFMA inputs do not flush them, probed in
+// tools/probes/mfma_f16_denorm.hip), fp16 activations, fp32 accumulation: every product is
+// a * W_hi + a * W_lo in the same accumulator, so the weights carry ~22 significant bits.
+// Why: with fp16-rounded weights the Poisson method's slow primal steps integrate the
+// rounded network's deterministic error (0.19 dB after 3000 iterations of ours-C), while
+// fp16 activations alone stay within 0.001 dB (profiles/r02/precision_drift.txt).
+// Twice the MFMAs of conv_body_v3.  The hi halves stay in registers (144 VGPRs, as in v3);
+// the lo halves of both M-tiles (72 KiB) sit in LDS for the launch, one A-fragment read per
+// K-step; with them the halo ring is 2 deep (2 x 44 KiB: tile t+1's DMA runs during tile t)
+// and the LDS is exactly 160 KiB.  4 waves, one per SIMD: wave w owns channels
+// 32m..32m+31 (m = w & 1) of tile rows 4(w>>1) .. +3 (four N-tiles, 64 accumulators); per
+// K-step 4 B fragments + 1 lo A fragment, 8 MFMAs.  The epilogue stores 2 x 16 B per lane
+// and N-tile straight from registers.
+// ------------------------------------------------------------------------------------
+constexpr int kW2Halo = 44 * 1024;
+constexpr int kW2Lo = 2 * kW2Halo;
+constexpr int kW2Lds = kW2Lo + kBodyWBytes;                    // 163840 B
+
+template <int ACT>
+__global__ __launch_bounds__(256, 1) void conv_body_w2_kernel(const half_t* __restrict__ in,
+                                                               half_t* __restrict__ out,
+                                                               const uint4* __restrict__ wpk,
+                                                               const uint4* __restrict__ wpk_lo,
+                                                               const float* __restrict__ bias,
+                                                               ConvShape s) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int m = wave & 1, rq = wave >> 1;    // M-tile, row quad
+  const int h = lane >> 5, col = lane & 31;
+  unsigned char* wlo = smem + kW2Lo;
+  for (int i = tid; i < kBodyWBytes / 16; i += 256) reinterpret_cast<uint4*>(wlo)[i] = wpk_lo[i];
+  float bl[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) bl[r] = bias[32 * m + 16 * h + r];
+  half8_t wA[kBodyKSteps];                    // hi halves, resident for the launch
+#pragma unroll
+  for (int ks = 0; ks < kBodyKSteps; ++ks)
+    wA[ks] = *reinterpret_cast<const half8_t*>(reinterpret_cast<const unsigned char*>(wpk) +
+                                               ((ks * 2 + m) * 64 + lane) * 16);
+  auto buf = [&](int i) { return smem + i * kW2Halo; };
+  RingDma<4, true> dma;
+  dma.init(s, wave);
+  auto issue_dma = [&](int tt, int bi) {      // clamped: always the same instruction count
+    dma.issue(buf(bi), in, s, tt < s.tiles ? tt : s.tiles - 1, wave);
+  };
+  int t = xcd_block(blockIdx.x, gridDim.x);
+  if (t < s.tiles) {
+    issue_dma(t, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");      // tile t (and the lo weights) landed
+  }
+  __syncthreads();
+  int cur = 0;
+  for (; t < s.tiles; t += gridDim.x) {
+    int b, ty0, tx0;
+    decode_tile(t, s, b, ty0, tx0);
+    issue_dma(t + gridDim.x, cur ^ 1);        // buffer cur ^ 1 was last read by tile t - 1
+    const unsigned char* hl = buf(cur);
+    auto ldB = [&](int ks, int n) {
+      const int tap = ks >> 2, sub = ks & 3;
+      return *reinterpret_cast<const half8_t*>(hl + halo_off(4 * rq + n + tap / 3, col + tap % 3, 2 * sub + h));
+    };
+    auto ldL = [&](int ks) {
+      return *reinterpret_cast<const half8_t*>(wlo + ((ks * 2 + m) * 64 + lane) * 16);
+    };
+    floatx16 acc[4];
+#pragma unroll
+    for (int n = 0; n < 4; ++n) acc[n] = floatx16{};
+    half8_t fb[4], fl = ldL(0);
+#pragma unroll
+    for (int n = 0; n < 4; ++n) fb[n] = ldB(0, n);
+#pragma unroll
+    for (int ks = 0; ks < kBodyKSteps; ++ks) {
+      const half8_t lo = fl;
+      if (ks + 1 < kBodyKSteps) fl = ldL(ks + 1);
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wA[ks], fb[n], acc[n], 0, 0, 0);
+        acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(lo, fb[n], acc[n], 0, 0, 0);
+        if (ks + 1 < kBodyKSteps) fb[n] = ldB(ks + 1, n);
+      }
+    }
+    // epilogue: lane (col, h) holds channels 32m + 16h .. +15 of pixel (row 4rq + n, column col)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      const int y = ty0 + 4 * rq + n;
+      const half8_t v0 = bias_act8<ACT>(acc[n], 0, bl), v1 = bias_act8<ACT>(acc[n], 8, bl + 8);
+      half_t* row = out + (((size_t)b * s.Hp + y + s.pad) * s.Wp + tx0 + s.pad) * kWidth;
+      const __amdgpu_buffer_rsrc_t rs =
+          __builtin_amdgcn_make_buffer_rsrc(row, (short)0, y < s.H ? min(kTileW, s.W - tx0) * 128 : 0, 0x00020000);
+      const unsigned off = (unsigned)(col * 128 + 64 * m + 32 * h);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i_t, v0), rs, off, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i_t, v1), rs, off + 16, 0, 0);
+    }
+    // tile t+1 landed: only this tile's 8 stores are younger than its DMA
+    asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    cur ^= 1;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA may land after the workgroup ends
+}
+
+template __global__ void conv_body_w2_kernel<0>(const half_t* __restrict__, half_t* __restrict__,
+                                                const uint4* __restrict__, const uint4* __restrict__,
+                                                const float* __restrict__, ConvShape);
+template __global__ void conv_body_w2_kernel<1>(const half_t* __restrict__, half_t* __restrict__,
+                                                const uint4* __restrict__, const uint4* __restrict__,
+                                                const float* __restrict__, ConvShape);
+
+// ------------------------------------------------------------------------------------
 // Head layer C -> 64 (basic_models.py:16,27-28).  Input: padded NHWC4 fp16 (8 B/pixel).
 // K = 9 taps x 4 channels = 36, padded to 48 = 3 K-steps of 16: k = 4*tap + ch.
 // ------------------------------------------------------------------------------------
+// W2: split weights (W_hi + W_lo, PNP_PREC_FP16W2), two MFMAs per product.
+template <bool W2>
 __global__ __launch_bounds__(256) void conv_head_kernel(const half_t* __restrict__ in4,
                                                          half_t* __restrict__ out,
                                                          const uint4* __restrict__ wpk,
+                                                         const uint4* __restrict__ wpk_lo,
                                                          const float* __restrict__ bias,
                                                          ConvShape s, int act) {
   __shared__ __attribute__((aligned(16))) unsigned char wl[kHeadWBytes];
+  __shared__ __attribute__((aligned(16))) unsigned char wll[W2 ? kHeadWBytes : 16];
   __shared__ __attribute__((aligned(16))) uint2 hl[kHaloPix];
   __shared__ __attribute__((aligned(16))) unsigned char stg_all[4 * 8192];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   unsigned char* stg = stg_all + wave * 8192;
   const int h = lane >> 5, col = lane & 31;
   for (int i = tid; i < kHeadWBytes / 16; i += 256) reinterpret_cast<uint4*>(wl)[i] = wpk[i];
+  if (W2)
+    for (int i = tid; i < kHeadWBytes / 16; i += 256) reinterpret_cast<uint4*>(wll)[i] = wpk_lo[i];
   float bias_r[2][16];
 #pragma unroll
   for (int m = 0; m < 2; ++m)
@@ -362,6 +479,17 @@ __global__ __launch_bounds__(256) void conv_head_kernel(const half_t* __restrict
         } else {
           acc01 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, bf, acc01, 0, 0, 0);
           acc11 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, bf, acc11, 0, 0, 0);
+        }
+        if (W2) {
+          const half8_t l0 = *reinterpret_cast<const half8_t*>(wll + ((ks * 2 + 0) * 64 + lane) * 16);
+          const half8_t l1 = *reinterpret_cast<const half8_t*>(wll + ((ks * 2 + 1) * 64 + lane) * 16);
+          if (n == 0) {
+            acc00 = __builtin_amdgcn_mfma_f32_32x32x16_f16(l0, bf, acc00, 0, 0, 0);
+            acc10 = __builtin_amdgcn_mfma_f32_32x32x16_f16(l1, bf, acc10, 0, 0, 0);
+          } else {
+            acc01 = __builtin_amdgcn_mfma_f32_32x32x16_f16(l0, bf, acc01, 0, 0, 0);
+            acc11 = __builtin_amdgcn_mfma_f32_32x32x16_f16(l1, bf, acc11, 0, 0, 0);
+          }
         }
       }
     }
@@ -414,10 +542,12 @@ __global__ __launch_bounds__(256) void conv_head_kernel(const half_t* __restrict
 constexpr int kTailHalo = 44 * 1024;                           // 11 uniform DMA slots per wave
 constexpr int kTailLds = 3 * kTailHalo;                         // 135168 B
 
+template <bool W2>
 __global__ __launch_bounds__(256, 1) void conv_tail_kernel(const half_t* __restrict__ in,
                                                             const float* __restrict__ xin,
                                                             float* __restrict__ xout,
                                                             const uint4* __restrict__ wpk,
+                                                            const uint4* __restrict__ wpk_lo,
                                                             const float* __restrict__ bias,
                                                             ConvShape s, int C, int residual_sign,
                                                             int clamp_out) {
@@ -425,10 +555,13 @@ __global__ __launch_bounds__(256, 1) void conv_tail_kernel(const half_t* __restr
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int q4 = lane >> 4, c16 = lane & 15;
-  half8_t wA[kTailKSteps];
+  half8_t wA[kTailKSteps], wL[W2 ? kTailKSteps : 1];
 #pragma unroll
-  for (int ks = 0; ks < kTailKSteps; ++ks)
+  for (int ks = 0; ks < kTailKSteps; ++ks) {
     wA[ks] = *reinterpret_cast<const half8_t*>(reinterpret_cast<const unsigned char*>(wpk) + (ks * 64 + lane) * 16);
+    if (W2)
+      wL[ks] = *reinterpret_cast<const half8_t*>(reinterpret_cast<const unsigned char*>(wpk_lo) + (ks * 64 + lane) * 16);
+  }
   float bias_r[kMaxC];
 #pragma unroll
   for (int c = 0; c < kMaxC; ++c) bias_r[c] = c < C ? bias[c] : 0.f;
@@ -485,6 +618,11 @@ __global__ __launch_bounds__(256, 1) void conv_tail_kernel(const half_t* __restr
       }
 #pragma unroll
       for (int n = 0; n < 4; ++n) acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wA[ks], fb[r][n], acc[n], 0, 0, 0);
+      if (W2) {
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+          acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wL[W2 ? ks : 0], fb[r][n], acc[n], 0, 0, 0);
+      }
     }
     // C/D map of 16x16: col = lane & 15 (pixel of N-tile n), row = 4*(lane>>4) + r (channel):
     // lanes 0..15 hold channels 0..3 of N-tile n.  Store-layout lane l wants N-tile l>>4,
@@ -521,6 +659,15 @@ __global__ __launch_bounds__(256, 1) void conv_tail_kernel(const half_t* __restr
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA may land after the workgroup ends
 }
+
+#define PNP_TAIL_INST(W)                                                                                     \
+  template __global__ void conv_tail_kernel<W>(const half_t* __restrict__, const float* __restrict__,         \
+                                               float* __restrict__, const uint4* __restrict__,                \
+                                               const uint4* __restrict__, const float* __restrict__, ConvShape, \
+                                               int, int, int);
+PNP_TAIL_INST(false)
+PNP_TAIL_INST(true)
+#undef PNP_TAIL_INST
 
 // ------------------------------------------------------------------------------------
 // Host-side weight packing (fp32 PyTorch layout -> fp16 MFMA fragment order).
@@ -603,13 +750,37 @@ hipError_t conv_kernels_init() {
     e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kV3Lds);
     if (e != hipSuccess) return e;
   }
-  return hipFuncSetAttribute((const void*)conv_tail_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, kTailLds);
+  for (const void* k : {(const void*)conv_body_w2_kernel<0>, (const void*)conv_body_w2_kernel<1>}) {
+    e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kW2Lds);
+    if (e != hipSuccess) return e;
+  }
+  for (const void* k : {(const void*)conv_tail_kernel<false>, (const void*)conv_tail_kernel<true>}) {
+    e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kTailLds);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
-void launch_conv_head(const half_t* in4, half_t* out, const void* w, const float* bias, const ConvShape& s,
-                      int act, int num_cus, int blocks_per_cu, hipStream_t st) {
+void launch_conv_head(const half_t* in4, half_t* out, const void* w, const void* w_lo, const float* bias,
+                      const ConvShape& s, int act, int num_cus, int blocks_per_cu, hipStream_t st) {
   const int grid = s.tiles < num_cus * blocks_per_cu ? s.tiles : num_cus * blocks_per_cu;
-  hipLaunchKernelGGL(conv_head_kernel, dim3(grid), dim3(256), 0, st, in4, out, (const uint4*)w, bias, s, act);
+  if (w_lo)
+    hipLaunchKernelGGL(conv_head_kernel<true>, dim3(grid), dim3(256), 0, st, in4, out, (const uint4*)w,
+                       (const uint4*)w_lo, bias, s, act);
+  else
+    hipLaunchKernelGGL(conv_head_kernel<false>, dim3(grid), dim3(256), 0, st, in4, out, (const uint4*)w,
+                       (const uint4*)nullptr, bias, s, act);
+}
+
+void launch_conv_body_w2(const half_t* in, half_t* out, const void* w, const void* w_lo, const float* bias,
+                         const ConvShape& s, int act, int num_cus, hipStream_t st) {
+  const int grid = s.tiles < num_cus ? s.tiles : num_cus;
+  if (act == 0)
+    hipLaunchKernelGGL((conv_body_w2_kernel<0>), dim3(grid), dim3(256), kW2Lds, st, in, out, (const uint4*)w,
+                       (const uint4*)w_lo, bias, s);
+  else
+    hipLaunchKernelGGL((conv_body_w2_kernel<1>), dim3(grid), dim3(256), kW2Lds, st, in, out, (const uint4*)w,
+                       (const uint4*)w_lo, bias, s);
 }
 
 void launch_conv_body(const half_t* in, half_t* out, const void* w, const float* bias, const ConvShape& s,
@@ -634,12 +805,16 @@ void launch_conv_body(const half_t* in, half_t* out, const void* w, const float*
 #undef V3
 }
 
-void launch_conv_tail(const half_t* in, const float* xin, float* xout, const void* w, const float* bias,
-                      const ConvShape& s, int C, int residual_sign, int clamp_out, int num_cus,
+void launch_conv_tail(const half_t* in, const float* xin, float* xout, const void* w, const void* w_lo,
+                      const float* bias, const ConvShape& s, int C, int residual_sign, int clamp_out, int num_cus,
                       hipStream_t st) {
   const int grid = s.tiles < num_cus ? s.tiles : num_cus;
-  hipLaunchKernelGGL(conv_tail_kernel, dim3(grid), dim3(256), kTailLds, st, in, xin, xout,
-                     (const uint4*)w, bias, s, C, residual_sign, clamp_out);
+  if (w_lo)
+    hipLaunchKernelGGL(conv_tail_kernel<true>, dim3(grid), dim3(256), kTailLds, st, in, xin, xout,
+                       (const uint4*)w, (const uint4*)w_lo, bias, s, C, residual_sign, clamp_out);
+  else
+    hipLaunchKernelGGL(conv_tail_kernel<false>, dim3(grid), dim3(256), kTailLds, st, in, xin, xout,
+                       (const uint4*)w, (const uint4*)nullptr, bias, s, C, residual_sign, clamp_out);
 }
 
 }  // namespace pnp

@@ -18,16 +18,21 @@ hipError_t conv_kernels_init();
 void pack_body_weights(const float* W, uint16_t* out);
 void pack_head_weights(const float* W, int C, uint16_t* out);
 void pack_tail_weights(const float* W, int C, uint16_t* out);
-void launch_conv_head(const half_t* in4, half_t* out, const void* w, const float* bias, const ConvShape& s,
-                      int act, int num_cus, int blocks_per_cu, hipStream_t st);
+// w_lo (nullable): the split weights' low halves (PNP_PREC_FP16W2), packed like w
+void launch_conv_head(const half_t* in4, half_t* out, const void* w, const void* w_lo, const float* bias,
+                      const ConvShape& s, int act, int num_cus, int blocks_per_cu, hipStream_t st);
 // one 64 -> 64 layer; ablate != 0 only in the PNP_PROFILING build (profiling, results wrong)
 void launch_conv_body(const half_t* in, half_t* out, const void* w, const float* bias, const ConvShape& s,
                       int act, int num_cus, int ablate, hipStream_t st);
 #ifdef PNP_PROFILING
 constexpr int kTuneAblate = 3;   // pnp_set_tuning key of the profiling build (not in include/pnppds.h)
 #endif
-void launch_conv_tail(const half_t* in, const float* xin, float* xout, const void* w, const float* bias,
-                      const ConvShape& s, int C, int residual_sign, int clamp_out, int num_cus, hipStream_t st);
+void launch_conv_tail(const half_t* in, const float* xin, float* xout, const void* w, const void* w_lo,
+                      const float* bias, const ConvShape& s, int C, int residual_sign, int clamp_out, int num_cus,
+                      hipStream_t st);
+// one 64 -> 64 layer with split weights W_hi + W_lo (PNP_PREC_FP16W2)
+void launch_conv_body_w2(const half_t* in, half_t* out, const void* w, const void* w_lo, const float* bias,
+                         const ConvShape& s, int act, int num_cus, hipStream_t st);
 // fp32-operand denoiser (conv32.hip, PNP_PREC_FP32): mode 0 = head (NCHW fp32 in), 1 = body,
 // 2 = tail (NCHW fp32 out + residual + clamp); activations fp32 padded NHWC64, pad 1.
 hipError_t conv32_kernels_init();

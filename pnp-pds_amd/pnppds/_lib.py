@@ -23,8 +23,8 @@ METHOD_A, METHOD_B, METHOD_C, METHOD_ADMM_B2 = 0, 1, 2, 3
  METHOD_C_PNPADMM, METHOD_C_RED) = range(4, 13)
 TV_METHODS = (METHOD_A_PDS_TV, METHOD_A_FBS_TV, METHOD_B_HTV)   # no denoiser
 OP_ID, OP_BLUR, OP_RANDOM_SAMPLING = 0, 1, 2
-PREC_FP16, PREC_FP32 = 0, 1
-PRECISIONS = {"fp16": PREC_FP16, "fp32": PREC_FP32}
+PREC_FP16, PREC_FP32, PREC_FP16W2 = 0, 1, 2
+PRECISIONS = {"fp16": PREC_FP16, "fp32": PREC_FP32, "fp16w2": PREC_FP16W2}
 TUNE_DENOISE_CHUNK = 1
 TUNE_ABLATE = 3          # profiling build only (make PROFILING=1, lib_prof/): not in include/pnppds.h
 
@@ -220,7 +220,8 @@ class Context:
         self._denoiser_key = key
 
     def set_precision(self, precision):
-        """Denoiser operands: 'fp16' (default; fp32 accumulation) or 'fp32' (the reference's own
+        """Denoiser operands: 'fp16' (default; fp32 accumulation), 'fp16w2' (fp16 activations,
+        weights as fp16 hi + lo pairs: two MFMAs per product) or 'fp32' (the reference's own
         precision, models/denoiser.py:37; about a tenth of the throughput)."""
         code = PRECISIONS[precision] if isinstance(precision, str) else int(precision)
         self._check(self.lib.pnp_set_precision(self.h, code))

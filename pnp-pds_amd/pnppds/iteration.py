@@ -65,8 +65,11 @@ BM3D_METHODS = ("A-PnPPDS-BM3D", "A-PnPFBS-BM3D", "comparisonB-1", "C-PnPPDS-BM3
 # ours-A stays within 0.0043 dB over the 1200 iterations of a blur experiment and ours-B within
 # 0.0006 dB over 300, but the Poisson method drifts (ours-C, random sampling, gamma1 = 0.00035:
 # 0.008 dB at 300 iterations, 0.19 dB at the 3000 that main.py:136-139 runs), because its tiny
-# primal steps integrate the fp16 denoiser's deterministic error through the dual.  fp32
-# operands hold every case to <= 0.00013 dB, so the Poisson-family methods default to them.
+# primal steps integrate the fp16 denoiser's deterministic error through the dual.  Splitting
+# the weights into fp16 hi + lo halves ('fp16w2') removes the weight rounding that drives the
+# early drift (0.0008 dB at 1500 iterations) but not the fp16 activations' noise floor, which
+# still costs 0.10 dB by iteration 2200 while the reference converges.  fp32 operands hold
+# every case to <= 0.00013 dB, so the Poisson-family methods default to them.
 FP32_METHODS = (_lib.METHOD_C, _lib.METHOD_C_PNPADMM, _lib.METHOD_C_RED)
 
 
@@ -74,7 +77,7 @@ def resolve_precision(precision, method_code: int) -> str:
     if precision == "auto":
         return "fp32" if method_code in FP32_METHODS else "fp16"
     if precision not in _lib.PRECISIONS:
-        raise ValueError(f"precision must be 'auto', 'fp16' or 'fp32', not {precision!r}")
+        raise ValueError(f"precision must be 'auto', 'fp16', 'fp16w2' or 'fp32', not {precision!r}")
     return precision
 
 
@@ -110,8 +113,9 @@ def test_iter_batch(x_0, x_obsrv, x_true, phi, adj_phi, gamma1, gamma2, alpha_s,
     Returns (x[B,C,H,W] f32, s+0.5 [B,C,H,W] f32, c[B,max_iter], psnr[B,max_iter], ssim[B,max_iter],
     avg_time).  ssim is computed on the device each iteration (iteration.py:189) when record_ssim;
     C == 1 batches are scored as the reference's (H, W) grayscale arrays.  precision: the
-    denoiser's MFMA operands, 'fp16', 'fp32' (the reference's, about 10x slower) or 'auto'
-    (default: fp32 for the Poisson methods, fp16 otherwise; FP32_METHODS)."""
+    denoiser's MFMA operands, 'fp16', 'fp16w2' (split weights, two MFMAs per product), 'fp32'
+    (the reference's, about 10x slower) or 'auto' (default: fp32 for the Poisson methods, fp16
+    otherwise; FP32_METHODS)."""
     m = resolve_method(method)
     _check_ops(phi, adj_phi)
     x0 = np.asarray(x_0)

@@ -83,6 +83,31 @@ def test_denoiser_fp32_golden(gpu_ctx, golden_denoiser, name):
     assert np.abs(out - o32).max() <= TOL_FP32 * scale
 
 
+@pytest.mark.parametrize("name", ["DnCNN_nobn_nch_3_nlev_0.01", "dncnn_15"])
+@pytest.mark.parametrize("B,C,H,W", [(3, 3, 50, 70), (2, 3, 256, 256), (1, 3, 8, 32)])
+def test_denoiser_fp16w2(gpu_ctx, name, B, C, H, W):
+    """Split weights (PNP_PREC_FP16W2): against the oracle emulating the same numerics (fp16
+    activations, fp16 hi + lo weights) to the fp16-activation tolerance, closer to the fp32
+    reference than the plain fp16 path, batch vs single bits."""
+    w = DenoiserWeights.load_npz(os.path.join(WEIGHTS_DIR, name + ".npz"))
+    if w.channels != C:
+        C = w.channels
+    rng = np.random.default_rng(B * 7 + H)
+    x = rng.uniform(0, 1, (B, C, H, W)).astype(np.float32)
+    gpu_ctx.set_precision("fp16w2")
+    try:
+        out = run_denoise(gpu_ctx, w, x)
+        one = run_denoise(gpu_ctx, w, x[B - 1:B])
+    finally:
+        gpu_ctx.set_precision("fp16")
+    emu = O.OracleDenoiser(w, emulate_fp16="w2").forward_batch(x)
+    np.testing.assert_allclose(out, emu, atol=TOL_VS_FP16_EMU)
+    np.testing.assert_array_equal(one[0], out[B - 1])
+    ref = O.OracleDenoiser(w).forward_batch(x)
+    e16 = np.abs(O.OracleDenoiser(w, emulate_fp16=True).forward_batch(x) - ref).mean()
+    assert np.abs(out - ref).mean() < e16          # on average nearer fp32 than fp16 weights
+
+
 @pytest.mark.parametrize("B,C,H,W", [(3, 3, 50, 70), (2, 1, 33, 31), (1, 3, 8, 32), (2, 3, 256, 256)])
 def test_denoiser_fp32_ragged_batched(gpu_ctx, B, C, H, W):
     """fp32 path: partial tiles, tiny images, several images per launch; batch vs single bits."""

@@ -7,9 +7,9 @@ sys.path.insert(0, ".")
 from conftest import load_golden
 from test_gpu_long import run_long
 
-for case in sys.argv[1:] or ["C_rs_300", "A_blur_1200", "B_blur_300"]:
+for case in [a for a in sys.argv[1:] if "," not in a] or ["C_rs_300", "A_blur_1200", "B_blur_300"]:
     g = load_golden(f"long_{case}.npz")
-    for prec in ("fp16", "fp32"):
+    for prec in (sys.argv[-1].split(",") if "," in sys.argv[-1] else ("fp16", "fp16w2", "fp32")):
         x, s, c, psnr, ssim, t = run_long(g, prec)
         d = np.abs(psnr - g["psnr"])
         idx = [0, 9, 49, 99, 199, len(d) // 2, len(d) - 1]

@@ -2,7 +2,8 @@
 parts of the denoiser (none / weights / activations / input only / both), |dPSNR| against the
 reference trajectory tests/golden/long_C_rs_3000.npz.  CPU only (profiling aid).
 
-    python tools/precision_drift_emu.py {none,w,a,in,both} 1000
+    python tools/precision_drift_emu.py {none,w,a,in,both,w2a} 1000
+    (w2a: fp16 activations with weights split into fp16 hi + lo pairs)
 """
 import os, sys, numpy as np, torch
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -17,7 +18,9 @@ class Emu(O.OracleDenoiser):
     def __init__(self, w, rw, ra, first_only=False):
         super().__init__(w)
         self.ra, self.first_only = ra, first_only
-        if rw: self.tw = [t.half().float() for t in self.tw]
+        if rw == 1: self.tw = [t.half().float() for t in self.tw]
+        if rw == 2:   # fp16 hi + fp16 lo split (lo = fp16(w - hi), subnormals kept): fp16x2 weights
+            self.tw = [t.half().float() + (t - t.half().float()).half().float() for t in self.tw]
     @torch.no_grad()
     def forward_batch(self, x):
         xin = torch.from_numpy(np.ascontiguousarray(x, np.float32)).clamp(0, 1)
@@ -27,7 +30,8 @@ class Emu(O.OracleDenoiser):
             h = F.conv2d(h, self.tw[i], self.tb[i], padding=1)
             if i < n - 1: h = F.leaky_relu(h, 0.01)
         return (h + xin).clamp(0, 1).numpy()
-rw, ra, fo = {'none': (0,0,0), 'w': (1,0,0), 'a': (0,1,0), 'both': (1,1,0), 'in': (0,1,1)}[mode]
+rw, ra, fo = {'none': (0,0,0), 'w': (1,0,0), 'a': (0,1,0), 'both': (1,1,0), 'in': (0,1,1),
+              'w2a': (2,1,0)}[mode]
 z = np.load(os.path.join(REPO, 'tests/golden/long_C_rs_3000.npz'))
 den = Emu(resolve_weights('DnCNN_nobn_nch_3_nlev_0.01', 3), rw, ra, fo)
 p = z['params']; g1, g2, as_, an, lam, m1, m2, gad, sig, sp, pa, _, ch, r = p
