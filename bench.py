@@ -233,6 +233,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile", type=int, default=1, help="HIP-event per-kernel timing in the timed region")
     ap.add_argument("--chunk", type=int, default=0, help="images per denoiser pass (0 = auto)")
+    ap.add_argument("--body-layers", type=int, default=0, choices=[0, 1, 2],
+                    help="body layers per launch on the fp16 path (0 = the library default)")
     ap.add_argument("--ablate", type=int, default=0,
                     help="profiling build only (PNP_LIB_PATH=lib_prof/...; results wrong): 1 DMA, 2 stores, 4 MFMA")
     args = ap.parse_args()
@@ -271,6 +273,8 @@ def main():
     ctx.set_denoiser(resolve_weights(arch, C))
     args.precision = resolve_precision(args.precision, resolve_method(cfg["method"]))
     ctx.set_precision(args.precision)
+    if args.body_layers:
+        ctx.set_body_layers(args.body_layers)
     h = load_blur_kernel("blur_1")
     if cfg["op"] == "blur":
         ctx.set_operator(_lib.OP_BLUR, h=h)

@@ -128,7 +128,9 @@ int pnp_set_precision(pnp_ctx* ctx, int precision);
  * PNP_TUNE_DENOISE_CHUNK: images per denoiser pass (0 = auto: the whole batch, unless its
  * activation ping-pong pair would exceed 8 GB (fp16) / 16 GB (fp32)).                */
 enum pnp_tuning_key {
-  PNP_TUNE_DENOISE_CHUNK = 1
+  PNP_TUNE_DENOISE_CHUNK = 1,
+  PNP_TUNE_BODY_LAYERS = 2   /* 64->64 layers per launch: 2 (default; conv_body_f2, the intermediate
+                                stays in LDS) or 1 (conv_body_v3).  Bit-identical results.     */
 };
 int pnp_set_tuning(pnp_ctx* ctx, int key, int value);
 

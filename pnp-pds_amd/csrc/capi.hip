@@ -49,6 +49,7 @@ struct pnp_ctx {
   int den_C = 0, den_depth = 0, den_act = 0, den_residual = 1, den_clamp = 1;
   int den_chunk = 0;   // images per denoiser pass; 0 = auto
   int ablate = 0;         // PNP_PROFILING build only: parts of conv_body_v3 skipped, results wrong
+  int body_pair = 1;      // PNP_TUNE_BODY_LAYERS: 2 body layers per launch (conv_body_f2) when 1
   bool den_ready = false;
   int prec = PNP_PREC_FP16;   // pnp_set_precision: fp16 MFMA operands (conv.hip) or fp32 (conv32.hip)
   DevBuf head_w, head_b, body_w, body_b, tail_w, tail_b;
@@ -322,6 +323,15 @@ void run_denoiser(pnp_ctx* ctx, const half_t* u16, const float* u32, float* xout
     for (int l = 0; l < nbody;) {
       const char* wl = (const char*)ctx->body_w.p + (size_t)l * kBodyWBytes;
       const float* bl = P<float>(ctx->body_b) + l * kWidth;
+      if (!w2 && ctx->body_pair && !ctx->ablate && l + 1 < nbody) {   // layers l, l+1 in one launch
+        ProfScope ps(ctx, "conv_body_f2", st);
+        launch_conv_body_f2(P<half_t>(act[cur]), P<half_t>(act[cur ^ 1]), wl, bl, wl + kBodyWBytes, bl + kWidth, s,
+                            ctx->den_act, ctx->num_cus, st);
+        check_launch(ctx, "conv_body_f2");
+        l += 2;
+        cur ^= 1;
+        continue;
+      }
       if (w2) {
         ProfScope ps(ctx, "conv_body_w2", st);
         launch_conv_body_w2(P<half_t>(act[cur]), P<half_t>(act[cur ^ 1]), wl,
@@ -822,6 +832,11 @@ int pnp_set_tuning(pnp_ctx* ctx, int key, int value) {
     if (key == PNP_TUNE_DENOISE_CHUNK) {
       if (value < 0) fail(ctx, PNP_E_ARG, "chunk must be >= 0");
       ctx->den_chunk = value;
+      return;
+    }
+    if (key == PNP_TUNE_BODY_LAYERS) {
+      if (value != 1 && value != 2) fail(ctx, PNP_E_ARG, "body layers per launch must be 1 or 2");
+      ctx->body_pair = value == 2;
       return;
     }
 #ifdef PNP_PROFILING

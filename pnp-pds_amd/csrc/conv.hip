@@ -79,6 +79,18 @@ __device__ __forceinline__ half8_t bias_act8(const floatx16& a, int off, const f
   return o;
 }
 
+// the same in scalar fp32 (beside MFMAs packed fp32 VALU costs issue cycles: MI355X_MICROARCH.md)
+template <int ACT>
+__device__ __forceinline__ half8_t bias_act8_s(const floatx16& a, int off, const float* bl) {
+  half8_t o;
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    const float v = a[off + r] + bl[r];
+    o[r] = (half_t)(ACT == 0 ? fmaxf(v, v * 0.01f) : fmaxf(v, 0.f));
+  }
+  return o;
+}
+
 typedef int v4i_t __attribute__((ext_vector_type(4)));
 typedef int v2i_t __attribute__((ext_vector_type(2)));
 
@@ -295,6 +307,245 @@ PNP_V3_INST(4, 0)
 PNP_V3_INST(6, 0)
 #endif
 #undef PNP_V3_INST
+
+// ------------------------------------------------------------------------------------
+// Two body layers per launch, streamed down 32-pixel-wide column strips (conv_body_f2).
+// Layers l and l+1 of basic_models.py:29-33: the intermediate activation never leaves the
+// CU.  A workgroup walks one strip (image b, columns x0 .. x0+31, all rows) in steps of 8
+// rows; per step j
+//   * waves 0-1 (layer l, one 32-channel M-tile each) compute intermediate rows 8j .. 8j+7
+//     over columns x0-1 .. x0+32 (8 row N-tiles of 32 + one N-tile of the 16 halo pixels:
+//     the only recompute is the strip's 2-column halo) from an 18-row input ring, and write them
+//     (fp16, zero outside the image = the next layer's padding) into an 18-row LDS ring;
+//   * waves 2-3 (layer l+1) compute output rows 8j-9 .. 8j-2 from intermediate rows computed
+//     in earlier steps and store them to HBM;
+//   * LDS-DMA brings input rows 8j+9 .. 8j+16 (the next step's) into ring rows no wave reads
+//     in this step (16 buffer_load ... lds per wave, no registers);
+//   * one workgroup barrier.
+// The two layers run side by side on different SIMDs (one wave per SIMD; each wave keeps its
+// layer's 36 A-fragments, 144 VGPRs, for the launch), so the HBM traffic per layer pair is
+// one read (x 36/32 for the strip halo) and one write instead of two of each.
+// Both rings are chunk-planar: plane c (c = 0..7) holds channels 8c .. 8c+7 of every ring
+// pixel, 16 B per pixel, so a B fragment (16 pixels of one chunk per ds_read_b128 lane group)
+// is 256 contiguous bytes (conflict-free without a swizzle) and the 36 fragment reads of an
+// N-tile are one address register per tap row + immediate offsets (chunk plane, tap column).
+// The K order per output and the fp16 rounding of the intermediate are those of conv_body_v3
+// twice, so the result is bit-identical to two one-layer launches.
+// LDS: input ring 18 x 36 px + intermediate ring 18 x 34 px, 128 B per pixel = 161280 B.
+// ------------------------------------------------------------------------------------
+constexpr int kF2Ring = 18;                                    // rows per ring
+constexpr int kF2InW = kTileW + 4, kF2MidW = kTileW + 2;       // 36, 34 pixels per ring row
+constexpr int kF2InPlane = kF2Ring * kF2InW * 16;              // 10368 B per chunk plane
+constexpr int kF2MidPlane = kF2Ring * kF2MidW * 16;            // 9792
+constexpr int kF2Mid = 8 * kF2InPlane;                         // 82944: intermediate ring offset
+constexpr int kF2Lds = kF2Mid + 8 * kF2MidPlane;               // 161280 B
+
+__device__ __forceinline__ int f2_slot(int row) { return (row + 1 + 18 * 64) % kF2Ring; }   // row >= -1 - 18*64
+
+#ifndef F2_PREFETCH
+#define F2_PREFETCH 2
+#endif
+// One wave's MFMA stream for a step: G groups of NT N-tiles against one chunk-planar ring
+// (PLANE bytes per chunk plane), acc[g][n] = sum_ks A[ks] B_gn[ks].  The stream runs through
+// the group boundaries without a bubble: B fragments are read F2_PREFETCH K-steps ahead
+// across them (one wave per SIMD: nothing else hides an LDS read's latency), the
+// accumulators are per group (AGPRs are free here), and group g's epilogue runs in halves
+// of N-tiles, epi(g, n, half) at K-step 2 + 3 (2n + half) of group g+1, beside its MFMAs.
+// side(fs) is called once per K-step (the halo DMA pieces go there).
+// ad[g][n][dy]: byte address of the lane's pixel in tap row dy of N-tile n of group g,
+// chunk h; K-step ks = 4 tap + sub reads chunk 2 sub + h of tap column dx = +16 dx bytes.
+template <int G, int NT, int PLANE, class Epi, class Side>
+__device__ __forceinline__ void f2_stream(const half8_t (&wA)[kBodyKSteps], const unsigned char* ring,
+                                          const int (&ad)[G][NT][3], floatx16 (&acc)[G][NT], Epi&& epi,
+                                          Side&& side) {
+  constexpr int KS = kBodyKSteps, T = G * KS, D = F2_PREFETCH;
+  auto ldB = [&](int fs, int n) {
+    const int g = fs / KS, ks = fs - g * KS;
+    const int tap = ks >> 2, sub = ks & 3, dy = tap / 3, dx = tap - 3 * dy;
+    return *reinterpret_cast<const half8_t*>(ring + ad[g][n][dy] + (2 * sub * PLANE + 16 * dx));
+  };
+  half8_t fb[D + 1][NT];
+#pragma unroll
+  for (int d = 0; d < D; ++d)
+#pragma unroll
+    for (int n = 0; n < NT; ++n) fb[d][n] = ldB(d, n);
+#pragma unroll
+  for (int fs = 0; fs < T; ++fs) {
+    const int g = fs / KS, ks = fs - g * KS;
+    if (fs + D < T) {
+#pragma unroll
+      for (int n = 0; n < NT; ++n) fb[(fs + D) % (D + 1)][n] = ldB(fs + D, n);
+    }
+#pragma unroll
+    for (int n = 0; n < NT; ++n)
+      acc[g][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wA[ks], fb[fs % (D + 1)][n],
+                                                         ks == 0 ? floatx16{} : acc[g][n], 0, 0, 0);
+    if (g > 0 && ks >= 2 && ks < 2 + 3 * 2 * NT && (ks - 2) % 3 == 0) epi(g - 1, (ks - 2) / 6, ((ks - 2) / 3) & 1);
+    side(fs);
+    __builtin_amdgcn_sched_barrier(0);       // keep the reads D K-steps ahead of their MFMAs
+  }
+#pragma unroll
+  for (int n = 0; n < NT; ++n) {
+    epi(G - 1, n, 0);
+    epi(G - 1, n, 1);
+  }
+}
+
+template <int ACT>
+__global__ __launch_bounds__(256, 1) void conv_body_f2_kernel(const half_t* __restrict__ in,
+                                                               half_t* __restrict__ out,
+                                                               const uint4* __restrict__ w1,
+                                                               const float* __restrict__ b1,
+                                                               const uint4* __restrict__ w2,
+                                                               const float* __restrict__ b2, ConvShape s,
+                                                               int strips_x, int nstrips, int nsteps) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  unsigned char* ring = smem;
+  unsigned char* mid = smem + kF2Mid;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int layer = wave >> 1, m = wave & 1;
+  const int h = lane >> 5, col = lane & 31;
+  const uint4* wsrc = layer ? w2 : w1;
+  half8_t wA[kBodyKSteps];
+#pragma unroll
+  for (int ks = 0; ks < kBodyKSteps; ++ks)
+    wA[ks] = *reinterpret_cast<const half8_t*>(reinterpret_cast<const unsigned char*>(wsrc) +
+                                               ((ks * 2 + m) * 64 + lane) * 16);
+  float bl[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) bl[r] = (layer ? b2 : b1)[32 * m + 16 * h + r];
+  const unsigned img_bytes = (unsigned)(s.Hp * s.Wp) * 128u;
+
+  for (int strip = blockIdx.x; strip < nstrips; strip += gridDim.x) {
+    const int b = strip / strips_x, x0 = (strip - b * strips_x) * kTileW;
+    const __amdgpu_buffer_rsrc_t src = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(in + (size_t)b * s.Hp * s.Wp * kWidth), (short)0, (int)img_bytes, 0x00020000);
+    // Input row `row` of the strip into its ring row: 8 DMAs (one per chunk plane), lane c <
+    // 36 = strip column x0 - 2 + c = padded column x0 + c; rows past the image read 0 (OOB).
+    auto dma_row = [&](int row) {
+      const unsigned vo = (unsigned)(((row + s.pad) * s.Wp + x0 + lane) * 128);
+      unsigned char* dst = ring + f2_slot(row) * (kF2InW * 16);
+      if (lane < kF2InW) {
+#define F2_DMA(c)                                                                                       \
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(src, (__attribute__((address_space(3))) void*)(dst + (c) * kF2InPlane), \
+                                           16, vo + 16 * (c), 0, 0, 0)   /* an imm offset would move the LDS side too */
+        F2_DMA(0); F2_DMA(1); F2_DMA(2); F2_DMA(3); F2_DMA(4); F2_DMA(5); F2_DMA(6); F2_DMA(7);
+#undef F2_DMA
+      }
+    };
+    // prologue: input rows -1 .. 8 (ring rows 0 .. 9); intermediate row -1 (ring row 0) = 0
+    for (int r = wave; r < 10; r += 4) dma_row(r - 1);
+    for (int q = tid; q < 8 * kF2MidW; q += 256) {
+      const int c = q / kF2MidW, p = q - c * kF2MidW;
+      *reinterpret_cast<v4i_t*>(mid + c * kF2MidPlane + p * 16) = v4i_t{0, 0, 0, 0};
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    for (int j = 0; j < nsteps; ++j) {
+      // The next step's new input rows 8j+9 .. 8j+16 (8 DMA pieces per row, one per chunk
+      // plane): waves 0-1 (layer l, 36 more MFMAs per step) one row each, waves 2-3 three.
+      const int row0 = 8 * j + 9 + (layer ? 2 + 3 * m : m);
+      unsigned dvo = (unsigned)(((row0 + s.pad) * s.Wp + x0 + lane) * 128);
+      unsigned char* ddst = ring + f2_slot(row0) * (kF2InW * 16);
+      auto piece = [&](int i) {                // piece i: plane i & 7 of row row0 + (i >> 3)
+        if ((i & 7) == 0 && i > 0) {
+          dvo += (unsigned)(s.Wp * 128);
+          ddst = ring + f2_slot(row0 + (i >> 3)) * (kF2InW * 16);
+        }
+        if (lane < kF2InW)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(
+              src, (__attribute__((address_space(3))) void*)(ddst + (i & 7) * kF2InPlane), 16,
+              dvo + 16 * (i & 7), 0, 0, 0);
+      };
+      if (layer == 0) {
+        // intermediate rows 8j .. 8j+7 (not needed after the last step): N-tile k < 8 = row
+        // 8j+k, columns 1 .. 32 of the ring; N-tile 8 = the strip halo, columns 0 and 33 of the
+        // 8 rows (16 pixels, lanes 16-31 repeat lanes 0-15 and store nothing); 3 groups of 3.
+        // Row-aligned tiles keep every 16-lane group of a fragment read on consecutive pixels.
+        if (j + 1 < nsteps) {
+          int ad[3][3][3], prow[3][3], pcol[3][3];
+#pragma unroll
+          for (int g = 0; g < 3; ++g)
+#pragma unroll
+            for (int n = 0; n < 3; ++n) {
+              const int k = 3 * g + n;
+              prow[g][n] = k < 8 ? k : (col & 15) >> 1;
+              pcol[g][n] = k < 8 ? 1 + col : ((col & 1) ? kF2MidW - 1 : 0);
+#pragma unroll
+              for (int dy = 0; dy < 3; ++dy)
+                ad[g][n][dy] = h * kF2InPlane + (f2_slot(8 * j + prow[g][n] - 1 + dy) * kF2InW + pcol[g][n]) * 16;
+            }
+          floatx16 acc[3][3];
+          f2_stream<3, 3, kF2InPlane>(
+              wA, ring, ad, acc,
+              [&](int g, int n, int hf) {
+                if (3 * g + n == 8 && col >= 16) return;
+                const int y1 = 8 * j + prow[g][n], x = x0 - 1 + pcol[g][n];
+                const bool inside = y1 < s.H && x >= 0 && x < s.W;
+                half8_t v = bias_act8_s<ACT>(acc[g][n], 8 * hf, bl + 8 * hf);
+                if (!inside) v = half8_t{};      // the next layer's zero padding
+                *reinterpret_cast<half8_t*>(mid + (4 * m + 2 * h + hf) * kF2MidPlane +
+                                            (f2_slot(y1) * kF2MidW + pcol[g][n]) * 16) = v;
+              },
+              [&](int fs) {
+                if ((fs & 3) == 2 && (fs >> 2) < 8) piece(fs >> 2);
+              });
+        } else {
+#pragma unroll 1
+          for (int i = 0; i < 8; ++i) piece(i);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMAs have landed
+      } else {
+        if (j > 0) {
+          // output rows 8j-9 .. 8j-2 (N-tile k = row 8j-9+k, pixel = column), 2 groups of 4
+          int ad[2][4][3];
+#pragma unroll
+          for (int g = 0; g < 2; ++g)
+#pragma unroll
+            for (int n = 0; n < 4; ++n)
+#pragma unroll
+              for (int dy = 0; dy < 3; ++dy)
+                ad[g][n][dy] = h * kF2MidPlane + (f2_slot(8 * j - 9 + 4 * g + n - 1 + dy) * kF2MidW + col) * 16;
+          floatx16 acc[2][4];
+          const int ncols = min(kTileW, s.W - x0);
+          f2_stream<2, 4, kF2MidPlane>(
+              wA, mid, ad, acc,
+              [&](int g, int n, int hf) {
+                const int y = 8 * j - 9 + 4 * g + n;
+                const half8_t v = bias_act8_s<ACT>(acc[g][n], 8 * hf, bl + 8 * hf);
+                half_t* row = out + (((size_t)b * s.Hp + y + s.pad) * s.Wp + x0 + s.pad) * kWidth;
+                const bool ok = y >= 0 && y < s.H;
+                const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                    ok ? (void*)row : (void*)out, (short)0, ok ? ncols * 128 : 0, 0x00020000);
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i_t, v), rs,
+                                                       (unsigned)(col * 128 + 64 * m + 32 * h + 16 * hf), 0, 0);
+              },
+              [&](int fs) {
+                if (fs < 24) piece(fs);          // every piece before the first store
+              });
+          asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // the DMAs (older than the 16 stores) landed
+        } else {
+#pragma unroll 1
+          for (int i = 0; i < 24; ++i) piece(i);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+      }
+      __syncthreads();
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template __global__ void conv_body_f2_kernel<0>(const half_t* __restrict__, half_t* __restrict__,
+                                                const uint4* __restrict__, const float* __restrict__,
+                                                const uint4* __restrict__, const float* __restrict__, ConvShape,
+                                                int, int, int);
+template __global__ void conv_body_f2_kernel<1>(const half_t* __restrict__, half_t* __restrict__,
+                                                const uint4* __restrict__, const float* __restrict__,
+                                                const uint4* __restrict__, const float* __restrict__, ConvShape,
+                                                int, int, int);
 
 // ------------------------------------------------------------------------------------
 // Body layer with split weights (PNP_PREC_FP16W2): W = W_hi + W_lo, both fp16 (W_lo =
@@ -750,6 +1001,10 @@ hipError_t conv_kernels_init() {
     e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kV3Lds);
     if (e != hipSuccess) return e;
   }
+  for (const void* k : {(const void*)conv_body_f2_kernel<0>, (const void*)conv_body_f2_kernel<1>}) {
+    e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kF2Lds);
+    if (e != hipSuccess) return e;
+  }
   for (const void* k : {(const void*)conv_body_w2_kernel<0>, (const void*)conv_body_w2_kernel<1>}) {
     e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kW2Lds);
     if (e != hipSuccess) return e;
@@ -770,6 +1025,19 @@ void launch_conv_head(const half_t* in4, half_t* out, const void* w, const void*
   else
     hipLaunchKernelGGL(conv_head_kernel<false>, dim3(grid), dim3(256), 0, st, in4, out, (const uint4*)w,
                        (const uint4*)nullptr, bias, s, act);
+}
+
+void launch_conv_body_f2(const half_t* in, half_t* out, const void* w1, const float* b1, const void* w2,
+                         const float* b2, const ConvShape& s, int act, int num_cus, hipStream_t st) {
+  const int strips_x = (s.W + kTileW - 1) / kTileW, nstrips = s.B * strips_x;
+  const int nsteps = (s.H + 1 + 7) / 8 + 1;                 // output rows 8j-9 .. 8j-2 cover 0 .. H-1
+  const int grid = nstrips < num_cus ? nstrips : num_cus;
+  if (act == 0)
+    hipLaunchKernelGGL((conv_body_f2_kernel<0>), dim3(grid), dim3(256), kF2Lds, st, in, out, (const uint4*)w1, b1,
+                       (const uint4*)w2, b2, s, strips_x, nstrips, nsteps);
+  else
+    hipLaunchKernelGGL((conv_body_f2_kernel<1>), dim3(grid), dim3(256), kF2Lds, st, in, out, (const uint4*)w1, b1,
+                       (const uint4*)w2, b2, s, strips_x, nstrips, nsteps);
 }
 
 void launch_conv_body_w2(const half_t* in, half_t* out, const void* w, const void* w_lo, const float* bias,

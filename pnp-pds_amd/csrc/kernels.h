@@ -30,6 +30,9 @@ constexpr int kTuneAblate = 3;   // pnp_set_tuning key of the profiling build (n
 void launch_conv_tail(const half_t* in, const float* xin, float* xout, const void* w, const void* w_lo,
                       const float* bias, const ConvShape& s, int C, int residual_sign, int clamp_out, int num_cus,
                       hipStream_t st);
+// two 64 -> 64 layers in one launch, streamed down 32-pixel column strips (needs pad >= 2)
+void launch_conv_body_f2(const half_t* in, half_t* out, const void* w1, const float* b1, const void* w2,
+                         const float* b2, const ConvShape& s, int act, int num_cus, hipStream_t st);
 // one 64 -> 64 layer with split weights W_hi + W_lo (PNP_PREC_FP16W2)
 void launch_conv_body_w2(const half_t* in, half_t* out, const void* w, const void* w_lo, const float* bias,
                          const ConvShape& s, int act, int num_cus, hipStream_t st);

@@ -26,6 +26,7 @@ OP_ID, OP_BLUR, OP_RANDOM_SAMPLING = 0, 1, 2
 PREC_FP16, PREC_FP32, PREC_FP16W2 = 0, 1, 2
 PRECISIONS = {"fp16": PREC_FP16, "fp32": PREC_FP32, "fp16w2": PREC_FP16W2}
 TUNE_DENOISE_CHUNK = 1
+TUNE_BODY_LAYERS = 2
 TUNE_ABLATE = 3          # profiling build only (make PROFILING=1, lib_prof/): not in include/pnppds.h
 
 
@@ -229,6 +230,10 @@ class Context:
     def set_denoise_chunk(self, images: int):
         """Images per denoiser pass (0 = auto).  Performance only."""
         self._check(self.lib.pnp_set_tuning(self.h, TUNE_DENOISE_CHUNK, int(images)))
+
+    def set_body_layers(self, n: int):
+        """64->64 denoiser layers per launch: 2 (default, fused) or 1.  Same bits either way."""
+        self._check(self.lib.pnp_set_tuning(self.h, TUNE_BODY_LAYERS, int(n)))
 
     def set_ablate(self, bits: int):
         """Profiling build only (make PROFILING=1, PNP_LIB_PATH=.../lib_prof/libpnppds.so;

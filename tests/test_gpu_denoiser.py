@@ -125,6 +125,27 @@ def test_denoiser_fp32_ragged_batched(gpu_ctx, B, C, H, W):
     np.testing.assert_array_equal(one[0], out[B - 1])
 
 
+@pytest.mark.parametrize("name,B,C,H,W", [("DnCNN_nobn_nch_3_nlev_0.01", 3, 3, 50, 70),
+                                          ("DnCNN_nobn_nch_3_nlev_0.01", 2, 3, 256, 256),
+                                          ("dncnn_15", 2, 1, 37, 45), ("DnCNN_nobn_nch_1_nlev_0.01", 1, 1, 8, 32),
+                                          ("dncnn_color_blind", 1, 3, 9, 33), ("DnCNN_nobn_nch_3_nlev_0.01", 1, 3, 64, 96)])
+def test_body_two_layers_per_launch_bit_identical(gpu_ctx, name, B, C, H, W):
+    """conv_body_f2 (two 64->64 layers per launch, the intermediate in LDS) runs each output's
+    MFMA K-sequence and the intermediate's fp16 rounding exactly as two conv_body_v3 launches:
+    same bits, for ragged shapes (H % 8, W % 32 != 0, images narrower than a strip), odd
+    layer counts (dncnn_15: 15 body layers) and both activations."""
+    rng = np.random.default_rng(11)
+    w = DenoiserWeights.load_npz(os.path.join(WEIGHTS_DIR, name + ".npz"))
+    x = rng.uniform(0, 1, (B, C, H, W)).astype(np.float32)
+    gpu_ctx.set_body_layers(1)
+    try:
+        single = run_denoise(gpu_ctx, w, x)
+    finally:
+        gpu_ctx.set_body_layers(2)
+    fused = run_denoise(gpu_ctx, w, x)
+    np.testing.assert_array_equal(fused, single)
+
+
 def test_denoiser_full_size_rgb(gpu_ctx):
     """256x256 RGB, real weights, batch 2 — the metric's image shape."""
     w = DenoiserWeights.load_npz(os.path.join(WEIGHTS_DIR, "DnCNN_nobn_nch_3_nlev_0.01.npz"))

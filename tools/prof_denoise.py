@@ -22,7 +22,8 @@ def main():
     ap.add_argument("--random", action="store_true", help="uniform-random input instead of structured images")
     ap.add_argument("--ablate", type=int, default=0,
                     help="profiling build only (PNP_LIB_PATH=.../lib_prof/libpnppds.so): 1 DMA, 2 stores, 4 MFMA skipped")
-    ap.add_argument("--precision", default="fp16", choices=["fp16", "fp32"])
+    ap.add_argument("--precision", default="fp16", choices=["fp16", "fp32", "fp16w2"])
+    ap.add_argument("--body-layers", type=int, default=0)
     a = ap.parse_args()
     import torch
     from pnppds import _lib
@@ -33,6 +34,8 @@ def main():
     ctx.set_precision(a.precision)
     if a.ablate:
         ctx.set_ablate(a.ablate)
+    if a.body_layers:
+        ctx.set_body_layers(a.body_layers)
     B, C, H, W = a.batch, 3, a.size, a.size
     if a.random:
         x = torch.rand((B, C, H, W), device="cuda:0")
