@@ -79,16 +79,15 @@ __device__ __forceinline__ half8_t bias_act8(const floatx16& a, int off, const f
   return o;
 }
 
-// the same in scalar fp32 (beside MFMAs packed fp32 VALU costs issue cycles: MI355X_MICROARCH.md)
-template <int ACT>
-__device__ __forceinline__ half8_t bias_act8_s(const floatx16& a, int off, const float* bl) {
-  half8_t o;
+// bias + activation of NV accumulator rows a[off + NV q ..] into o[NV q ..], scalar fp32 (beside
+// MFMAs packed fp32 VALU costs extra issue cycles: MI355X_MICROARCH.md); same values as bias_act8
+template <int ACT, int NV>
+__device__ __forceinline__ void bias_act_s(half8_t& o, int q, const floatx16& a, int off, const float* bl) {
 #pragma unroll
-  for (int r = 0; r < 8; ++r) {
-    const float v = a[off + r] + bl[r];
-    o[r] = (half_t)(ACT == 0 ? fmaxf(v, v * 0.01f) : fmaxf(v, 0.f));
+  for (int r = 0; r < NV; ++r) {
+    const float v = a[off + NV * q + r] + bl[NV * q + r];
+    o[NV * q + r] = (half_t)(ACT == 0 ? fmaxf(v, v * 0.01f) : fmaxf(v, 0.f));
   }
-  return o;
 }
 
 typedef int v4i_t __attribute__((ext_vector_type(4)));
@@ -334,6 +333,7 @@ PNP_V3_INST(6, 0)
 // LDS: input ring 18 x 36 px + intermediate ring 18 x 34 px, 128 B per pixel = 161280 B.
 // ------------------------------------------------------------------------------------
 constexpr int kF2Ring = 18;                                    // rows per ring
+struct SGeom { int b, x0; };
 constexpr int kF2InW = kTileW + 4, kF2MidW = kTileW + 2;       // 36, 34 pixels per ring row
 constexpr int kF2InPlane = kF2Ring * kF2InW * 16;              // 10368 B per chunk plane
 constexpr int kF2MidPlane = kF2Ring * kF2MidW * 16;            // 9792
@@ -345,12 +345,21 @@ __device__ __forceinline__ int f2_slot(int row) { return (row + 1 + 18 * 64) % k
 #ifndef F2_PREFETCH
 #define F2_PREFETCH 2
 #endif
+#ifndef F2_L1_ROWS
+#define F2_L1_ROWS 1
+#endif
+#ifndef F2_EPI_PARTS
+#define F2_EPI_PARTS 4
+#endif
+constexpr int kF2EpiParts = F2_EPI_PARTS;  // 2 or 4: epilogue parts per N-tile (8 or 4 channels each)
+constexpr int kF2L1Rows = F2_L1_ROWS;      // halo rows DMA'd per step by each layer-l wave (of 8)
 // One wave's MFMA stream for a step: G groups of NT N-tiles against one chunk-planar ring
 // (PLANE bytes per chunk plane), acc[g][n] = sum_ks A[ks] B_gn[ks].  The stream runs through
 // the group boundaries without a bubble: B fragments are read F2_PREFETCH K-steps ahead
 // across them (one wave per SIMD: nothing else hides an LDS read's latency), the
-// accumulators are per group (AGPRs are free here), and group g's epilogue runs in halves
-// of N-tiles, epi(g, n, half) at K-step 2 + 3 (2n + half) of group g+1, beside its MFMAs.
+// accumulators are per group (AGPRs are free here), and group g's epilogue runs in
+// kF2EpiParts parts per N-tile, epi(g, n, q) at K-step 2 + kF2EpiParts n + q of group g+1, so
+// that each K-step's VALU fits beside its MFMAs (one wave per SIMD: MI355X_MICROARCH.md).
 // side(fs) is called once per K-step (the halo DMA pieces go there).
 // ad[g][n][dy]: byte address of the lane's pixel in tap row dy of N-tile n of group g,
 // chunk h; K-step ks = 4 tap + sub reads chunk 2 sub + h of tap column dx = +16 dx bytes.
@@ -380,15 +389,14 @@ __device__ __forceinline__ void f2_stream(const half8_t (&wA)[kBodyKSteps], cons
     for (int n = 0; n < NT; ++n)
       acc[g][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wA[ks], fb[fs % (D + 1)][n],
                                                          ks == 0 ? floatx16{} : acc[g][n], 0, 0, 0);
-    if (g > 0 && ks >= 2 && ks < 2 + 3 * 2 * NT && (ks - 2) % 3 == 0) epi(g - 1, (ks - 2) / 6, ((ks - 2) / 3) & 1);
+    if (g > 0 && ks >= 2 && ks < 2 + kF2EpiParts * NT) epi(g - 1, (ks - 2) / kF2EpiParts, (ks - 2) % kF2EpiParts);
     side(fs);
     __builtin_amdgcn_sched_barrier(0);       // keep the reads D K-steps ahead of their MFMAs
   }
 #pragma unroll
-  for (int n = 0; n < NT; ++n) {
-    epi(G - 1, n, 0);
-    epi(G - 1, n, 1);
-  }
+  for (int n = 0; n < NT; ++n)
+#pragma unroll
+    for (int q = 0; q < kF2EpiParts; ++q) epi(G - 1, n, q);
 }
 
 template <int ACT>
@@ -398,7 +406,7 @@ __global__ __launch_bounds__(256, 1) void conv_body_f2_kernel(const half_t* __re
                                                                const float* __restrict__ b1,
                                                                const uint4* __restrict__ w2,
                                                                const float* __restrict__ b2, ConvShape s,
-                                                               int strips_x, int nstrips, int nsteps) {
+                                                               int strips_x, int nstrips, int sb) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned char* ring = smem;
   unsigned char* mid = smem + kF2Mid;
@@ -417,122 +425,181 @@ __global__ __launch_bounds__(256, 1) void conv_body_f2_kernel(const half_t* __re
   for (int r = 0; r < 16; ++r) bl[r] = (layer ? b2 : b1)[32 * m + 16 * h + r];
   const unsigned img_bytes = (unsigned)(s.Hp * s.Wp) * 128u;
 
-  for (int strip = blockIdx.x; strip < nstrips; strip += gridDim.x) {
-    const int b = strip / strips_x, x0 = (strip - b * strips_x) * kTileW;
-    const __amdgpu_buffer_rsrc_t src = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(in + (size_t)b * s.Hp * s.Wp * kWidth), (short)0, (int)img_bytes, 0x00020000);
-    // Input row `row` of the strip into its ring row: 8 DMAs (one per chunk plane), lane c <
-    // 36 = strip column x0 - 2 + c = padded column x0 + c; rows past the image read 0 (OOB).
-    auto dma_row = [&](int row) {
-      const unsigned vo = (unsigned)(((row + s.pad) * s.Wp + x0 + lane) * 128);
-      unsigned char* dst = ring + f2_slot(row) * (kF2InW * 16);
-      if (lane < kF2InW) {
-#define F2_DMA(c)                                                                                       \
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(src, (__attribute__((address_space(3))) void*)(dst + (c) * kF2InPlane), \
-                                           16, vo + 16 * (c), 0, 0, 0)   /* an imm offset would move the LDS side too */
-        F2_DMA(0); F2_DMA(1); F2_DMA(2); F2_DMA(3); F2_DMA(4); F2_DMA(5); F2_DMA(6); F2_DMA(7);
-#undef F2_DMA
-      }
-    };
-    // prologue: input rows -1 .. 8 (ring rows 0 .. 9); intermediate row -1 (ring row 0) = 0
-    for (int r = wave; r < 10; r += 4) dma_row(r - 1);
-    for (int q = tid; q < 8 * kF2MidW; q += 256) {
-      const int c = q / kF2MidW, p = q - c * kF2MidW;
-      *reinterpret_cast<v4i_t*>(mid + c * kF2MidPlane + p * 16) = v4i_t{0, 0, 0, 0};
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+  // The workgroup's strips k = 0 .. K-1 (strip blockIdx.x + k gridDim.x) form one stream of
+  // global rows: row r of strip k is global row k S + r, S = 8 sb >= H + 1, so rows H .. S-1
+  // of a strip (zero) are also the zero row -1 of the next, and the steps run on across strip
+  // boundaries without a prologue or a drain per strip.
+  const int S = 8 * sb;
+  const int K = (nstrips - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
+  auto geom = [&](int k) {                               // (image, first column) of strip k
+    const int st = min(blockIdx.x + k * gridDim.x, (unsigned)nstrips - 1);
+    const int b = st / strips_x;
+    return SGeom{b, (st - b * strips_x) * kTileW};
+  };
+  int kJ = 0, jb = 0;                                    // step J = kJ sb + jb: strip kJ, row block jb
+  // strips kJ-1, kJ, kJ+1 (no divisions in the steps); plain ints picked by value (a select
+  // of addresses would keep them in scratch memory)
+  int gpb, gpx, gcb, gcx, gnb, gnx;
+  {
+    const SGeom g0 = geom(0), g1 = geom(1);
+    gpb = gcb = g0.b;
+    gpx = gcx = g0.x0;
+    gnb = g1.b;
+    gnx = g1.x0;
+  }
+  auto pick = [&](int k) {
+    const int pb = gpb, px = gpx, cb = gcb, cx = gcx, nb = gnb, nx = gnx;
+    return SGeom{k > kJ ? nb : (k < kJ ? pb : cb), k > kJ ? nx : (k < kJ ? px : cx)};
+  };
+  auto locate = [&](int R, int kJ, int& k, int& r) {    // global row -> (strip, row), |strip - kJ| <= 1
+    k = kJ;
+    r = R - kJ * S;
+    if (r < 0) { --k; r += S; } else if (r >= S) { ++k; r -= S; }
+  };
+  // DMA state of one input row: descriptor of its strip's image (none = zeros), lane offset
+  __amdgpu_buffer_rsrc_t dsrc;
+  unsigned dvo;
+  unsigned char* ddst;
+  auto dma_at = [&](int R, int kJ) {                     // lane c < 36: padded column x0 + c
+    int k, r;
+    locate(R, kJ, k, r);
+    const bool valid = R >= 0 && k < K;
+    const SGeom G = pick(k);
+    dsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(in + (size_t)G.b * s.Hp * s.Wp * kWidth), (short)0,
+                                             valid ? (int)img_bytes : 0, 0x00020000);
+    dvo = (unsigned)(((r + s.pad) * s.Wp + G.x0 + lane) * 128);   // rows past the image read 0 (OOB)
+    ddst = ring + f2_slot(R) * (kF2InW * 16);
+  };
+  auto dma_plane = [&](int c) {
+    if (lane < kF2InW)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(dsrc, (__attribute__((address_space(3))) void*)(ddst + c * kF2InPlane),
+                                               16, dvo + 16 * c, 0, 0, 0);   // an imm offset would move the LDS side too
+  };
+  // prologue: input rows -1 .. 8 (ring rows 0 .. 9); intermediate row -1 (ring row 0) = 0
+  for (int r = wave; r < 10; r += 4) {
+    dma_at(r - 1, 0);
+#pragma unroll 1
+    for (int c = 0; c < 8; ++c) dma_plane(c);
+  }
+  for (int q = tid; q < 8 * kF2MidW; q += 256) {
+    const int c = q / kF2MidW, p = q - c * kF2MidW;
+    *reinterpret_cast<v4i_t*>(mid + c * kF2MidPlane + p * 16) = v4i_t{0, 0, 0, 0};
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
 
-    for (int j = 0; j < nsteps; ++j) {
-      // The next step's new input rows 8j+9 .. 8j+16 (8 DMA pieces per row, one per chunk
-      // plane): waves 0-1 (layer l, 36 more MFMAs per step) one row each, waves 2-3 three.
-      const int row0 = 8 * j + 9 + (layer ? 2 + 3 * m : m);
-      unsigned dvo = (unsigned)(((row0 + s.pad) * s.Wp + x0 + lane) * 128);
-      unsigned char* ddst = ring + f2_slot(row0) * (kF2InW * 16);
-      auto piece = [&](int i) {                // piece i: plane i & 7 of row row0 + (i >> 3)
-        if ((i & 7) == 0 && i > 0) {
-          dvo += (unsigned)(s.Wp * 128);
-          ddst = ring + f2_slot(row0 + (i >> 3)) * (kF2InW * 16);
-        }
-        if (lane < kF2InW)
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(
-              src, (__attribute__((address_space(3))) void*)(ddst + (i & 7) * kF2InPlane), 16,
-              dvo + 16 * (i & 7), 0, 0, 0);
-      };
-      if (layer == 0) {
-        // intermediate rows 8j .. 8j+7 (not needed after the last step): N-tile k < 8 = row
-        // 8j+k, columns 1 .. 32 of the ring; N-tile 8 = the strip halo, columns 0 and 33 of the
-        // 8 rows (16 pixels, lanes 16-31 repeat lanes 0-15 and store nothing); 3 groups of 3.
-        // Row-aligned tiles keep every 16-lane group of a fragment read on consecutive pixels.
-        if (j + 1 < nsteps) {
-          int ad[3][3][3], prow[3][3], pcol[3][3];
+  for (int J = 0; J <= K * sb; ++J) {
+    // The next step's new input rows 8J+9 .. 8J+16 (8 DMA pieces per row, one per chunk
+    // plane): waves 0-1 (layer l, 36 more MFMAs per step) kF2L1Rows rows each, waves 2-3 the rest.
+    const int row0 = 8 * J + 9 + (layer ? 2 * kF2L1Rows + (4 - kF2L1Rows) * m : kF2L1Rows * m);
+    auto piece = [&](int i) {                            // piece i: plane i & 7 of row row0 + (i >> 3)
+      if ((i & 7) == 0) dma_at(row0 + (i >> 3), kJ);
+      dma_plane(i & 7);
+    };
+    if (layer == 0) {
+      const int x0 = gcx;
+      if (J < K * sb && 8 * jb < s.H) {
+        // intermediate rows 8jb .. 8jb+7 of strip kJ: N-tile k < 8 = row 8jb+k, columns 1 .. 32 of
+        // the ring; N-tile 8 = the strip halo, columns 0 and 33 of the 8 rows (16 pixels, lanes
+        // 16-31 repeat lanes 0-15 and store nothing); 3 groups of 3.  Row-aligned tiles keep
+        // every 16-lane group of a fragment read on consecutive pixels.
+        int ad[3][3][3], prow[3][3], pcol[3][3];
 #pragma unroll
-          for (int g = 0; g < 3; ++g)
+        for (int g = 0; g < 3; ++g)
 #pragma unroll
-            for (int n = 0; n < 3; ++n) {
-              const int k = 3 * g + n;
-              prow[g][n] = k < 8 ? k : (col & 15) >> 1;
-              pcol[g][n] = k < 8 ? 1 + col : ((col & 1) ? kF2MidW - 1 : 0);
+          for (int n = 0; n < 3; ++n) {
+            const int k = 3 * g + n;
+            prow[g][n] = k < 8 ? k : (col & 15) >> 1;
+            pcol[g][n] = k < 8 ? 1 + col : ((col & 1) ? kF2MidW - 1 : 0);
 #pragma unroll
-              for (int dy = 0; dy < 3; ++dy)
-                ad[g][n][dy] = h * kF2InPlane + (f2_slot(8 * j + prow[g][n] - 1 + dy) * kF2InW + pcol[g][n]) * 16;
-            }
-          floatx16 acc[3][3];
-          f2_stream<3, 3, kF2InPlane>(
-              wA, ring, ad, acc,
-              [&](int g, int n, int hf) {
-                if (3 * g + n == 8 && col >= 16) return;
-                const int y1 = 8 * j + prow[g][n], x = x0 - 1 + pcol[g][n];
-                const bool inside = y1 < s.H && x >= 0 && x < s.W;
-                half8_t v = bias_act8_s<ACT>(acc[g][n], 8 * hf, bl + 8 * hf);
-                if (!inside) v = half8_t{};      // the next layer's zero padding
-                *reinterpret_cast<half8_t*>(mid + (4 * m + 2 * h + hf) * kF2MidPlane +
-                                            (f2_slot(y1) * kF2MidW + pcol[g][n]) * 16) = v;
-              },
-              [&](int fs) {
-                if ((fs & 3) == 2 && (fs >> 2) < 8) piece(fs >> 2);
-              });
-        } else {
-#pragma unroll 1
-          for (int i = 0; i < 8; ++i) piece(i);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMAs have landed
+            for (int dy = 0; dy < 3; ++dy)
+              ad[g][n][dy] = h * kF2InPlane + (f2_slot(8 * J + prow[g][n] - 1 + dy) * kF2InW + pcol[g][n]) * 16;
+          }
+        floatx16 acc[3][3];
+        half8_t stage;
+        f2_stream<3, 3, kF2InPlane>(
+            wA, ring, ad, acc,
+            [&](int g, int n, int q) {           // part q: rows 8 hf + NV sub .. of the accumulator
+              constexpr int PH = kF2EpiParts / 2, NV = 8 / PH;
+              const int hf = q / PH, sub = q % PH;
+              bias_act_s<ACT, NV>(stage, sub, acc[g][n], 8 * hf, bl + 8 * hf);
+              if (sub != PH - 1 || (3 * g + n == 8 && col >= 16)) return;
+              const int x = x0 - 1 + pcol[g][n];
+              const bool inside = 8 * jb + prow[g][n] < s.H && x >= 0 && x < s.W;
+              *reinterpret_cast<half8_t*>(mid + (4 * m + 2 * h + hf) * kF2MidPlane +
+                                          (f2_slot(8 * J + prow[g][n]) * kF2MidW + pcol[g][n]) * 16) =
+                  inside ? stage : half8_t{};   // zero outside the image: the next layer's padding
+            },
+            [&](int fs) {
+              if ((fs & 3) == 2 && (fs >> 2) < 8 * kF2L1Rows) piece(fs >> 2);
+            });
       } else {
-        if (j > 0) {
-          // output rows 8j-9 .. 8j-2 (N-tile k = row 8j-9+k, pixel = column), 2 groups of 4
-          int ad[2][4][3];
-#pragma unroll
-          for (int g = 0; g < 2; ++g)
-#pragma unroll
-            for (int n = 0; n < 4; ++n)
-#pragma unroll
-              for (int dy = 0; dy < 3; ++dy)
-                ad[g][n][dy] = h * kF2MidPlane + (f2_slot(8 * j - 9 + 4 * g + n - 1 + dy) * kF2MidW + col) * 16;
-          floatx16 acc[2][4];
-          const int ncols = min(kTileW, s.W - x0);
-          f2_stream<2, 4, kF2MidPlane>(
-              wA, mid, ad, acc,
-              [&](int g, int n, int hf) {
-                const int y = 8 * j - 9 + 4 * g + n;
-                const half8_t v = bias_act8_s<ACT>(acc[g][n], 8 * hf, bl + 8 * hf);
-                half_t* row = out + (((size_t)b * s.Hp + y + s.pad) * s.Wp + x0 + s.pad) * kWidth;
-                const bool ok = y >= 0 && y < s.H;
-                const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-                    ok ? (void*)row : (void*)out, (short)0, ok ? ncols * 128 : 0, 0x00020000);
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i_t, v), rs,
-                                                       (unsigned)(col * 128 + 64 * m + 32 * h + 16 * hf), 0, 0);
-              },
-              [&](int fs) {
-                if (fs < 24) piece(fs);          // every piece before the first store
-              });
-          asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // the DMAs (older than the 16 stores) landed
-        } else {
+        // a block below the image (or past the last strip): zero rows, no MFMAs
 #pragma unroll 1
-          for (int i = 0; i < 24; ++i) piece(i);
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        for (int i = 0; i < 8 * kF2L1Rows; ++i) piece(i);
+        for (int q = lane; q < 8 * kF2MidW * 4; q += 64) {   // 8 rows x 34 pixels x this M-tile's 4 planes
+          const int c = q / (8 * kF2MidW), p = q - c * (8 * kF2MidW), rr = p / kF2MidW, pc = p - rr * kF2MidW;
+          *reinterpret_cast<v4i_t*>(mid + (4 * m + c) * kF2MidPlane + (f2_slot(8 * J + rr) * kF2MidW + pc) * 16) =
+              v4i_t{0, 0, 0, 0};
         }
       }
-      __syncthreads();
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMAs have landed
+    } else {
+      if (J > 0) {
+        // global output rows 8J-9 .. 8J-2 (N-tile t = row 8J-9+t, pixel = column), 2 groups of 4
+        int ad[2][4][3];
+#pragma unroll
+        for (int g = 0; g < 2; ++g)
+#pragma unroll
+          for (int n = 0; n < 4; ++n)
+#pragma unroll
+            for (int dy = 0; dy < 3; ++dy)
+              ad[g][n][dy] = h * kF2MidPlane + (f2_slot(8 * J - 9 + 4 * g + n - 1 + dy) * kF2MidW + col) * 16;
+        __amdgpu_buffer_rsrc_t ors[8];                     // output row 8J-9+t (none: stores dropped)
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          const int R = 8 * J - 9 + t;
+          int k, r;
+          locate(R, kJ, k, r);
+          const bool ok = R >= 0 && k < K && r < s.H;
+          const SGeom G = pick(k);
+          half_t* row = out + (((size_t)G.b * s.Hp + r + s.pad) * s.Wp + G.x0 + s.pad) * kWidth;
+          ors[t] = __builtin_amdgcn_make_buffer_rsrc(ok ? (void*)row : (void*)out, (short)0,
+                                                     ok ? min(kTileW, s.W - G.x0) * 128 : 0, 0x00020000);
+        }
+        floatx16 acc[2][4];
+        half8_t stage;
+        f2_stream<2, 4, kF2MidPlane>(
+            wA, mid, ad, acc,
+            [&](int g, int n, int q) {
+              constexpr int PH = kF2EpiParts / 2, NV = 8 / PH;
+              const int hf = q / PH, sub = q % PH;
+              bias_act_s<ACT, NV>(stage, sub, acc[g][n], 8 * hf, bl + 8 * hf);
+              if (sub != PH - 1) return;
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i_t, stage), ors[4 * g + n],
+                                                     (unsigned)(col * 128 + 64 * m + 32 * h + 16 * hf), 0, 0);
+            },
+            [&](int fs) {
+              if (fs < 8 * (4 - kF2L1Rows)) piece(fs);   // every piece before the first store
+            });
+        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // the DMAs (older than the 16 stores) landed
+      } else {
+#pragma unroll 1
+        for (int i = 0; i < 8 * (4 - kF2L1Rows); ++i) piece(i);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    }
+    __syncthreads();
+    if (++jb == sb) {
+      jb = 0;
+      ++kJ;
+      gpb = gcb;
+      gpx = gcx;
+      gcb = gnb;
+      gcx = gnx;
+      const SGeom g = geom(kJ + 1);
+      gnb = g.b;
+      gnx = g.x0;
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1030,14 +1097,14 @@ void launch_conv_head(const half_t* in4, half_t* out, const void* w, const void*
 void launch_conv_body_f2(const half_t* in, half_t* out, const void* w1, const float* b1, const void* w2,
                          const float* b2, const ConvShape& s, int act, int num_cus, hipStream_t st) {
   const int strips_x = (s.W + kTileW - 1) / kTileW, nstrips = s.B * strips_x;
-  const int nsteps = (s.H + 1 + 7) / 8 + 1;                 // output rows 8j-9 .. 8j-2 cover 0 .. H-1
+  const int sb = (s.H + 1 + 7) / 8;                         // 8-row blocks per strip: S = 8 sb >= H + 1
   const int grid = nstrips < num_cus ? nstrips : num_cus;
   if (act == 0)
     hipLaunchKernelGGL((conv_body_f2_kernel<0>), dim3(grid), dim3(256), kF2Lds, st, in, out, (const uint4*)w1, b1,
-                       (const uint4*)w2, b2, s, strips_x, nstrips, nsteps);
+                       (const uint4*)w2, b2, s, strips_x, nstrips, sb);
   else
     hipLaunchKernelGGL((conv_body_f2_kernel<1>), dim3(grid), dim3(256), kF2Lds, st, in, out, (const uint4*)w1, b1,
-                       (const uint4*)w2, b2, s, strips_x, nstrips, nsteps);
+                       (const uint4*)w2, b2, s, strips_x, nstrips, sb);
 }
 
 void launch_conv_body_w2(const half_t* in, half_t* out, const void* w, const void* w_lo, const float* bias,
