@@ -233,6 +233,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile", type=int, default=1, help="HIP-event per-kernel timing in the timed region")
     ap.add_argument("--chunk", type=int, default=0, help="images per denoiser pass (0 = auto)")
+    ap.add_argument("--graph", type=int, default=0, choices=[0, 1],
+                    help="1: iteration launches replayed from a hipGraph (not while --profile)")
     ap.add_argument("--body-layers", type=int, default=0, choices=[0, 1, 2],
                     help="body layers per launch on the fp16 path (0 = the library default)")
     ap.add_argument("--ablate", type=int, default=0,
@@ -275,6 +277,8 @@ def main():
     ctx.set_precision(args.precision)
     if args.body_layers:
         ctx.set_body_layers(args.body_layers)
+    if args.graph:
+        ctx.set_graph(args.graph)
     h = load_blur_kernel("blur_1")
     if cfg["op"] == "blur":
         ctx.set_operator(_lib.OP_BLUR, h=h)

@@ -129,8 +129,13 @@ int pnp_set_precision(pnp_ctx* ctx, int precision);
  * activation ping-pong pair would exceed 8 GB (fp16) / 16 GB (fp32)).                */
 enum pnp_tuning_key {
   PNP_TUNE_DENOISE_CHUNK = 1,
-  PNP_TUNE_BODY_LAYERS = 2   /* 64->64 layers per launch: 2 (default; conv_body_f2, the intermediate
-                                stays in LDS) or 1 (conv_body_v3).  Bit-identical results.     */
+  PNP_TUNE_BODY_LAYERS = 2,  /* 64->64 layers per launch: 0 = auto (default: 2 when the batch has
+                                at least one 32-column strip per CU, else 1), 1 (conv_body_v3)
+                                or 2 (conv_body_f2, the intermediate stays in LDS).
+                                Bit-identical results.                                         */
+  PNP_TUNE_GRAPH = 3          /* 1: iteration launches replayed from a hipGraph (two iterations
+                                per replay, methods A/B/C); 0: direct launches (default).
+                                Same results either way.                                       */
 };
 int pnp_set_tuning(pnp_ctx* ctx, int key, int value);
 

@@ -49,7 +49,7 @@ struct pnp_ctx {
   int den_C = 0, den_depth = 0, den_act = 0, den_residual = 1, den_clamp = 1;
   int den_chunk = 0;   // images per denoiser pass; 0 = auto
   int ablate = 0;         // PNP_PROFILING build only: parts of conv_body_v3 skipped, results wrong
-  int body_pair = 1;      // PNP_TUNE_BODY_LAYERS: 2 body layers per launch (conv_body_f2) when 1
+  int body_layers = 0;    // PNP_TUNE_BODY_LAYERS: 0 auto (use_pair), 1 conv_body_v3, 2 conv_body_f2
   bool den_ready = false;
   int prec = PNP_PREC_FP16;   // pnp_set_precision: fp16 MFMA operands (conv.hip) or fp32 (conv32.hip)
   DevBuf head_w, head_b, body_w, body_b, tail_w, tail_b;
@@ -82,6 +82,16 @@ struct pnp_ctx {
   DevBuf scr_u32, scr_u16, scr_act[2], scr_part, scr_theta;
   DevBuf act32[2];   // fp32 hidden activations (PNP_PREC_FP32), shared by the solver and pnp_op_denoise
   DevBuf l1_scr;     // l1-ball select histograms + per-image state (launch_l1_select)
+
+  // graph replay of the iteration launches (small batches): PNP_TUNE_GRAPH
+  int graph_mode = 0;          // 0 off (default), 1 on
+  long long gen = 0;           // bumped by every setter and buffer (re)allocation: a graph built at
+  long long warm_gen = -1;     //   another generation is stale; warm_gen: gen after the last plain step
+  hipGraphExec_t gexec = nullptr;
+  long long gexec_gen = -1;
+  bool capturing = false;      // solver_step is being captured: record unconditionally, itp set
+  const int* itp = nullptr;    // device iteration counter the metric kernels read while captured
+  DevBuf it_dev;
 
   // profiling
   bool prof = false;
@@ -142,8 +152,10 @@ void ensure(pnp_ctx* ctx, DevBuf& b, size_t bytes, bool zero = false) {
     b.p = nullptr;
     b.bytes = 0;
   }
+  if (ctx->capturing) fail(ctx, PNP_E_STATE, "allocation inside a graph capture");
   hipError_t e = hipMalloc(&b.p, bytes);
   if (e != hipSuccess) fail(ctx, PNP_E_OOM, "hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
+  ctx->gen++;
   b.bytes = bytes;
   b.geom = -1;
   if (zero) HIPCHK(ctx, hipMemsetAsync(b.p, 0, bytes, ctx->stream));
@@ -244,6 +256,18 @@ void ensure_act(pnp_ctx* ctx, DevBuf (&act)[2], int B, int H, int W, hipStream_t
 // Images per denoiser pass.  Auto: the whole batch, unless its two fp16 activation
 // images (2 x B x (H+2)(W+2) x 128 B) would exceed 8 GB.  (Passes sized to stay in the
 // 256 MB Infinity Cache measured no faster at 256x256: conv_body is not HBM-bound.)
+// Two body layers per launch (conv_body_f2) when its strips fill the chip: one workgroup per
+// 32-column strip walks the strip's rows serially, so a batch with fewer strips than CUs (B = 1
+// at 256^2: 8 strips, 0.23 ms per layer pair) runs one layer per launch over 8 x 32 tiles
+// (256 workgroups, 0.013 ms per layer).  Auto = at least one strip per CU and >= 80 % of the
+// last round of strips busy.
+bool use_pair(pnp_ctx* ctx, int mb, int W) {
+  if (ctx->body_layers) return ctx->body_layers == 2;
+  const long long strips = (long long)mb * ((W + kTileW - 1) / kTileW), cus = ctx->num_cus;
+  const long long rounds = (strips + cus - 1) / cus;
+  return strips >= cus && strips * 5 >= rounds * cus * 4;
+}
+
 int denoise_chunk(pnp_ctx* ctx, int B, int H, int W) {
   if (ctx->den_chunk > 0) return std::min(ctx->den_chunk, B);
   const double per_img = 2.0 * (H + 2 * kActPad) * (W + 2 * kActPad) * kWidth * sizeof(half_t);
@@ -320,10 +344,11 @@ void run_denoiser(pnp_ctx* ctx, const half_t* u16, const float* u32, float* xout
     }
     int cur = 0;
     const int nbody = ctx->den_depth - 2;
+    const bool pair = use_pair(ctx, mb, W);
     for (int l = 0; l < nbody;) {
       const char* wl = (const char*)ctx->body_w.p + (size_t)l * kBodyWBytes;
       const float* bl = P<float>(ctx->body_b) + l * kWidth;
-      if (!w2 && ctx->body_pair && !ctx->ablate && l + 1 < nbody) {   // layers l, l+1 in one launch
+      if (!w2 && pair && !ctx->ablate && l + 1 < nbody) {   // layers l, l+1 in one launch
         ProfScope ps(ctx, "conv_body_f2", st);
         launch_conv_body_f2(P<half_t>(act[cur]), P<half_t>(act[cur ^ 1]), wl, bl, wl + kBodyWBytes, bl + kWidth, s,
                             ctx->den_act, ctx->num_cus, st);
@@ -373,7 +398,7 @@ double l2_eps(pnp_ctx* ctx, size_t n) {
 // iteration.py:189: ssim_data[i] = eval_ssim(x_true, x_n), only when asked (record_ssim)
 bool want_ssim(pnp_ctx* ctx) {
   const pnp_params& p = ctx->prm;
-  return p.record_metrics && p.record_ssim && ctx->has_true && ctx->it < ctx->cap;
+  return p.record_metrics && p.record_ssim && ctx->has_true && (ctx->capturing || ctx->it < ctx->cap);
 }
 
 // mm_chunks > 0: K2 already wrote x+'s (min, max) partials to ctx->ssim_mm
@@ -381,7 +406,7 @@ void record_ssim(pnp_ctx* ctx, const float* xn, hipStream_t st, int mm_chunks = 
   if (!want_ssim(ctx)) return;
   ProfScope ps(ctx, "ssim", st);
   launch_ssim(P<float>(ctx->xtrue), xn, ctx->ssim_scr.p, P<double>(ctx->metrics), ctx->B, ctx->C, ctx->H, ctx->W,
-              ctx->it, ctx->cap, st, mm_chunks > 0 ? P<float>(ctx->ssim_mm) : nullptr, mm_chunks);
+              ctx->it, ctx->cap, st, mm_chunks > 0 ? P<float>(ctx->ssim_mm) : nullptr, mm_chunks, ctx->itp);
   check_launch(ctx, "ssim");
 }
 
@@ -394,7 +419,7 @@ void solver_iteration(pnp_ctx* ctx) {
   float* xo = P<float>(ctx->x[ctx->cur]);
   float* xn = P<float>(ctx->x[ctx->cur ^ 1]);
   const bool mb = ctx->method == PNP_METHOD_B;
-  const int record = p.record_metrics && ctx->it < ctx->cap;
+  const int record = p.record_metrics && (ctx->capturing || ctx->it < ctx->cap);
   {
     ProfScope ps(ctx, "k1_primal_pre", st);
     launch_k1(od.kind, xo, P<float>(ctx->y), P<float>(ctx->s), P<float>(ctx->u32), P<half_t>(ctx->u16),
@@ -421,10 +446,11 @@ void solver_iteration(pnp_ctx* ctx) {
   {
     ProfScope ps(ctx, "k3_dual", st);
     launch_k3(ctx->method, P<float>(ctx->y), P<float>(ctx->xobs), P<double>(ctx->partials), od, B, C, H, W, p.gamma2,
-              l2_eps(ctx, n), P<double>(ctx->metrics), ctx->it, ctx->cap, record, ctx->has_true, st);
+              l2_eps(ctx, n), P<double>(ctx->metrics), ctx->it, ctx->cap, record, ctx->has_true, st, ctx->itp);
     check_launch(ctx, "k3");
   }
   record_ssim(ctx, xn, st, mm_chunks);
+  if (ctx->capturing) launch_it_advance(P<int>(ctx->it_dev), st);
   ctx->cur ^= 1;
   ctx->it += 1;
 }
@@ -639,7 +665,86 @@ void solver_step(pnp_ctx* ctx) {
   else solver_iteration_cmp(ctx);
 }
 
+// ---- graph replay ----------------------------------------------------------------------
+// Two iterations (x ping-pong back to the same buffer) are captured once into a hipGraph and
+// replayed; the metric kernels then take the iteration number (their metrics row) from a
+// device counter the graph advances.  The kernels and their arguments are those of the plain
+// path, so the results are the same bits.  Any setter or (re)allocation bumps ctx->gen and
+// the next run recaptures.  Off by default: measured at B = 1 (cfg1 / cfg2, 0.22-0.25 ms per
+// iteration) the GPU work outlasts the host's launches, so replays gain nothing there; it is
+// for hosts that are slower or busy (small batches).
+bool graph_enabled(pnp_ctx* ctx) {
+  if (ctx->prof || ctx->graph_mode != 1) return false;
+  return ctx->method == PNP_METHOD_A || ctx->method == PNP_METHOD_B || ctx->method == PNP_METHOD_C;
+}
+
+void graph_release(pnp_ctx* ctx) {
+  if (ctx->gexec) (void)hipGraphExecDestroy(ctx->gexec);
+  ctx->gexec = nullptr;
+  ctx->gexec_gen = -1;
+}
+
+void graph_build(pnp_ctx* ctx) {
+  graph_release(ctx);
+  ensure(ctx, ctx->it_dev, sizeof(int));
+  const int it0 = ctx->it, cur0 = ctx->cur;
+  hipGraph_t g = nullptr;
+  HIPCHK(ctx, hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
+  ctx->capturing = true;
+  ctx->itp = P<int>(ctx->it_dev);
+  try {
+    solver_step(ctx);
+    solver_step(ctx);
+  } catch (...) {
+    ctx->capturing = false;
+    ctx->itp = nullptr;
+    (void)hipStreamEndCapture(ctx->stream, &g);
+    if (g) (void)hipGraphDestroy(g);
+    ctx->it = it0;
+    ctx->cur = cur0;
+    throw;
+  }
+  ctx->capturing = false;
+  ctx->itp = nullptr;
+  ctx->it = it0;
+  ctx->cur = cur0;
+  HIPCHK(ctx, hipStreamEndCapture(ctx->stream, &g));
+  const hipError_t e = hipGraphInstantiate(&ctx->gexec, g, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(g);
+  if (e != hipSuccess) {
+    ctx->gexec = nullptr;
+    fail(ctx, PNP_E_HIP, "hipGraphInstantiate: %s", hipGetErrorString(e));
+  }
+  ctx->gexec_gen = ctx->gen;
+}
+
+// n iterations: plain steps until the state is warm (no allocation pending) and x sits in
+// buffer 0, then graph replays of two iterations, then a plain step for an odd remainder.
+void solver_run(pnp_ctx* ctx, int n) {
+  auto plain = [&] {
+    solver_step(ctx);
+    ctx->warm_gen = ctx->gen;
+  };
+  if (!graph_enabled(ctx)) {
+    for (int i = 0; i < n; ++i) plain();
+    return;
+  }
+  while (n > 0 && (ctx->cur != 0 || ctx->warm_gen != ctx->gen)) {
+    plain();
+    --n;
+  }
+  if (n >= 2) {
+    if (!ctx->gexec || ctx->gexec_gen != ctx->gen) graph_build(ctx);
+    HIPCHK(ctx, hipMemsetD32Async((hipDeviceptr_t)ctx->it_dev.p, ctx->it, 1, ctx->stream));
+    for (int k = 0; k < n / 2; ++k) HIPCHK(ctx, hipGraphLaunch(ctx->gexec, ctx->stream));
+    ctx->it += 2 * (n / 2);
+    n &= 1;
+  }
+  if (n) plain();
+}
+
 void solver_setup(pnp_ctx* ctx, int method, const pnp_params* params, int B, int C, int H, int W, int cap) {
+  ctx->gen++;
   if (!params) fail(ctx, PNP_E_ARG, "params is NULL");
   if (method < PNP_METHOD_A || method > PNP_METHOD_C_RED)
     fail(ctx, PNP_E_UNSUPPORTED, "method %d not supported on device", method);
@@ -698,6 +803,7 @@ void solver_setup(pnp_ctx* ctx, int method, const pnp_params* params, int B, int
 }
 
 void solver_reset_state(pnp_ctx* ctx) {
+  ctx->gen++;
   check_operator_shape(ctx, ctx->H, ctx->W);
   if (ctx->op_kind == PNP_OP_BLUR && (ctx->op_R > ctx->H || ctx->op_R > ctx->W))
     fail(ctx, PNP_E_ARG, "blur kernel radius %d larger than the image", ctx->op_R);
@@ -813,6 +919,8 @@ int pnp_destroy(pnp_ctx* ctx) {
                     &ctx->dg_img, &ctx->dg_draws, &ctx->dg_first, &ctx->dg_status,
                     &ctx->head_w32, &ctx->body_w32, &ctx->tail_w32, &ctx->act32[0], &ctx->act32[1], &ctx->l1_scr, &ctx->ssim_mm, &ctx->head_wlo, &ctx->body_wlo, &ctx->tail_wlo};
   for (DevBuf* b : bufs) release(*b);
+  graph_release(ctx);
+  release(ctx->it_dev);
   for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
@@ -829,14 +937,20 @@ int pnp_synchronize(pnp_ctx* ctx) {
 int pnp_set_tuning(pnp_ctx* ctx, int key, int value) {
   if (!ctx) return PNP_E_ARG;
   return guarded(ctx, [&] {
+    ctx->gen++;
+    if (key == PNP_TUNE_GRAPH) {
+      if (value < 0 || value > 1) fail(ctx, PNP_E_ARG, "graph mode must be 0 (off) or 1 (on)");
+      ctx->graph_mode = value;
+      return;
+    }
     if (key == PNP_TUNE_DENOISE_CHUNK) {
       if (value < 0) fail(ctx, PNP_E_ARG, "chunk must be >= 0");
       ctx->den_chunk = value;
       return;
     }
     if (key == PNP_TUNE_BODY_LAYERS) {
-      if (value != 1 && value != 2) fail(ctx, PNP_E_ARG, "body layers per launch must be 1 or 2");
-      ctx->body_pair = value == 2;
+      if (value < 0 || value > 2) fail(ctx, PNP_E_ARG, "body layers per launch must be 0 (auto), 1 or 2");
+      ctx->body_layers = value;
       return;
     }
 #ifdef PNP_PROFILING
@@ -855,6 +969,7 @@ int pnp_set_precision(pnp_ctx* ctx, int precision) {
     if (precision != PNP_PREC_FP16 && precision != PNP_PREC_FP32 && precision != PNP_PREC_FP16W2)
       fail(ctx, PNP_E_UNSUPPORTED, "precision %d not supported", precision);
     ctx->prec = precision;
+    ctx->gen++;
   });
 }
 
@@ -862,6 +977,7 @@ int pnp_set_denoiser(pnp_ctx* ctx, int channels, int depth, int width, const flo
                      int activation, int residual_sign, int clamp_io) {
   if (!ctx) return PNP_E_ARG;
   return guarded(ctx, [&] {
+    ctx->gen++;
     if (width != kWidth) fail(ctx, PNP_E_UNSUPPORTED, "width %d unsupported (only 64)", width);
     if (channels < 1 || channels > kMaxC) fail(ctx, PNP_E_UNSUPPORTED, "channels %d unsupported (1..4)", channels);
     if (depth < 3) fail(ctx, PNP_E_UNSUPPORTED, "depth %d < 3", depth);
@@ -947,6 +1063,7 @@ int pnp_set_operator(pnp_ctx* ctx, int kind, const double* h, int kh, int kw, co
                      int W) {
   if (!ctx) return PNP_E_ARG;
   return guarded(ctx, [&] {
+    ctx->gen++;
     // the loaded solver state depends on the operator (the Poisson-ADMM c1 = Phi^T 1 and the
     // shape checks of solver_setup): a new operator needs pnp_solver_load / pnp_run again
     ctx->loaded = false;
@@ -1069,7 +1186,7 @@ int pnp_solver_iterate(pnp_ctx* ctx, int n_iter) {
       ctx->prof_log.clear();
       ctx->ev_used = 0;
     }
-    for (int i = 0; i < n_iter; ++i) solver_step(ctx);
+    solver_run(ctx, n_iter);
   });
 }
 
@@ -1111,7 +1228,7 @@ int pnp_run(pnp_ctx* ctx, int method, const pnp_params* params, int B, int C, in
     solver_reset_state(ctx);
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     const auto t0 = std::chrono::steady_clock::now();
-    for (int i = 0; i < max_iter; ++i) solver_step(ctx);
+    solver_run(ctx, max_iter);
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     if (avg_time_s) *avg_time_s = max_iter ? dt / max_iter : 0.0;
@@ -1121,6 +1238,7 @@ int pnp_run(pnp_ctx* ctx, int method, const pnp_params* params, int B, int C, in
 
 int pnp_profile_enable(pnp_ctx* ctx, int enable) {
   if (!ctx) return PNP_E_ARG;
+  ctx->gen++;
   ctx->prof = enable != 0;
   ctx->prof_log.clear();
   ctx->ev_used = 0;

@@ -83,7 +83,7 @@ int k2_minmax_chunks(int C, int H, int W);
 void launch_k3(int method, float* y, const float* xobs, const double* partials, const OpDesc& op, int B, int C,
                int H, int W,
                double gamma2, double eps, double* metrics, int it, int cap, int record, int has_true,
-               hipStream_t st);
+               hipStream_t st, const int* itp = nullptr);
 int partial_tiles(int H, int W);
 int k2_partials(const OpDesc& op, int C, int H, int W);   // partial-sum entries per image written by launch_k2
 int chunk_count(size_t n);
@@ -142,13 +142,15 @@ constexpr int kMetrics = 3;
 size_t ssim_scratch_bytes(int B, int C, int H, int W);
 // mm_ext / mm_chunks: x's (min, max) partials from launch_k2, or null (then computed here)
 void launch_ssim(const float* xt, const float* x, void* scratch, double* metrics, int B, int C, int H, int W,
-                 int it, int cap, hipStream_t st, const float* mm_ext = nullptr, int mm_chunks = 0);
+                 int it, int cap, hipStream_t st, const float* mm_ext = nullptr, int mm_chunks = 0, const int* itp = nullptr);
 // comparisonB-2: out = k + ca*a + cb*b + cc*c + cd*d (null inputs skipped), fp64 arithmetic
 void launch_lincomb(float* out, double k, const float* a, double ca, const float* b, double cb, const float* c,
                     double cc, const float* d, double cd, size_t count, hipStream_t st);
 // c_n / PSNR of xn against xo / xt into metrics[b][it] (partials: B * chunk_count(n) * 4 doubles)
 void launch_metrics(const float* xn, const float* xo, const float* xt, double* partials, double* metrics, int B,
-                    size_t n, int it, int cap, hipStream_t st);
+                    size_t n, int it, int cap, hipStream_t st, const int* itp = nullptr);
+// graph replays: the iteration number (metrics row) lives in device memory, advanced per iteration
+void launch_it_advance(int* itp, hipStream_t st);
 void launch_pack_input(const float* x, float* u32, half_t* u16, int B, int C, int H, int W, int clamp_in,
                        hipStream_t st);
 

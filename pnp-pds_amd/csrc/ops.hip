@@ -461,6 +461,7 @@ __device__ __forceinline__ void reduce_partials(const double* __restrict__ parti
 
 __device__ __forceinline__ void write_metrics(double* metrics, int b, int it, int cap, const double (&a)[4],
                                               double n_elem, int has_true) {
+  if (it >= cap) return;                                            // (graph replays run past the record)
   double* m = metrics + ((size_t)b * cap + it) * kMetrics;
   m[0] = sqrt(a[1]) / sqrt(a[2]);                                   // iteration.py:187
   m[1] = has_true ? 10.0 * log10(1.0 / (a[3] / n_elem)) : __builtin_nan("");   // utils_eval.py:4-7
@@ -473,9 +474,11 @@ __device__ __forceinline__ void write_metrics(double* metrics, int b, int it, in
 __global__ __launch_bounds__(256) void k3_l2_dual(float* __restrict__ y, const float* __restrict__ xobs,
                                                    const double* __restrict__ partials, int tiles, size_t n,
                                                    double gamma2, double eps, double* __restrict__ metrics,
-                                                   int it, int cap, int record, int has_true) {
+                                                   int it, int cap, int record, int has_true,
+                                                   const int* __restrict__ itp) {
   __shared__ double red[4];
   const int b = blockIdx.y;
+  if (itp) it = *itp;                        // graph replay: the iteration number from the device counter
   double a[4];
   reduce_partials(partials, b, tiles, a, red);
   const double nrm = sqrt(a[0]);
@@ -491,9 +494,11 @@ __global__ __launch_bounds__(256) void k3_l2_dual(float* __restrict__ y, const f
 }
 
 __global__ __launch_bounds__(256) void k3_metrics(const double* __restrict__ partials, int tiles, size_t n,
-                                                   double* __restrict__ metrics, int it, int cap, int has_true) {
+                                                   double* __restrict__ metrics, int it, int cap, int has_true,
+                                                   const int* __restrict__ itp) {
   __shared__ double red[4];
   double a[4];
+  if (itp) it = *itp;
   reduce_partials(partials, blockIdx.x, tiles, a, red);
   if (threadIdx.x == 0) write_metrics(metrics, blockIdx.x, it, cap, a, (double)n, has_true);
 }
@@ -1422,9 +1427,11 @@ __global__ __launch_bounds__(256) void ssim_gray_kernel(const float* __restrict_
 // per image: RGB mean over channels of (sum S / cropped count); gray mean over rows
 __global__ __launch_bounds__(256) void ssim_final_kernel(const double* __restrict__ ps, const float* __restrict__ rows,
                                                          double* __restrict__ metrics, int C, int H, int W, int tiles,
-                                                         int gray, int it, int cap) {
+                                                         int gray, int it, int cap, const int* __restrict__ itp) {
   __shared__ double red[4];
   const int b = blockIdx.x;
+  if (itp) it = *itp;
+  if (it >= cap) return;
   double val;
   if (gray) {
     double a = 0;
@@ -1663,19 +1670,24 @@ int k2_partials(const OpDesc& op, int C, int H, int W) {
 
 void launch_k3(int method, float* y, const float* xobs, const double* partials, const OpDesc& op, int B, int C,
                int H, int W, double gamma2, double eps, double* metrics, int it, int cap, int record, int has_true,
-               hipStream_t st) {
+               hipStream_t st, const int* itp) {
   TileGrid g = tile_grid(H, W);
   g.tiles = k2_partials(op, C, H, W);
   const size_t n = (size_t)C * H * W;
   if (method == M_C) {
     if (record) hipLaunchKernelGGL(k3_metrics, dim3(B), dim3(256), 0, st, partials, g.tiles, n, metrics, it, cap,
-                                   has_true);
+                                   has_true, itp);
     return;
   }
   const int chunks = (int)((n + 2047) / 2048);
   hipLaunchKernelGGL(k3_l2_dual, dim3(chunks, B), dim3(256), 0, st, y, xobs, partials, g.tiles, n, gamma2, eps,
-                     metrics, it, cap, record, has_true);
+                     metrics, it, cap, record, has_true, itp);
 }
+
+__global__ void it_advance_kernel(int* itp) {
+  if (threadIdx.x == 0) *itp += 1;
+}
+void launch_it_advance(int* itp, hipStream_t st) { hipLaunchKernelGGL(it_advance_kernel, dim3(1), dim3(64), 0, st, itp); }
 
 void launch_l1_select(const float* v, float* theta, void* scratch, int B, size_t n, double eta, hipStream_t st) {
   L1Scratch* scr = reinterpret_cast<L1Scratch*>(scratch);
@@ -1765,10 +1777,10 @@ void launch_lincomb(float* out, double k, const float* a, double ca, const float
 }
 
 void launch_metrics(const float* xn, const float* xo, const float* xt, double* partials, double* metrics, int B,
-                    size_t n, int it, int cap, hipStream_t st) {
+                    size_t n, int it, int cap, hipStream_t st, const int* itp) {
   const int chunks = chunk_count(n);
   hipLaunchKernelGGL(metric_partials_kernel, dim3(chunks, B), dim3(256), 0, st, xn, xo, xt, partials, n, chunks);
-  hipLaunchKernelGGL(k3_metrics, dim3(B), dim3(256), 0, st, partials, chunks, n, metrics, it, cap, xt ? 1 : 0);
+  hipLaunchKernelGGL(k3_metrics, dim3(B), dim3(256), 0, st, partials, chunks, n, metrics, it, cap, xt ? 1 : 0, itp);
 }
 
 }  // namespace pnp
@@ -1783,7 +1795,7 @@ size_t ssim_scratch_bytes(int B, int C, int H, int W) {
 }
 
 void launch_ssim(const float* xt, const float* x, void* scratch, double* metrics, int B, int C, int H, int W,
-                 int it, int cap, hipStream_t st, const float* mm_ext, int mm_chunks) {
+                 int it, int cap, hipStream_t st, const float* mm_ext, int mm_chunks, const int* itp) {
   const size_t n = (size_t)C * H * W;
   int chunks = chunk_count(n);
   const int tx = (W + kSsTW - 1) / kSsTW, tiles = tx * ((H + kSsTH - 1) / kSsTH);
@@ -1803,7 +1815,8 @@ void launch_ssim(const float* xt, const float* x, void* scratch, double* metrics
   else
     hipLaunchKernelGGL(ssim_rgb_kernel, dim3(tiles, B * C), dim3(256), 0, st, xt, x, mm, ps, C, H, W, tx, tiles,
                        chunks);
-  hipLaunchKernelGGL(ssim_final_kernel, dim3(B), dim3(256), 0, st, ps, rows, metrics, C, H, W, tiles, gray, it, cap);
+  hipLaunchKernelGGL(ssim_final_kernel, dim3(B), dim3(256), 0, st, ps, rows, metrics, C, H, W, tiles, gray, it, cap,
+                     itp);
 }
 
 }  // namespace pnp

@@ -27,6 +27,7 @@ PREC_FP16, PREC_FP32, PREC_FP16W2 = 0, 1, 2
 PRECISIONS = {"fp16": PREC_FP16, "fp32": PREC_FP32, "fp16w2": PREC_FP16W2}
 TUNE_DENOISE_CHUNK = 1
 TUNE_BODY_LAYERS = 2
+TUNE_GRAPH = 3
 TUNE_ABLATE = 3          # profiling build only (make PROFILING=1, lib_prof/): not in include/pnppds.h
 
 
@@ -231,8 +232,14 @@ class Context:
         """Images per denoiser pass (0 = auto).  Performance only."""
         self._check(self.lib.pnp_set_tuning(self.h, TUNE_DENOISE_CHUNK, int(images)))
 
+    def set_graph(self, mode: int):
+        """Iteration launches replayed from a hipGraph: 1 = on, 0 = off (default).  Same results
+        either way (methods A/B/C; the others always launch directly)."""
+        self._check(self.lib.pnp_set_tuning(self.h, TUNE_GRAPH, int(mode)))
+
     def set_body_layers(self, n: int):
-        """64->64 denoiser layers per launch: 2 (default, fused) or 1.  Same bits either way."""
+        """64->64 denoiser layers per launch: 0 = auto (default; fused pairs when the batch has a
+        32-column strip per CU), 1 or 2.  Same bits either way."""
         self._check(self.lib.pnp_set_tuning(self.h, TUNE_BODY_LAYERS, int(n)))
 
     def set_ablate(self, bits: int):

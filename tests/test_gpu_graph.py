@@ -1,0 +1,70 @@
+"""hipGraph replay of the iteration launches (PNP_TUNE_GRAPH) gives the same bits as direct
+launches: x, s and every recorded metric (c_n, PSNR, SSIM), for ours-A/B/C, odd and even
+iteration counts, iterations split over several pnp_solver_iterate calls, metrics capacity
+shorter than the run, and a rebuild after a setter changes the state."""
+import numpy as np
+import pytest
+
+from conftest import load_golden
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup(case, B):
+    from pnppds import _lib
+    from pnppds import operators as ops
+    from pnppds.iteration import make_params, resolve_method, resolve_precision
+    from pnppds.weights import resolve_weights
+    g = load_golden(f"iter_{case}.npz")
+    g1, g2, as_, an, lam, m1, m2, gadmm, sig, sp, palpha, iters, ch, r = g["params"]
+    ctx = _lib.Context(0)
+    m = resolve_method(str(g["method"]))
+    ctx.set_precision(resolve_precision("auto", m))
+    ctx.set_denoiser(resolve_weights(str(g["arch"]), int(ch)))
+    phi, _ = ops.get_observation_operators(str(g["deg_op"]), "blur_1", r)
+    phi.configure(ctx, g["x_0"].shape[-2], g["x_0"].shape[-1])
+    prm = make_params(g1, g2, as_, an, lam, int(m1), int(m2), gadmm, sig, sp, palpha, r, True, True)
+    rng = np.random.default_rng(1)
+    x0 = np.stack([g["x_0"]] * B) + 0.01 * rng.standard_normal((B,) + g["x_0"].shape)
+    xo = np.stack([g["x_obs"]] * B).astype(np.float32)
+    xt = np.stack([g["x_true"]] * B).astype(np.float32)
+    return ctx, m, prm, x0.astype(np.float32), xo, xt
+
+
+@pytest.mark.parametrize("case,B,iters", [("A_blur", 1, 7), ("A_rs", 2, 6), ("B_blur", 1, 5), ("C_rs", 2, 5)])
+def test_graph_equals_direct_launches(case, B, iters):
+    ctx, m, prm, x0, xo, xt = _setup(case, B)
+    ctx.set_graph(0)
+    ref = ctx.run(m, prm, x0, xo, xt, iters)
+    ctx.set_graph(1)
+    got = ctx.run(m, prm, x0, xo, xt, iters)
+    for a, b in zip(ref[:5], got[:5]):
+        np.testing.assert_array_equal(a, b)
+    assert np.isfinite(got[3]).all() and np.isfinite(got[4]).all()   # every PSNR / SSIM row written
+
+
+def test_graph_split_iterate_and_short_capacity():
+    """Iterations in several calls (odd counts: plain steps realign the x ping-pong), a metrics
+    capacity shorter than the run (the counter runs past it), and a setter between calls (the
+    graph is recaptured)."""
+    ctx, m, prm, x0, xo, xt = _setup("A_blur", 1)
+    B, Cc, H, W = x0.shape
+    out = {}
+    for mode in (0, 1):
+        ctx.set_graph(mode)
+        ctx.solver_setup(m, prm, B, Cc, H, W, 6)
+        ctx.solver_load(x0, xo, xt)
+        ctx.solver_iterate(3)
+        ctx.solver_iterate(4)
+        ctx.set_denoise_chunk(1)                      # bumps the state generation
+        ctx.solver_iterate(2)
+        out[mode] = ctx.solver_fetch()
+    for a, b in zip(out[0], out[1]):
+        np.testing.assert_array_equal(a, b)
+    assert np.isfinite(out[1][2]).all()               # c rows 0..5 written, rows past 6 dropped
+
+
+def test_graph_mode_rejects_bad_values(gpu_ctx):
+    from pnppds._lib import PnpError
+    with pytest.raises(PnpError):
+        gpu_ctx.set_graph(2)
