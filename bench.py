@@ -354,6 +354,8 @@ def main():
             line["kernel_calls_per_step"] = {k: round(v[1] / K, 2) for k, v in prof.items()}
             fp32 = args.precision == "fp32"
             kname = {"fp32": "conv32_body", "fp16w2": "conv_body_w2"}.get(args.precision, "conv_body")
+            if kname == "conv_body" and "conv_body_f2" in prof:
+                kname = "conv_body_f2"
             if kname in prof:
                 body_ms = prof[kname][0]
                 m = images_per_launch(B, H, W, args.chunk, fp32)
@@ -373,6 +375,14 @@ def main():
                                         "unit": "TFLOP/s (MFMA work, 2x algorithmic)",
                                         "frac": round(2 * tfl / FP16_PEAK_TFLOPS, 4), "traffic": None,
                                         "bytes_per_launch": by, "flops_per_launch": fl, "hbm_gbs": round(gbs, 1)}
+                elif kname == "conv_body_f2":   # two layers per launch, one read + one write: 576 FLOP/B, MFMA roof
+                    line["roofline"] = {"kernel": "conv_body_f2 (two 64->64 3x3 layers per launch, fp16 MFMA; "
+                                                  "the intermediate stays in LDS)", "bound": "mfma",
+                                        "achieved": round(2 * tfl, 1), "peak": FP16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                                        "frac": round(2 * tfl / FP16_PEAK_TFLOPS, 4), "traffic": traffic,
+                                        "bytes_per_launch": by, "flops_per_launch": 2 * fl, "hbm_gbs": round(gbs, 1),
+                                        "hbm_frac": round(gbs / HBM_PEAK_GBS, 4), "traffic_source": src,
+                                        "ms_per_layer": round(body_ms / 2, 4)}
                 else:      # 288 FLOP/B, below the 2500 / 8 = 312 FLOP/B ridge: HBM roof
                     line["roofline"] = {"kernel": "conv_body (64->64 3x3 implicit GEMM, fp16 MFMA)", "bound": "hbm",
                                         "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

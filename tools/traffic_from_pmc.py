@@ -17,12 +17,12 @@ import csv
 import json
 import re
 
-WIDE_READ = ("conv_body2", "conv_body", "conv_head", "conv_tail")
+WIDE_READ = ("conv_body_f2", "conv_body", "conv_head", "conv_tail")
 
 
 def short(name):
     n = re.sub(r"\(.*", "", name)
-    for k in ("conv_body2", "conv_body", "conv_head", "conv_tail", "k1", "k2", "k3_l2_dual", "l1_select"):
+    for k in ("conv_body_f2", "conv_body", "conv_head", "conv_tail", "k1", "k2", "k3_l2_dual", "l1_", "ssim"):
         if k in n:
             return k
     return None
