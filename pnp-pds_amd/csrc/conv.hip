@@ -393,11 +393,27 @@ __device__ __forceinline__ void f2_stream(const half8_t (&wA)[kBodyKSteps], cons
     side(fs);
     __builtin_amdgcn_sched_barrier(0);       // keep the reads D K-steps ahead of their MFMAs
   }
+  side(T);                                   // (end of the MFMA stream)
 #pragma unroll
   for (int n = 0; n < NT; ++n)
 #pragma unroll
     for (int q = 0; q < kF2EpiParts; ++q) epi(G - 1, n, q);
 }
+
+#ifdef F2_STAMPS
+// Diagnostic build only (tools/f2_stamps.py): per wave, cycles summed over the steps of
+// [0] step setup, [1] MFMA stream, [2] last group's epilogue, [3] DMA wait, [4] barrier wait,
+// [5] steps.  Written to a buffer nothing else reads; never in the product library.
+__device__ unsigned long long f2_stamp_buf[1024 * 4 * 8];
+#define F2_STAMP(k)                                              \
+  do {                                                           \
+    const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
+    st_acc[k] += now_ - st_t;                                    \
+    st_t = now_;                                                 \
+  } while (0)
+#else
+#define F2_STAMP(k) ((void)0)
+#endif
 
 template <int ACT>
 __global__ __launch_bounds__(256, 1) void conv_body_f2_kernel(const half_t* __restrict__ in,
@@ -488,6 +504,9 @@ __global__ __launch_bounds__(256, 1) void conv_body_f2_kernel(const half_t* __re
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
+#ifdef F2_STAMPS
+  unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0}, st_t = __builtin_amdgcn_s_memtime();
+#endif
   for (int J = 0; J <= K * sb; ++J) {
     // The next step's new input rows 8J+9 .. 8J+16 (8 DMA pieces per row, one per chunk
     // plane): waves 0-1 (layer l, 36 more MFMAs per step) kF2L1Rows rows each, waves 2-3 the rest.
@@ -504,19 +523,36 @@ __global__ __launch_bounds__(256, 1) void conv_body_f2_kernel(const half_t* __re
         // 16-31 repeat lanes 0-15 and store nothing); 3 groups of 3.  Row-aligned tiles keep
         // every 16-lane group of a fragment read on consecutive pixels.
         int ad[3][3][3], prow[3][3], pcol[3][3];
+        {
+          int sl = f2_slot(8 * J - 1);                   // input rows 8J-1 .. 8J+8: ring slots stepped
+          int rowoff[10];
 #pragma unroll
-        for (int g = 0; g < 3; ++g)
-#pragma unroll
-          for (int n = 0; n < 3; ++n) {
-            const int k = 3 * g + n;
-            prow[g][n] = k < 8 ? k : (col & 15) >> 1;
-            pcol[g][n] = k < 8 ? 1 + col : ((col & 1) ? kF2MidW - 1 : 0);
-#pragma unroll
-            for (int dy = 0; dy < 3; ++dy)
-              ad[g][n][dy] = h * kF2InPlane + (f2_slot(8 * J + prow[g][n] - 1 + dy) * kF2InW + pcol[g][n]) * 16;
+          for (int q = 0; q < 10; ++q) {
+            rowoff[q] = sl * (kF2InW * 16);
+            sl = sl == kF2Ring - 1 ? 0 : sl + 1;
           }
+          const int hr = (col & 15) >> 1, hc = (col & 1) ? kF2MidW - 1 : 0;   // the halo tile's pixel
+#pragma unroll
+          for (int g = 0; g < 3; ++g)
+#pragma unroll
+            for (int n = 0; n < 3; ++n) {
+              const int k = 3 * g + n;
+              prow[g][n] = k < 8 ? k : hr;
+              pcol[g][n] = k < 8 ? 1 + col : hc;
+#pragma unroll
+              for (int dy = 0; dy < 3; ++dy) {
+                // row k - 1 + dy: uniform for the row tiles; the halo tile's row is per lane
+                int ro = rowoff[0];
+#pragma unroll
+                for (int q = 1; q < 10; ++q)
+                  if (k == 8) ro = hr + dy == q ? rowoff[q] : ro;
+                ad[g][n][dy] = h * kF2InPlane + (k < 8 ? rowoff[k + dy] : ro) + pcol[g][n] * 16;
+              }
+            }
+        }
         floatx16 acc[3][3];
         half8_t stage;
+        F2_STAMP(0);
         f2_stream<3, 3, kF2InPlane>(
             wA, ring, ad, acc,
             [&](int g, int n, int q) {           // part q: rows 8 hf + NV sub .. of the accumulator
@@ -532,7 +568,9 @@ __global__ __launch_bounds__(256, 1) void conv_body_f2_kernel(const half_t* __re
             },
             [&](int fs) {
               if ((fs & 3) == 2 && (fs >> 2) < 8 * kF2L1Rows) piece(fs >> 2);
+              if (fs == 3 * kBodyKSteps) F2_STAMP(1);
             });
+        F2_STAMP(2);
       } else {
         // a block below the image (or past the last strip): zero rows, no MFMAs
 #pragma unroll 1
@@ -544,31 +582,47 @@ __global__ __launch_bounds__(256, 1) void conv_body_f2_kernel(const half_t* __re
         }
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMAs have landed
+      F2_STAMP(3);
     } else {
       if (J > 0) {
         // global output rows 8J-9 .. 8J-2 (N-tile t = row 8J-9+t, pixel = column), 2 groups of 4
+        // mid rows 8J-10 .. 8J-1: ring slots stepped from the first (no per-row modulo)
         int ad[2][4][3];
+        {
+          const int lb = h * kF2MidPlane + col * 16;
+          int sl = f2_slot(8 * J - 10);
+          int rowoff[10];
 #pragma unroll
-        for (int g = 0; g < 2; ++g)
+          for (int q = 0; q < 10; ++q) {
+            rowoff[q] = sl * (kF2MidW * 16);
+            sl = sl == kF2Ring - 1 ? 0 : sl + 1;
+          }
 #pragma unroll
-          for (int n = 0; n < 4; ++n)
+          for (int g = 0; g < 2; ++g)
 #pragma unroll
-            for (int dy = 0; dy < 3; ++dy)
-              ad[g][n][dy] = h * kF2MidPlane + (f2_slot(8 * J - 9 + 4 * g + n - 1 + dy) * kF2MidW + col) * 16;
-        __amdgpu_buffer_rsrc_t ors[8];                     // output row 8J-9+t (none: stores dropped)
+            for (int n = 0; n < 4; ++n)
 #pragma unroll
-        for (int t = 0; t < 8; ++t) {
-          const int R = 8 * J - 9 + t;
+              for (int dy = 0; dy < 3; ++dy) ad[g][n][dy] = lb + rowoff[4 * g + n + dy];
+        }
+        // output rows 8J-9+t (none: stores dropped): strip and row of the first, then row by row
+        __amdgpu_buffer_rsrc_t ors[8];
+        {
           int k, r;
-          locate(R, kJ, k, r);
-          const bool ok = R >= 0 && k < K && r < s.H;
-          const SGeom G = pick(k);
-          half_t* row = out + (((size_t)G.b * s.Hp + r + s.pad) * s.Wp + G.x0 + s.pad) * kWidth;
-          ors[t] = __builtin_amdgcn_make_buffer_rsrc(ok ? (void*)row : (void*)out, (short)0,
-                                                     ok ? min(kTileW, s.W - G.x0) * 128 : 0, 0x00020000);
+          locate(8 * J - 9, kJ, k, r);
+          const bool first = 8 * J - 9 >= 0;
+#pragma unroll
+          for (int t = 0; t < 8; ++t) {
+            if (t > 0 && ++r == S) { r = 0; ++k; }
+            const bool ok = (first || t >= 9 - 8 * J) && k < K && r < s.H;
+            const SGeom G = pick(k);
+            half_t* row = out + (((size_t)G.b * s.Hp + r + s.pad) * s.Wp + G.x0 + s.pad) * kWidth;
+            ors[t] = __builtin_amdgcn_make_buffer_rsrc(ok ? (void*)row : (void*)out, (short)0,
+                                                       ok ? min(kTileW, s.W - G.x0) * 128 : 0, 0x00020000);
+          }
         }
         floatx16 acc[2][4];
         half8_t stage;
+        F2_STAMP(0);
         f2_stream<2, 4, kF2MidPlane>(
             wA, mid, ad, acc,
             [&](int g, int n, int q) {
@@ -581,8 +635,11 @@ __global__ __launch_bounds__(256, 1) void conv_body_f2_kernel(const half_t* __re
             },
             [&](int fs) {
               if (fs < 8 * (4 - kF2L1Rows)) piece(fs);   // every piece before the first store
+              if (fs == 2 * kBodyKSteps) F2_STAMP(1);
             });
+        F2_STAMP(2);
         asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // the DMAs (older than the 16 stores) landed
+        F2_STAMP(3);
       } else {
 #pragma unroll 1
         for (int i = 0; i < 8 * (4 - kF2L1Rows); ++i) piece(i);
@@ -590,6 +647,10 @@ __global__ __launch_bounds__(256, 1) void conv_body_f2_kernel(const half_t* __re
       }
     }
     __syncthreads();
+    F2_STAMP(4);
+#ifdef F2_STAMPS
+    st_acc[5] += 1;
+#endif
     if (++jb == sb) {
       jb = 0;
       ++kJ;
@@ -603,6 +664,10 @@ __global__ __launch_bounds__(256, 1) void conv_body_f2_kernel(const half_t* __re
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#ifdef F2_STAMPS
+  if (lane == 0 && blockIdx.x < 1024)
+    for (int k = 0; k < 6; ++k) f2_stamp_buf[(blockIdx.x * 4 + wave) * 8 + k] = st_acc[k];
+#endif
 }
 
 template __global__ void conv_body_f2_kernel<0>(const half_t* __restrict__, half_t* __restrict__,
@@ -1153,3 +1218,10 @@ void launch_conv_tail(const half_t* in, const float* xin, float* xout, const voi
 }
 
 }  // namespace pnp
+
+#ifdef F2_STAMPS
+extern "C" int pnp_diag_f2_stamps(unsigned long long* host, int n) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(pnp::f2_stamp_buf), (size_t)n * sizeof(unsigned long long), 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
