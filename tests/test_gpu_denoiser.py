@@ -128,12 +128,16 @@ def test_denoiser_fp32_ragged_batched(gpu_ctx, B, C, H, W):
 @pytest.mark.parametrize("name,B,C,H,W", [("DnCNN_nobn_nch_3_nlev_0.01", 3, 3, 50, 70),
                                           ("DnCNN_nobn_nch_3_nlev_0.01", 2, 3, 256, 256),
                                           ("dncnn_15", 2, 1, 37, 45), ("DnCNN_nobn_nch_1_nlev_0.01", 1, 1, 8, 32),
-                                          ("dncnn_color_blind", 1, 3, 9, 33), ("DnCNN_nobn_nch_3_nlev_0.01", 1, 3, 64, 96)])
+                                          ("dncnn_color_blind", 1, 3, 9, 33), ("DnCNN_nobn_nch_3_nlev_0.01", 1, 3, 64, 96),
+                                          # more strips than CUs: workgroups chain strips of different
+                                          # images / columns into one row stream (2-3 strips each)
+                                          ("DnCNN_nobn_nch_3_nlev_0.01", 90, 3, 20, 70), ("dncnn_15", 300, 1, 9, 33)])
 def test_body_two_layers_per_launch_bit_identical(gpu_ctx, name, B, C, H, W):
     """conv_body_f2 (two 64->64 layers per launch, the intermediate in LDS) runs each output's
     MFMA K-sequence and the intermediate's fp16 rounding exactly as two conv_body_v3 launches:
     same bits, for ragged shapes (H % 8, W % 32 != 0, images narrower than a strip), odd
-    layer counts (dncnn_15: 15 body layers) and both activations."""
+    layer counts (dncnn_15: 15 body layers), both activations, and batches with more strips
+    than CUs (each workgroup chains several strips)."""
     rng = np.random.default_rng(11)
     w = DenoiserWeights.load_npz(os.path.join(WEIGHTS_DIR, name + ".npz"))
     x = rng.uniform(0, 1, (B, C, H, W)).astype(np.float32)
