@@ -71,6 +71,24 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def stream_copy_gbs(torch, device, nbytes=1 << 30, reps=10):
+    """Measured HBM copy bandwidth (report the roofline also against a measured
+    STREAM-copy peak): a device-to-device copy of nbytes, read + write counted, best of reps."""
+    a = torch.empty(nbytes // 4, dtype=torch.float32, device=device)
+    b = torch.empty_like(a)
+    a.fill_(1.0)
+    best = float("inf")
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        b.copy_(a)
+        e1.record()
+        e1.synchronize()
+        best = min(best, e0.elapsed_time(e1) * 1e-3)
+    del a, b
+    return 2 * nbytes / best / 1e9
+
+
 def synthetic_batch(B, C, H, W, seed):
     """Structured synthetic images in [0,1] (gradients, sinusoids, rectangles), float32."""
     rng = np.random.default_rng(seed)
@@ -391,8 +409,11 @@ def main():
                                         "mfma_tflops": round(tfl, 1), "mfma_frac": round(tfl / FP16_PEAK_TFLOPS, 4),
                                         "traffic_source": src}
             pb = prox_bytes(cfg["method"], B, C, H, W)
+            copy_gbs = stream_copy_gbs(torch, f"cuda:{local}")
+            line["hbm_copy_gbs"] = round(copy_gbs, 1)
             line["prox_hbm"] = {k: {"GB/s": round(pb[k] / (prof[k][0] * 1e-3) / 1e9, 1),
-                                    "frac": round(pb[k] / (prof[k][0] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+                                    "frac": round(pb[k] / (prof[k][0] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                    "frac_of_copy": round(pb[k] / (prof[k][0] * 1e-3) / 1e9 / copy_gbs, 4)}
                                 for k in pb if k in prof}
         line["psnr_img0_db"] = [round(float(psnr_hist[0, 0]), 4), round(float(psnr_hist[0, cap - 1]), 4)]
         line["ssim_img0"] = [round(float(ssim_hist[0, 0]), 5), round(float(ssim_hist[0, cap - 1]), 5)]

@@ -342,6 +342,13 @@ constexpr int kF2Lds = kF2Mid + 8 * kF2MidPlane;               // 161280 B
 
 __device__ __forceinline__ int f2_slot(int row) { return (row + 1 + 18 * 64) % kF2Ring; }   // row >= -1 - 18*64
 
+#if defined(F2_STAMPS) && !defined(F2_STREAM_KERNEL)
+#define F2_STREAM_KERNEL
+#endif
+#ifdef F2_STREAM_KERNEL
+// ---- A/B and diagnostic builds only (tools/build_ab.sh -DF2_STREAM_KERNEL): the one-wave-
+// per-SIMD form of the same schedule, one software-pipelined MFMA stream per wave and step
+// (2.29-2.34 ms per pair vs conv_body_f8's 2.24). ----
 #ifndef F2_PREFETCH
 #define F2_PREFETCH 2
 #endif
@@ -678,6 +685,7 @@ template __global__ void conv_body_f2_kernel<1>(const half_t* __restrict__, half
                                                 const uint4* __restrict__, const float* __restrict__,
                                                 const uint4* __restrict__, const float* __restrict__, ConvShape,
                                                 int, int, int);
+#endif  // F2_STREAM_KERNEL
 
 // ------------------------------------------------------------------------------------
 // Body layer with split weights (PNP_PREC_FP16W2): W = W_hi + W_lo, both fp16 (W_lo =
@@ -694,6 +702,289 @@ template __global__ void conv_body_f2_kernel<1>(const half_t* __restrict__, half
 // 32m..32m+31 (m = w & 1) of tile rows 4(w>>1) .. +3 (four N-tiles, 64 accumulators); per
 // K-step 4 B fragments + 1 lo A fragment, 8 MFMAs.  The epilogue stores 2 x 16 B per lane
 // and N-tile straight from registers.
+// ------------------------------------------------------------------------------------
+// conv_body_f8: the f2 schedule (two body layers per launch, strips streamed 8 rows per step,
+// chunk-planar rings, LDS-DMA halo rows) on 8 waves, two per SIMD, so each SIMD carries one
+// layer-l and one layer-l+1 wave (waves w and w+4 share a SIMD) and each hides the other's
+// fragment-read latency, epilogues and DMA issue instead of software pipelining inside one
+// wave.  Wave w: layer w >> 2, M-tile w & 1, half (w >> 1) & 1 of the step's N-tiles:
+//   layer l,   half 0: the strip-halo tile + rows 0-3 (groups {1, 2}, {halo, 0}, {3});
+//   layer l,   half 1: rows 4-7 ({4, 5}, {6, 7});
+//   layer l+1, half h: output rows 4h .. 4h+3 of the step ({0, 1}, {2, 3} + 4h).
+// A group's epilogue follows its K-loop.  256 registers per wave (VGPR + AGPR): 144 for the
+// weights, 2 N-tiles of accumulators per group.  Same K order and roundings as conv_body_v3.
+// ------------------------------------------------------------------------------------
+template <int NT, int PLANE, class Side>
+__device__ __forceinline__ void f8_kloop(const half8_t (&wA)[kBodyKSteps], const unsigned char* ring,
+                                         const int (&ad)[NT][3], floatx16 (&acc)[NT], Side&& side) {
+  auto ldB = [&](int ks, int n) {
+    const int tap = ks >> 2, sub = ks & 3, dy = tap / 3, dx = tap - 3 * dy;
+    return *reinterpret_cast<const half8_t*>(ring + ad[n][dy] + (2 * sub * PLANE + 16 * dx));
+  };
+#ifndef F8_PREFETCH
+#define F8_PREFETCH 2
+#endif
+  constexpr int D = F8_PREFETCH;
+  half8_t fb[D + 1][NT];
+#pragma unroll
+  for (int d = 0; d < D; ++d)
+#pragma unroll
+    for (int n = 0; n < NT; ++n) fb[d][n] = ldB(d, n);
+#pragma unroll
+  for (int ks = 0; ks < kBodyKSteps; ++ks) {
+    if (ks + D < kBodyKSteps) {
+#pragma unroll
+      for (int n = 0; n < NT; ++n) fb[(ks + D) % (D + 1)][n] = ldB(ks + D, n);
+    }
+#pragma unroll
+    for (int n = 0; n < NT; ++n)
+      acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wA[ks], fb[ks % (D + 1)][n], ks == 0 ? floatx16{} : acc[n],
+                                                      0, 0, 0);
+    side(ks);
+#ifndef F8_NO_SCHED_BARRIER
+    __builtin_amdgcn_sched_barrier(0);
+#endif
+  }
+}
+
+template <int ACT>
+__global__ __launch_bounds__(512, 1) void conv_body_f8_kernel(const half_t* __restrict__ in,
+                                                               half_t* __restrict__ out,
+                                                               const uint4* __restrict__ w1,
+                                                               const float* __restrict__ b1,
+                                                               const uint4* __restrict__ w2,
+                                                               const float* __restrict__ b2, ConvShape s,
+                                                               int strips_x, int nstrips, int sb) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  unsigned char* ring = smem;
+  unsigned char* mid = smem + kF2Mid;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int layer = wave >> 2, m = wave & 1, half = (wave >> 1) & 1;
+  const int h = lane >> 5, col = lane & 31;
+  const uint4* wsrc = layer ? w2 : w1;
+  half8_t wA[kBodyKSteps];
+#pragma unroll
+  for (int ks = 0; ks < kBodyKSteps; ++ks)
+    wA[ks] = *reinterpret_cast<const half8_t*>(reinterpret_cast<const unsigned char*>(wsrc) +
+                                               ((ks * 2 + m) * 64 + lane) * 16);
+  float bl[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) bl[r] = (layer ? b2 : b1)[32 * m + 16 * h + r];
+  const unsigned img_bytes = (unsigned)(s.Hp * s.Wp) * 128u;
+
+  const int S = 8 * sb;
+  const int K = (nstrips - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
+  auto geom = [&](int k) {
+    const int st = min(blockIdx.x + k * gridDim.x, (unsigned)nstrips - 1);
+    const int b = st / strips_x;
+    return SGeom{b, (st - b * strips_x) * kTileW};
+  };
+  int kJ = 0, jb = 0;
+  int gpb, gpx, gcb, gcx, gnb, gnx;
+  {
+    const SGeom g0 = geom(0), g1 = geom(1);
+    gpb = gcb = g0.b;
+    gpx = gcx = g0.x0;
+    gnb = g1.b;
+    gnx = g1.x0;
+  }
+  auto pick = [&](int k) {
+    const int pb = gpb, px = gpx, cb = gcb, cx = gcx, nb = gnb, nx = gnx;
+    return SGeom{k > kJ ? nb : (k < kJ ? pb : cb), k > kJ ? nx : (k < kJ ? px : cx)};
+  };
+  auto locate = [&](int R, int kJ, int& k, int& r) {
+    k = kJ;
+    r = R - kJ * S;
+    if (r < 0) { --k; r += S; } else if (r >= S) { ++k; r -= S; }
+  };
+  __amdgpu_buffer_rsrc_t dsrc;
+  unsigned dvo;
+  unsigned char* ddst;
+  auto dma_at = [&](int R, int kJ) {
+    int k, r;
+    locate(R, kJ, k, r);
+    const bool valid = R >= 0 && k < K;
+    const SGeom G = pick(k);
+    dsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(in + (size_t)G.b * s.Hp * s.Wp * kWidth), (short)0,
+                                             valid ? (int)img_bytes : 0, 0x00020000);
+    dvo = (unsigned)(((r + s.pad) * s.Wp + G.x0 + lane) * 128);
+    ddst = ring + f2_slot(R) * (kF2InW * 16);
+  };
+  auto dma_plane = [&](int c) {
+    if (lane < kF2InW)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(dsrc, (__attribute__((address_space(3))) void*)(ddst + c * kF2InPlane),
+                                               16, dvo + 16 * c, 0, 0, 0);
+  };
+  for (int r = wave; r < 10; r += 8) {
+    dma_at(r - 1, 0);
+#pragma unroll 1
+    for (int c = 0; c < 8; ++c) dma_plane(c);
+  }
+  for (int q = tid; q < 8 * kF2MidW; q += 512) {
+    const int c = q / kF2MidW, p = q - c * kF2MidW;
+    *reinterpret_cast<v4i_t*>(mid + c * kF2MidPlane + p * 16) = v4i_t{0, 0, 0, 0};
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  for (int J = 0; J <= K * sb; ++J) {
+    // this wave's DMA row of the next step: input row 8J+9+wave, one piece per chunk plane,
+    // issued during the wave's first group
+#ifdef F8_DMA_SKEW
+    // 64 pieces (row, plane): waves on the SIMDs with 8 N-tiles per step (w & 2) take 12,
+    // the others (9 N-tiles) 4
+    const int pcnt = (wave & 2) ? 12 : 4;
+    const int pbeg = (wave & 2) ? 16 + 12 * ((wave & 1) + 2 * (wave >> 2)) : 4 * ((wave & 1) + 2 * (wave >> 2));
+    auto side = [&](int ks) {
+      if ((ks % 3) == 1 && ks / 3 < pcnt) {
+        const int id = pbeg + ks / 3;
+        if (ks / 3 == 0 || (id & 7) == 0) dma_at(8 * J + 9 + (id >> 3), kJ);
+        dma_plane(id & 7);
+      }
+    };
+#else
+    auto side = [&](int ks) {
+      if (ks == 1) dma_at(8 * J + 9 + wave, kJ);
+      if ((ks & 3) == 1 && (ks >> 2) < 8) dma_plane(ks >> 2);
+    };
+#endif
+    auto noside = [](int) {};
+    if (layer == 0) {
+      const int x0 = gcx;
+      if (J < K * sb && 8 * jb < s.H) {
+        int sl = f2_slot(8 * J - 1);
+        int rowoff[10];
+#pragma unroll
+        for (int q = 0; q < 10; ++q) {
+          rowoff[q] = sl * (kF2InW * 16);
+          sl = sl == kF2Ring - 1 ? 0 : sl + 1;
+        }
+        const int hr = (col & 15) >> 1, hc = (col & 1) ? kF2MidW - 1 : 0;
+        // N-tile k: row tile k < 8 (columns 1..32) or the halo tile (k == 8)
+        auto group = [&](auto ntc, int k0, int k1, bool first) {
+          constexpr int NT = decltype(ntc)::value;
+          int ad[NT][3], prow[NT], pcol[NT];
+#pragma unroll
+          for (int n = 0; n < NT; ++n) {
+            const int k = n == 0 ? k0 : k1;
+            prow[n] = k < 8 ? k : hr;
+            pcol[n] = k < 8 ? 1 + col : hc;
+#pragma unroll
+            for (int dy = 0; dy < 3; ++dy) {
+              int ro = rowoff[0];
+#pragma unroll
+              for (int q = 1; q < 10; ++q) ro = prow[n] + dy == q ? rowoff[q] : ro;
+              ad[n][dy] = h * kF2InPlane + ro + pcol[n] * 16;
+            }
+          }
+          floatx16 acc[NT];
+          if (first) f8_kloop<NT, kF2InPlane>(wA, ring, ad, acc, side);
+          else f8_kloop<NT, kF2InPlane>(wA, ring, ad, acc, noside);
+#pragma unroll
+          for (int n = 0; n < NT; ++n) {
+            const int k = n == 0 ? k0 : k1;
+            if (k == 8 && col >= 16) continue;
+            const int pc = pcol[n], pr = prow[n], x = x0 - 1 + pc;
+            const bool inside = 8 * jb + pr < s.H && x >= 0 && x < s.W;
+            half8_t v0 = bias_act8<ACT>(acc[n], 0, bl), v1 = bias_act8<ACT>(acc[n], 8, bl + 8);
+            if (!inside) { v0 = half8_t{}; v1 = half8_t{}; }   // the next layer's zero padding
+            unsigned char* d = mid + (4 * m + 2 * h) * kF2MidPlane + (f2_slot(8 * J + pr) * kF2MidW + pc) * 16;
+            *reinterpret_cast<half8_t*>(d) = v0;
+            *reinterpret_cast<half8_t*>(d + kF2MidPlane) = v1;
+          }
+        };
+        using I1 = std::integral_constant<int, 1>;
+        using I2 = std::integral_constant<int, 2>;
+        if (half == 0) {                                 // (the halo group after the DMA has landed)
+          group(I2{}, 1, 2, true);
+          group(I2{}, 8, 0, false);
+          group(I1{}, 3, 3, false);
+        } else {
+          group(I2{}, 4, 5, true);
+          group(I2{}, 6, 7, false);
+        }
+      } else {
+        // a block below the image (or past the last strip): zero rows 4 half .. 4 half + 3, no MFMAs
+#pragma unroll 1
+        for (int ks = 0; ks < kBodyKSteps; ++ks) side(ks);
+        for (int q = lane; q < 4 * kF2MidW * 4; q += 64) {
+          const int c = q / (4 * kF2MidW), p = q - c * (4 * kF2MidW), rr = p / kF2MidW, pc = p - rr * kF2MidW;
+          *reinterpret_cast<v4i_t*>(mid + (4 * m + c) * kF2MidPlane +
+                                    (f2_slot(8 * J + 4 * half + rr) * kF2MidW + pc) * 16) = v4i_t{0, 0, 0, 0};
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMAs have landed
+    } else {
+      if (J > 0) {
+        // output rows 8J-9 + 4 half + t, t = 0..3, in two groups of two
+        int sl = f2_slot(8 * J - 10 + 4 * half);
+        int rowoff[6];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) {
+          rowoff[q] = sl * (kF2MidW * 16);
+          sl = sl == kF2Ring - 1 ? 0 : sl + 1;
+        }
+        const int lb = h * kF2MidPlane + col * 16;
+        auto group = [&](int t0, bool first) {
+          int ad[2][3];
+#pragma unroll
+          for (int n = 0; n < 2; ++n)
+#pragma unroll
+            for (int dy = 0; dy < 3; ++dy) ad[n][dy] = lb + rowoff[t0 + n + dy];
+          floatx16 acc[2];
+          if (first) f8_kloop<2, kF2MidPlane>(wA, mid, ad, acc, side);
+          else f8_kloop<2, kF2MidPlane>(wA, mid, ad, acc, noside);
+#pragma unroll
+          for (int n = 0; n < 2; ++n) {
+            const int R = 8 * J - 9 + 4 * half + t0 + n;
+            int k, r;
+            locate(R, kJ, k, r);
+            const bool ok = R >= 0 && k < K && r < s.H;
+            const SGeom G = pick(k);
+            half_t* row = out + (((size_t)G.b * s.Hp + r + s.pad) * s.Wp + G.x0 + s.pad) * kWidth;
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                ok ? (void*)row : (void*)out, (short)0, ok ? min(kTileW, s.W - G.x0) * 128 : 0, 0x00020000);
+            const half8_t v0 = bias_act8<ACT>(acc[n], 0, bl), v1 = bias_act8<ACT>(acc[n], 8, bl + 8);
+            const unsigned off = (unsigned)(col * 128 + 64 * m + 32 * h);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i_t, v0), rs, off, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i_t, v1), rs, off + 16, 0, 0);
+          }
+        };
+        group(0, true);
+        group(2, false);
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // the DMAs (older than the 8 stores) landed
+      } else {
+#pragma unroll 1
+        for (int ks = 0; ks < kBodyKSteps; ++ks) side(ks);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    }
+    __syncthreads();
+    if (++jb == sb) {
+      jb = 0;
+      ++kJ;
+      gpb = gcb;
+      gpx = gcx;
+      gcb = gnb;
+      gcx = gnx;
+      const SGeom g = geom(kJ + 1);
+      gnb = g.b;
+      gnx = g.x0;
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template __global__ void conv_body_f8_kernel<0>(const half_t* __restrict__, half_t* __restrict__,
+                                                const uint4* __restrict__, const float* __restrict__,
+                                                const uint4* __restrict__, const float* __restrict__, ConvShape,
+                                                int, int, int);
+template __global__ void conv_body_f8_kernel<1>(const half_t* __restrict__, half_t* __restrict__,
+                                                const uint4* __restrict__, const float* __restrict__,
+                                                const uint4* __restrict__, const float* __restrict__, ConvShape,
+                                                int, int, int);
+
 // ------------------------------------------------------------------------------------
 constexpr int kW2Halo = 44 * 1024;
 constexpr int kW2Lo = 2 * kW2Halo;
@@ -1133,7 +1424,11 @@ hipError_t conv_kernels_init() {
     e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kV3Lds);
     if (e != hipSuccess) return e;
   }
-  for (const void* k : {(const void*)conv_body_f2_kernel<0>, (const void*)conv_body_f2_kernel<1>}) {
+  for (const void* k : {
+#ifdef F2_STREAM_KERNEL
+           (const void*)conv_body_f2_kernel<0>, (const void*)conv_body_f2_kernel<1>,
+#endif
+           (const void*)conv_body_f8_kernel<0>, (const void*)conv_body_f8_kernel<1>}) {
     e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kF2Lds);
     if (e != hipSuccess) return e;
   }
@@ -1164,12 +1459,21 @@ void launch_conv_body_f2(const half_t* in, half_t* out, const void* w1, const fl
   const int strips_x = (s.W + kTileW - 1) / kTileW, nstrips = s.B * strips_x;
   const int sb = (s.H + 1 + 7) / 8;                         // 8-row blocks per strip: S = 8 sb >= H + 1
   const int grid = nstrips < num_cus ? nstrips : num_cus;
+#ifndef F2_STREAM_KERNEL
+  if (act == 0)
+    hipLaunchKernelGGL((conv_body_f8_kernel<0>), dim3(grid), dim3(512), kF2Lds, st, in, out, (const uint4*)w1, b1,
+                       (const uint4*)w2, b2, s, strips_x, nstrips, sb);
+  else
+    hipLaunchKernelGGL((conv_body_f8_kernel<1>), dim3(grid), dim3(512), kF2Lds, st, in, out, (const uint4*)w1, b1,
+                       (const uint4*)w2, b2, s, strips_x, nstrips, sb);
+#else
   if (act == 0)
     hipLaunchKernelGGL((conv_body_f2_kernel<0>), dim3(grid), dim3(256), kF2Lds, st, in, out, (const uint4*)w1, b1,
                        (const uint4*)w2, b2, s, strips_x, nstrips, sb);
   else
     hipLaunchKernelGGL((conv_body_f2_kernel<1>), dim3(grid), dim3(256), kF2Lds, st, in, out, (const uint4*)w1, b1,
                        (const uint4*)w2, b2, s, strips_x, nstrips, sb);
+#endif
 }
 
 void launch_conv_body_w2(const half_t* in, half_t* out, const void* w, const void* w_lo, const float* bias,
