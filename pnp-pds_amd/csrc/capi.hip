@@ -53,6 +53,7 @@ struct pnp_ctx {
   bool den_ready = false;
   int prec = PNP_PREC_FP16;   // pnp_set_precision: fp16 MFMA operands (conv.hip) or fp32 (conv32.hip)
   DevBuf head_w, head_b, body_w, body_b, tail_w, tail_b;
+  DevBuf body_w16;                       // 16x16x32 MFMA fragments of the body layers (conv_body_x8)
   DevBuf head_w32, body_w32, tail_w32;   // fp32 MFMA fragments (PNP_PREC_FP32)
   DevBuf head_wlo, body_wlo, tail_wlo;   // fp16 low halves W - fp16(W) (PNP_PREC_FP16W2)
 
@@ -350,8 +351,9 @@ void run_denoiser(pnp_ctx* ctx, const half_t* u16, const float* u32, float* xout
       const float* bl = P<float>(ctx->body_b) + l * kWidth;
       if (!w2 && pair && !ctx->ablate && l + 1 < nbody) {   // layers l, l+1 in one launch
         ProfScope ps(ctx, "conv_body_f2", st);
-        launch_conv_body_f2(P<half_t>(act[cur]), P<half_t>(act[cur ^ 1]), wl, bl, wl + kBodyWBytes, bl + kWidth, s,
-                            ctx->den_act, ctx->num_cus, st);
+        const char* w16 = (const char*)ctx->body_w16.p + (size_t)l * kBodyWBytes;
+        launch_conv_body_f2(P<half_t>(act[cur]), P<half_t>(act[cur ^ 1]), w16, w16 + kBodyWBytes, wl,
+                            wl + kBodyWBytes, bl, bl + kWidth, s, ctx->den_act, ctx->num_cus, st);
         check_launch(ctx, "conv_body_f2");
         l += 2;
         cur ^= 1;
@@ -917,7 +919,7 @@ int pnp_destroy(pnp_ctx* ctx) {
                     &ctx->z, &ctx->p, &ctx->t, &ctx->dense_fwd, &ctx->dense_adj, &ctx->ssim_scr,
                     &ctx->taps64, &ctx->y1, &ctx->d, &ctx->c1, &ctx->dg_words, &ctx->dg_flag, &ctx->dg_rank, &ctx->dg_scan, &ctx->dg_noise,
                     &ctx->dg_img, &ctx->dg_draws, &ctx->dg_first, &ctx->dg_status,
-                    &ctx->head_w32, &ctx->body_w32, &ctx->tail_w32, &ctx->act32[0], &ctx->act32[1], &ctx->l1_scr, &ctx->ssim_mm, &ctx->head_wlo, &ctx->body_wlo, &ctx->tail_wlo};
+                    &ctx->head_w32, &ctx->body_w32, &ctx->tail_w32, &ctx->act32[0], &ctx->act32[1], &ctx->l1_scr, &ctx->ssim_mm, &ctx->head_wlo, &ctx->body_wlo, &ctx->tail_wlo, &ctx->body_w16};
   for (DevBuf* b : bufs) release(*b);
   graph_release(ctx);
   release(ctx->it_dev);
@@ -995,8 +997,10 @@ int pnp_set_denoiser(pnp_ctx* ctx, int channels, int depth, int width, const flo
     pack_head_weights(p, channels, hw.data());
     std::memcpy(hb.data(), p + kWidth * channels * 9, kWidth * sizeof(float));
     p += n_head;
+    std::vector<uint16_t> bw16(bw.size());
     for (int l = 0; l < depth - 2; ++l) {
       pack_body_weights(p, bw.data() + (size_t)l * kBodyWBytes / 2);
+      pack_body_weights16(p, bw16.data() + (size_t)l * kBodyWBytes / 2);
       std::memcpy(bb.data() + (size_t)l * kWidth, p + kWidth * kWidth * 9, kWidth * sizeof(float));
       p += n_body;
     }
@@ -1047,6 +1051,8 @@ int pnp_set_denoiser(pnp_ctx* ctx, int channels, int depth, int width, const flo
     HIPCHK(ctx, hipMemcpy(ctx->head_w.p, hw.data(), hw.size() * 2, hipMemcpyHostToDevice));
     HIPCHK(ctx, hipMemcpy(ctx->head_b.p, hb.data(), hb.size() * 4, hipMemcpyHostToDevice));
     HIPCHK(ctx, hipMemcpy(ctx->body_w.p, bw.data(), bw.size() * 2, hipMemcpyHostToDevice));
+    ensure(ctx, ctx->body_w16, bw16.size() * 2);
+    HIPCHK(ctx, hipMemcpy(ctx->body_w16.p, bw16.data(), bw16.size() * 2, hipMemcpyHostToDevice));
     HIPCHK(ctx, hipMemcpy(ctx->body_b.p, bb.data(), bb.size() * 4, hipMemcpyHostToDevice));
     HIPCHK(ctx, hipMemcpy(ctx->tail_w.p, tw.data(), tw.size() * 2, hipMemcpyHostToDevice));
     HIPCHK(ctx, hipMemcpy(ctx->tail_b.p, tb.data(), tb.size() * 4, hipMemcpyHostToDevice));

@@ -335,10 +335,13 @@ PNP_V3_INST(6, 0)
 constexpr int kF2Ring = 18;                                    // rows per ring
 struct SGeom { int b, x0; };
 constexpr int kF2InW = kTileW + 4, kF2MidW = kTileW + 2;       // 36, 34 pixels per ring row
-constexpr int kF2InPlane = kF2Ring * kF2InW * 16;              // 10368 B per chunk plane
-constexpr int kF2MidPlane = kF2Ring * kF2MidW * 16;            // 9792
-constexpr int kF2Mid = 8 * kF2InPlane;                         // 82944: intermediate ring offset
-constexpr int kF2Lds = kF2Mid + 8 * kF2MidPlane;               // 161280 B
+// Chunk planes padded to multiples of 256 B: the 16x16x32 B fragments (conv_body_x8) read
+// two planes per ds_read_b128 lane group, which then hit disjoint banks (unpadded: 2-way
+// conflicts on every read); the two rings then fill the LDS exactly.
+constexpr int kF2InPlane = (kF2Ring * kF2InW * 16 + 255) / 256 * 256;     // 10496 B per chunk plane
+constexpr int kF2MidPlane = (kF2Ring * kF2MidW * 16 + 255) / 256 * 256;   // 9984
+constexpr int kF2Mid = 8 * kF2InPlane;                         // 83968: intermediate ring offset
+constexpr int kF2Lds = kF2Mid + 8 * kF2MidPlane;               // 163840 B: all of it
 
 __device__ __forceinline__ int f2_slot(int row) { return (row + 1 + 18 * 64) % kF2Ring; }   // row >= -1 - 18*64
 
@@ -702,6 +705,7 @@ template __global__ void conv_body_f2_kernel<1>(const half_t* __restrict__, half
 // 32m..32m+31 (m = w & 1) of tile rows 4(w>>1) .. +3 (four N-tiles, 64 accumulators); per
 // K-step 4 B fragments + 1 lo A fragment, 8 MFMAs.  The epilogue stores 2 x 16 B per lane
 // and N-tile straight from registers.
+#ifdef F2_F8_KERNEL   // A/B builds only: the same schedule on 32x32x16 MFMAs
 // ------------------------------------------------------------------------------------
 // conv_body_f8: the f2 schedule (two body layers per launch, strips streamed 8 rows per step,
 // chunk-planar rings, LDS-DMA halo rows) on 8 waves, two per SIMD, so each SIMD carries one
@@ -981,6 +985,293 @@ template __global__ void conv_body_f8_kernel<0>(const half_t* __restrict__, half
                                                 const uint4* __restrict__, const float* __restrict__, ConvShape,
                                                 int, int, int);
 template __global__ void conv_body_f8_kernel<1>(const half_t* __restrict__, half_t* __restrict__,
+                                                const uint4* __restrict__, const float* __restrict__,
+                                                const uint4* __restrict__, const float* __restrict__, ConvShape,
+                                                int, int, int);
+#endif  // F2_F8_KERNEL
+
+// ------------------------------------------------------------------------------------
+// conv_body_x8: conv_body_f8's schedule on v_mfma_f32_16x16x32_f16 (MI355X_MICROARCH.md:
+// under the chip's power limit this shape delivers ~1.12-1.15x the FLOP/s of 32x32x16 at
+// equal cycles per FLOP).  K-step ks (18 of 32) = tap ks >> 1, channel half ks & 1; an
+// N-subtile is 16 pixels; a wave's 32-channel M-tile is two 16-row A-subtiles sharing each
+// B fragment.  A row r of subtile q is channel 8 (r >> 2) + 4 q + (r & 3) of the M-tile, so
+// lane l ends with the 8 consecutive channels of chunk 4M + (l >> 4) of pixel l & 15: one
+// 16-B store per lane and subtile.  The strip halo is exactly one N-subtile (16 pixels).
+// Weights: pack_body_weights16, [18 ks][2 M-tiles][2 subtiles][64 lanes][8 x f16].
+// ------------------------------------------------------------------------------------
+constexpr int kX8KSteps = 18;
+
+template <int NT, int PLANE, class Side>
+__device__ __forceinline__ void x8_kloop(const half8_t (&wA)[kX8KSteps][2], const unsigned char* ring,
+                                         const int (&ad)[NT][3], floatx4 (&acc)[NT][2], Side&& side) {
+  auto ldB = [&](int ks, int n) {
+    const int tap = ks >> 1, hs = ks & 1, dy = tap / 3, dx = tap - 3 * dy;
+    return *reinterpret_cast<const half8_t*>(ring + ad[n][dy] + (4 * hs * PLANE + 16 * dx));
+  };
+  constexpr int D = 2;
+  half8_t fb[D + 1][NT];
+#pragma unroll
+  for (int d = 0; d < D; ++d)
+#pragma unroll
+    for (int n = 0; n < NT; ++n) fb[d][n] = ldB(d, n);
+#pragma unroll
+  for (int ks = 0; ks < kX8KSteps; ++ks) {
+    if (ks + D < kX8KSteps) {
+#pragma unroll
+      for (int n = 0; n < NT; ++n) fb[(ks + D) % (D + 1)][n] = ldB(ks + D, n);
+    }
+#pragma unroll
+    for (int n = 0; n < NT; ++n)
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+        acc[n][q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wA[ks][q], fb[ks % (D + 1)][n],
+                                                           ks == 0 ? floatx4{} : acc[n][q], 0, 0, 0);
+    side(ks);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// bias + activation of a lane's chunk (acc[0] = channels +0..3, acc[1] = +4..7) -> 8 x fp16
+template <int ACT>
+__device__ __forceinline__ half8_t x8_bias_act(const floatx4 (&a)[2], const float* bl) {
+  half8_t o;
+#pragma unroll
+  for (int r = 0; r < 8; r += 2) {
+    f2v_t v = f2v_t{a[r >> 2][r & 3], a[r >> 2][(r & 3) + 1]} + f2v_t{bl[r], bl[r + 1]};
+    if (ACT == 0) {
+      const f2v_t t = v * 0.01f;
+      v = f2v_t{fmaxf(v.x, t.x), fmaxf(v.y, t.y)};
+    } else {
+      v = f2v_t{fmaxf(v.x, 0.f), fmaxf(v.y, 0.f)};
+    }
+    o[r] = (half_t)v.x;
+    o[r + 1] = (half_t)v.y;
+  }
+  return o;
+}
+
+template <int ACT>
+__global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __restrict__ in,
+                                                               half_t* __restrict__ out,
+                                                               const uint4* __restrict__ w1,
+                                                               const float* __restrict__ b1,
+                                                               const uint4* __restrict__ w2,
+                                                               const float* __restrict__ b2, ConvShape s,
+                                                               int strips_x, int nstrips, int sb) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  unsigned char* ring = smem;
+  unsigned char* mid = smem + kF2Mid;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int layer = wave >> 2, m = wave & 1, half = (wave >> 1) & 1;
+  const int g = lane >> 4, px = lane & 15;               // chunk-in-M-tile, pixel of an N-subtile
+  const uint4* wsrc = layer ? w2 : w1;
+  half8_t wA[kX8KSteps][2];
+#pragma unroll
+  for (int ks = 0; ks < kX8KSteps; ++ks)
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+      wA[ks][q] = *reinterpret_cast<const half8_t*>(reinterpret_cast<const unsigned char*>(wsrc) +
+                                                    (((ks * 2 + m) * 2 + q) * 64 + lane) * 16);
+  float bl[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) bl[r] = (layer ? b2 : b1)[32 * m + 8 * g + r];
+  const unsigned img_bytes = (unsigned)(s.Hp * s.Wp) * 128u;
+
+  const int S = 8 * sb;
+  const int K = (nstrips - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
+  auto geom = [&](int k) {
+    const int st = min(blockIdx.x + k * gridDim.x, (unsigned)nstrips - 1);
+    const int b = st / strips_x;
+    return SGeom{b, (st - b * strips_x) * kTileW};
+  };
+  int kJ = 0, jb = 0;
+  int gpb, gpx, gcb, gcx, gnb, gnx;
+  {
+    const SGeom g0 = geom(0), g1 = geom(1);
+    gpb = gcb = g0.b;
+    gpx = gcx = g0.x0;
+    gnb = g1.b;
+    gnx = g1.x0;
+  }
+  auto pick = [&](int k) {
+    const int pb = gpb, pxx = gpx, cb = gcb, cx = gcx, nb = gnb, nx = gnx;
+    return SGeom{k > kJ ? nb : (k < kJ ? pb : cb), k > kJ ? nx : (k < kJ ? pxx : cx)};
+  };
+  auto locate = [&](int R, int kJ, int& k, int& r) {
+    k = kJ;
+    r = R - kJ * S;
+    if (r < 0) { --k; r += S; } else if (r >= S) { ++k; r -= S; }
+  };
+  __amdgpu_buffer_rsrc_t dsrc;
+  unsigned dvo;
+  unsigned char* ddst;
+  auto dma_at = [&](int R, int kJ) {
+    int k, r;
+    locate(R, kJ, k, r);
+    const bool valid = R >= 0 && k < K;
+    const SGeom G = pick(k);
+    dsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(in + (size_t)G.b * s.Hp * s.Wp * kWidth), (short)0,
+                                             valid ? (int)img_bytes : 0, 0x00020000);
+    dvo = (unsigned)(((r + s.pad) * s.Wp + G.x0 + lane) * 128);
+    ddst = ring + f2_slot(R) * (kF2InW * 16);
+  };
+  auto dma_plane = [&](int c) {
+    if (lane < kF2InW)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(dsrc, (__attribute__((address_space(3))) void*)(ddst + c * kF2InPlane),
+                                               16, dvo + 16 * c, 0, 0, 0);
+  };
+  for (int r = wave; r < 10; r += 8) {
+    dma_at(r - 1, 0);
+#pragma unroll 1
+    for (int c = 0; c < 8; ++c) dma_plane(c);
+  }
+  for (int q = tid; q < 8 * kF2MidW; q += 512) {
+    const int c = q / kF2MidW, p = q - c * kF2MidW;
+    *reinterpret_cast<v4i_t*>(mid + c * kF2MidPlane + p * 16) = v4i_t{0, 0, 0, 0};
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  for (int J = 0; J <= K * sb; ++J) {
+    auto side = [&](int ks) {                            // this wave's DMA row of the next step
+      if (ks == 0) dma_at(8 * J + 9 + wave, kJ);
+      if ((ks & 1) == 0 && (ks >> 1) < 8) dma_plane(ks >> 1);
+    };
+    auto noside = [](int) {};
+    if (layer == 0) {
+      const int x0 = gcx;
+      if (J < K * sb && 8 * jb < s.H) {
+        int sl = f2_slot(8 * J - 1);
+        int rowoff[10];
+#pragma unroll
+        for (int q = 0; q < 10; ++q) {
+          rowoff[q] = sl * (kF2InW * 16);
+          sl = sl == kF2Ring - 1 ? 0 : sl + 1;
+        }
+        // N-subtile u < 16: row u >> 1, columns 1 + 16 (u & 1) .. +15; u == 16: the strip halo
+        // (columns 0 and 33 of the 8 rows: pixel px -> row px >> 1, column px & 1 ? 33 : 0)
+        auto group = [&](auto ntc, int u0, int u1, bool first) {
+          constexpr int NT = decltype(ntc)::value;
+          int ad[NT][3], prow[NT], pcol[NT];
+#pragma unroll
+          for (int n = 0; n < NT; ++n) {
+            const int u = n == 0 ? u0 : u1;
+            prow[n] = u < 16 ? u >> 1 : px >> 1;
+            pcol[n] = u < 16 ? 1 + 16 * (u & 1) + px : ((px & 1) ? kF2MidW - 1 : 0);
+#pragma unroll
+            for (int dy = 0; dy < 3; ++dy) {
+              int ro = rowoff[0];
+#pragma unroll
+              for (int q = 1; q < 10; ++q) ro = prow[n] + dy == q ? rowoff[q] : ro;
+              ad[n][dy] = g * kF2InPlane + ro + pcol[n] * 16;
+            }
+          }
+          floatx4 acc[NT][2];
+          if (first) x8_kloop<NT, kF2InPlane>(wA, ring, ad, acc, side);
+          else x8_kloop<NT, kF2InPlane>(wA, ring, ad, acc, noside);
+#pragma unroll
+          for (int n = 0; n < NT; ++n) {
+            const int x = x0 - 1 + pcol[n];
+            const bool inside = 8 * jb + prow[n] < s.H && x >= 0 && x < s.W;
+            half8_t v = x8_bias_act<ACT>(acc[n], bl);
+            if (!inside) v = half8_t{};                   // the next layer's zero padding
+            *reinterpret_cast<half8_t*>(mid + (4 * m + g) * kF2MidPlane +
+                                        (f2_slot(8 * J + prow[n]) * kF2MidW + pcol[n]) * 16) = v;
+          }
+        };
+        using I1 = std::integral_constant<int, 1>;
+        using I2 = std::integral_constant<int, 2>;
+        if (half == 0) {                                 // rows 0-3 + the halo: 9 N-subtiles
+          group(I2{}, 0, 1, true);
+          group(I2{}, 2, 3, false);
+          group(I2{}, 4, 5, false);
+          group(I2{}, 6, 7, false);
+          group(I1{}, 16, 16, false);
+        } else {                                         // rows 4-7: 8
+          group(I2{}, 8, 9, true);
+          group(I2{}, 10, 11, false);
+          group(I2{}, 12, 13, false);
+          group(I2{}, 14, 15, false);
+        }
+      } else {
+#pragma unroll 1
+        for (int ks = 0; ks < kX8KSteps; ++ks) side(ks);
+        for (int q = lane; q < 4 * kF2MidW * 4; q += 64) {
+          const int c = q / (4 * kF2MidW), p = q - c * (4 * kF2MidW), rr = p / kF2MidW, pc = p - rr * kF2MidW;
+          *reinterpret_cast<v4i_t*>(mid + (4 * m + c) * kF2MidPlane +
+                                    (f2_slot(8 * J + 4 * half + rr) * kF2MidW + pc) * 16) = v4i_t{0, 0, 0, 0};
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      if (J > 0) {
+        // output rows 8J-9 + 4 half + t, t = 0..3: N-subtiles (t, column half), two per group
+        int sl = f2_slot(8 * J - 10 + 4 * half);
+        int rowoff[6];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) {
+          rowoff[q] = sl * (kF2MidW * 16);
+          sl = sl == kF2Ring - 1 ? 0 : sl + 1;
+        }
+        const int lb = g * kF2MidPlane + px * 16;
+        auto group = [&](int t, bool first) {
+          int ad[2][3];
+#pragma unroll
+          for (int n = 0; n < 2; ++n)
+#pragma unroll
+            for (int dy = 0; dy < 3; ++dy) ad[n][dy] = lb + rowoff[t + dy] + 16 * 16 * n;
+          floatx4 acc[2][2];
+          if (first) x8_kloop<2, kF2MidPlane>(wA, mid, ad, acc, side);
+          else x8_kloop<2, kF2MidPlane>(wA, mid, ad, acc, noside);
+          const int R = 8 * J - 9 + 4 * half + t;
+          int k, r;
+          locate(R, kJ, k, r);
+          const bool ok = R >= 0 && k < K && r < s.H;
+          const SGeom G = pick(k);
+          half_t* row = out + (((size_t)G.b * s.Hp + r + s.pad) * s.Wp + G.x0 + s.pad) * kWidth;
+          const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+              ok ? (void*)row : (void*)out, (short)0, ok ? min(kTileW, s.W - G.x0) * 128 : 0, 0x00020000);
+#pragma unroll
+          for (int n = 0; n < 2; ++n) {
+            const half8_t v = x8_bias_act<ACT>(acc[n], bl);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i_t, v), rs,
+                                                   (unsigned)((16 * n + px) * 128 + 64 * m + 16 * g), 0, 0);
+          }
+        };
+        group(0, true);
+        group(1, false);
+        group(2, false);
+        group(3, false);
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // the DMAs (older than the 8 stores) landed
+      } else {
+#pragma unroll 1
+        for (int ks = 0; ks < kX8KSteps; ++ks) side(ks);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    }
+    __syncthreads();
+    if (++jb == sb) {
+      jb = 0;
+      ++kJ;
+      gpb = gcb;
+      gpx = gcx;
+      gcb = gnb;
+      gcx = gnx;
+      const SGeom gg = geom(kJ + 1);
+      gnb = gg.b;
+      gnx = gg.x0;
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template __global__ void conv_body_x8_kernel<0>(const half_t* __restrict__, half_t* __restrict__,
+                                                const uint4* __restrict__, const float* __restrict__,
+                                                const uint4* __restrict__, const float* __restrict__, ConvShape,
+                                                int, int, int);
+template __global__ void conv_body_x8_kernel<1>(const half_t* __restrict__, half_t* __restrict__,
                                                 const uint4* __restrict__, const float* __restrict__,
                                                 const uint4* __restrict__, const float* __restrict__, ConvShape,
                                                 int, int, int);
@@ -1367,6 +1658,25 @@ void pack_body_weights(const float* W, uint16_t* out) {
   }
 }
 
+// W: [64][64][3][3].  out: [18 k-steps][2 M-tiles][2 subtiles][64 lanes][8] fp16 bits for
+// v_mfma_f32_16x16x32_f16: lane l holds A[row l & 15][k = 8 (l >> 4) .. +7]; row r of
+// subtile q is channel 32 M + 8 (r >> 2) + 4 q + (r & 3); k-step ks = tap ks >> 1, input
+// channels 32 (ks & 1) + k.
+void pack_body_weights16(const float* W, uint16_t* out) {
+  for (int ks = 0; ks < kX8KSteps; ++ks) {
+    const int tap = ks >> 1, hs = ks & 1, ky = tap / 3, kx = tap % 3;
+    for (int M = 0; M < 2; ++M)
+      for (int q = 0; q < 2; ++q)
+        for (int l = 0; l < 64; ++l)
+          for (int j = 0; j < 8; ++j) {
+            const int r = l & 15;
+            const int co = 32 * M + 8 * (r >> 2) + 4 * q + (r & 3);
+            const int ci = 32 * hs + 8 * (l >> 4) + j;
+            out[(((ks * 2 + M) * 2 + q) * 64 + l) * 8 + j] = f32_to_f16_bits(W[((co * 64 + ci) * 3 + ky) * 3 + kx]);
+          }
+  }
+}
+
 // W: [64][C][3][3].  k = 4*tap + ch, 3 k-steps of 16.
 void pack_head_weights(const float* W, int C, uint16_t* out) {
   for (int ks = 0; ks < kHeadKSteps; ++ks)
@@ -1428,7 +1738,10 @@ hipError_t conv_kernels_init() {
 #ifdef F2_STREAM_KERNEL
            (const void*)conv_body_f2_kernel<0>, (const void*)conv_body_f2_kernel<1>,
 #endif
-           (const void*)conv_body_f8_kernel<0>, (const void*)conv_body_f8_kernel<1>}) {
+#ifdef F2_F8_KERNEL
+           (const void*)conv_body_f8_kernel<0>, (const void*)conv_body_f8_kernel<1>,
+#endif
+           (const void*)conv_body_x8_kernel<0>, (const void*)conv_body_x8_kernel<1>}) {
     e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kF2Lds);
     if (e != hipSuccess) return e;
   }
@@ -1454,26 +1767,30 @@ void launch_conv_head(const half_t* in4, half_t* out, const void* w, const void*
                        (const uint4*)nullptr, bias, s, act);
 }
 
-void launch_conv_body_f2(const half_t* in, half_t* out, const void* w1, const float* b1, const void* w2,
-                         const float* b2, const ConvShape& s, int act, int num_cus, hipStream_t st) {
+// Two body layers per launch: conv_body_x8 (16x16x32 MFMAs, w16_*: pack_body_weights16);
+// A/B builds: -DF2_F8_KERNEL (conv_body_f8, 32x32x16, w32_*) or -DF2_STREAM_KERNEL
+// (conv_body_f2_kernel, one wave per SIMD).
+void launch_conv_body_f2(const half_t* in, half_t* out, const void* w16_1, const void* w16_2, const void* w32_1,
+                         const void* w32_2, const float* b1, const float* b2, const ConvShape& s, int act,
+                         int num_cus, hipStream_t st) {
   const int strips_x = (s.W + kTileW - 1) / kTileW, nstrips = s.B * strips_x;
   const int sb = (s.H + 1 + 7) / 8;                         // 8-row blocks per strip: S = 8 sb >= H + 1
   const int grid = nstrips < num_cus ? nstrips : num_cus;
-#ifndef F2_STREAM_KERNEL
-  if (act == 0)
-    hipLaunchKernelGGL((conv_body_f8_kernel<0>), dim3(grid), dim3(512), kF2Lds, st, in, out, (const uint4*)w1, b1,
-                       (const uint4*)w2, b2, s, strips_x, nstrips, sb);
-  else
-    hipLaunchKernelGGL((conv_body_f8_kernel<1>), dim3(grid), dim3(512), kF2Lds, st, in, out, (const uint4*)w1, b1,
-                       (const uint4*)w2, b2, s, strips_x, nstrips, sb);
+#define F2_LAUNCH(KERN, NT, W1, W2)                                                                              \
+  hipLaunchKernelGGL((KERN), dim3(grid), dim3(NT), kF2Lds, st, in, out, (const uint4*)(W1), b1, (const uint4*)(W2), \
+                     b2, s, strips_x, nstrips, sb)
+#if defined(F2_STREAM_KERNEL)
+  if (act == 0) F2_LAUNCH(conv_body_f2_kernel<0>, 256, w32_1, w32_2);
+  else F2_LAUNCH(conv_body_f2_kernel<1>, 256, w32_1, w32_2);
+#elif defined(F2_F8_KERNEL)
+  if (act == 0) F2_LAUNCH(conv_body_f8_kernel<0>, 512, w32_1, w32_2);
+  else F2_LAUNCH(conv_body_f8_kernel<1>, 512, w32_1, w32_2);
 #else
-  if (act == 0)
-    hipLaunchKernelGGL((conv_body_f2_kernel<0>), dim3(grid), dim3(256), kF2Lds, st, in, out, (const uint4*)w1, b1,
-                       (const uint4*)w2, b2, s, strips_x, nstrips, sb);
-  else
-    hipLaunchKernelGGL((conv_body_f2_kernel<1>), dim3(grid), dim3(256), kF2Lds, st, in, out, (const uint4*)w1, b1,
-                       (const uint4*)w2, b2, s, strips_x, nstrips, sb);
+  if (act == 0) F2_LAUNCH(conv_body_x8_kernel<0>, 512, w16_1, w16_2);
+  else F2_LAUNCH(conv_body_x8_kernel<1>, 512, w16_1, w16_2);
 #endif
+#undef F2_LAUNCH
+  (void)w16_1; (void)w16_2; (void)w32_1; (void)w32_2;
 }
 
 void launch_conv_body_w2(const half_t* in, half_t* out, const void* w, const void* w_lo, const float* bias,

@@ -16,6 +16,7 @@ struct ConvShape {
 ConvShape make_conv_shape(int B, int H, int W);
 hipError_t conv_kernels_init();
 void pack_body_weights(const float* W, uint16_t* out);
+void pack_body_weights16(const float* W, uint16_t* out);   // v_mfma_f32_16x16x32_f16 fragments (conv_body_x8)
 void pack_head_weights(const float* W, int C, uint16_t* out);
 void pack_tail_weights(const float* W, int C, uint16_t* out);
 // w_lo (nullable): the split weights' low halves (PNP_PREC_FP16W2), packed like w
@@ -31,8 +32,9 @@ void launch_conv_tail(const half_t* in, const float* xin, float* xout, const voi
                       const float* bias, const ConvShape& s, int C, int residual_sign, int clamp_out, int num_cus,
                       hipStream_t st);
 // two 64 -> 64 layers in one launch, streamed down 32-pixel column strips (needs pad >= 2)
-void launch_conv_body_f2(const half_t* in, half_t* out, const void* w1, const float* b1, const void* w2,
-                         const float* b2, const ConvShape& s, int act, int num_cus, hipStream_t st);
+void launch_conv_body_f2(const half_t* in, half_t* out, const void* w16_1, const void* w16_2, const void* w32_1,
+                         const void* w32_2, const float* b1, const float* b2, const ConvShape& s, int act,
+                         int num_cus, hipStream_t st);
 // one 64 -> 64 layer with split weights W_hi + W_lo (PNP_PREC_FP16W2)
 void launch_conv_body_w2(const half_t* in, half_t* out, const void* w, const void* w_lo, const float* bias,
                          const ConvShape& s, int act, int num_cus, hipStream_t st);
