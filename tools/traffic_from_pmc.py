@@ -22,7 +22,7 @@ WIDE_READ = ("conv_body_f2", "conv_body", "conv_head", "conv_tail")
 
 def short(name):
     n = re.sub(r"\(.*", "", name)
-    if "conv_body_f8" in n or "conv_body_f2" in n:   # the two-layer launch (bench scope "conv_body_f2")
+    if any(k in n for k in ("conv_body_x8", "conv_body_f8", "conv_body_f2")):   # the two-layer launch (bench scope "conv_body_f2")
         return "conv_body_f2"
     for k in ("conv_body_f2", "conv_body", "conv_head", "conv_tail", "k1", "k2", "k3_l2_dual", "l1_", "ssim"):
         if k in n:
