@@ -150,18 +150,17 @@ def measured_traffic(kernel, cfg_name, B):
 def prox_bytes(method, B, C, H, W):
     """Algorithmic HBM bytes per launch of the fused passes (fp32 state)."""
     n = B * C * H * W
-    npx = B * H * W
     if method == "A-Proposed":
-        return {"k1_primal_pre": 4 * n * 3 + 8 * npx,      # read x, y; write u32; write u16 (8 B/pixel)
+        return {"k1_primal_pre": 4 * n * 3,                # read x, y; write u32 (the denoiser head reads it)
                 "k2_dual": 4 * n * 6,                      # read x+, x, y, xobs, xtrue; write v
                 "k3_dual": 4 * n * 3}                      # read v, xobs; write y
     if method == "B-Proposed":
-        return {"k1_primal_pre": 4 * n * 5 + 8 * npx,      # read x, y, s; write u32, w; write u16
+        return {"k1_primal_pre": 4 * n * 5,                # read x, y, s; write u32, w
                 "l1_select": 4 * n * 3,                    # 3 radix-level histogram passes over w
                 "k2_dual": 4 * n * 9,                      # read x+, x, y, xobs, xtrue, s, w; write v, s+
                 "k3_dual": 4 * n * 3}
     if method == "C-Proposed":
-        return {"k1_primal_pre": 4 * n * 3 + 8 * npx,
+        return {"k1_primal_pre": 4 * n * 3,
                 "k2_dual": 4 * n * 6}                      # read x+, x, y, xobs, xtrue; write y+ (GKL fused)
     return {}
 

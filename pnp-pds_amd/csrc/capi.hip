@@ -68,7 +68,7 @@ struct pnp_ctx {
   bool loaded = false, has_true = false;
   pnp_params prm{};
   int cur = 0;
-  DevBuf x[2], y, s, w, xobs, xtrue, u32, u16, act[2], partials, metrics, theta;
+  DevBuf x[2], y, s, w, xobs, xtrue, u32, act[2], partials, metrics, theta;
   DevBuf z, p, t;   // comparisonB-2 and the other comparison methods
   DevBuf y1, d, c1; // TV dual [B][2C][H][W]; Poisson-ADMM d and Phi^T 1
   DevBuf ssim_scr;  // SSIM partials (record_ssim)
@@ -80,7 +80,7 @@ struct pnp_ctx {
   uint32_t dg_seed = 0;
 
   // scratch for single ops
-  DevBuf scr_u32, scr_u16, scr_act[2], scr_part, scr_theta;
+  DevBuf scr_u32, scr_act[2], scr_part, scr_theta;
   DevBuf act32[2];   // fp32 hidden activations (PNP_PREC_FP32), shared by the solver and pnp_op_denoise
   DevBuf l1_scr;     // l1-ball select histograms + per-image state (launch_l1_select)
 
@@ -230,7 +230,7 @@ void check_operator_shape(pnp_ctx* ctx, int H, int W) {
     fail(ctx, PNP_E_ARG, "bad image size");
 }
 
-// -------- denoiser forward: u16 (padded NHWC4) + u32 (NCHW) -> xout --------------------
+// -------- denoiser forward: u32 (NCHW fp32) -> xout ------------------------------------
 size_t act_bytes(int B, int H, int W, int ch, int pad) {
   // + slack: partial tiles read up to 12 rows / 36 pixels past the last image
   const size_t Wp = (size_t)W + 2 * pad;
@@ -319,8 +319,8 @@ void run_denoiser32(pnp_ctx* ctx, const float* u32, float* xout, int B, int H, i
   }
 }
 
-// Denoiser forward over B images: u16 (padded NHWC4) + u32 (NCHW, residual input) -> xout.
-void run_denoiser(pnp_ctx* ctx, const half_t* u16, const float* u32, float* xout, DevBuf (&act)[2], int B, int H,
+// Denoiser forward over B images: u32 (NCHW fp32: the head's input and the residual) -> xout.
+void run_denoiser(pnp_ctx* ctx, const float* u32, float* xout, DevBuf (&act)[2], int B, int H,
                   int W, hipStream_t st) {
   if (!ctx->den_ready) fail(ctx, PNP_E_STATE, "denoiser not set (pnp_set_denoiser)");
   if (ctx->prec == PNP_PREC_FP32) {
@@ -333,13 +333,12 @@ void run_denoiser(pnp_ctx* ctx, const half_t* u16, const float* u32, float* xout
   for (int b0 = 0; b0 < B; b0 += m) {
     const int mb = std::min(m, B - b0);
     ConvShape s = make_conv_shape(mb, H, W);
-    const half_t* in4 = u16 + (size_t)b0 * (H + 2) * (W + 2) * 4;
     const float* xin = u32 + (size_t)b0 * C * H * W;
     float* xo = xout + (size_t)b0 * C * H * W;
     const bool w2 = ctx->prec == PNP_PREC_FP16W2;
     {
       ProfScope ps(ctx, "conv_head", st);
-      launch_conv_head(in4, P<half_t>(act[0]), ctx->head_w.p, w2 ? ctx->head_wlo.p : nullptr, P<float>(ctx->head_b),
+      launch_conv_head(xin, C, P<half_t>(act[0]), ctx->head_w.p, w2 ? ctx->head_wlo.p : nullptr, P<float>(ctx->head_b),
                        s, ctx->den_act, ctx->num_cus, 4, st);
       check_launch(ctx, "conv_head");
     }
@@ -424,7 +423,7 @@ void solver_iteration(pnp_ctx* ctx) {
   const int record = p.record_metrics && (ctx->capturing || ctx->it < ctx->cap);
   {
     ProfScope ps(ctx, "k1_primal_pre", st);
-    launch_k1(od.kind, xo, P<float>(ctx->y), P<float>(ctx->s), P<float>(ctx->u32), P<half_t>(ctx->u16),
+    launch_k1(od.kind, xo, P<float>(ctx->y), P<float>(ctx->s), P<float>(ctx->u32),
               P<float>(ctx->w), od, B, C, H, W, (float)p.gamma1, ctx->den_clamp, mb, st);
     check_launch(ctx, "k1");
   }
@@ -434,7 +433,7 @@ void solver_iteration(pnp_ctx* ctx) {
     l1_select(ctx, P<float>(ctx->w), P<float>(ctx->theta), B, n, eta, st);
     check_launch(ctx, "l1_select");
   }
-  run_denoiser(ctx, P<half_t>(ctx->u16), P<float>(ctx->u32), xn, ctx->act, B, H, W, st);
+  run_denoiser(ctx, P<float>(ctx->u32), xn, ctx->act, B, H, W, st);
   int mm_chunks = 0;
   {
     ProfScope ps(ctx, "k2_dual", st);
@@ -482,11 +481,11 @@ void solver_iteration_admm(pnp_ctx* ctx) {
     {
       ProfScope ps(ctx, "admm_x_grad", st);
       launch_op_phi(od.kind, 0, xn, t, od, B * C, H, W, st, w);               // Phi x + s - z + y
-      launch_k1(od.kind, xn, t, nullptr, P<float>(ctx->u32), P<half_t>(ctx->u16), nullptr, od, B, C, H, W,
+      launch_k1(od.kind, xn, t, nullptr, P<float>(ctx->u32), nullptr, od, B, C, H, W,
                 (float)g, ctx->den_clamp, 0, st);                              // x - Phi^T(.) / g1 -> denoiser input
       check_launch(ctx, "admm_x_grad");
     }
-    run_denoiser(ctx, P<half_t>(ctx->u16), P<float>(ctx->u32), xn, ctx->act, B, H, W, st);   // admm.py:35
+    run_denoiser(ctx, P<float>(ctx->u32), xn, ctx->act, B, H, W, st);   // admm.py:35
   }
   {
     ProfScope ps(ctx, "admm_s_step", st);
@@ -542,8 +541,8 @@ void solver_iteration_cmp(pnp_ctx* ctx) {
     launch_lincomb(out, k, a, ca, b, cb, c, cc, d, cd, N, st);
   };
   auto denoise = [&](const float* in, float* out) {          // Denoiser_J.denoise / KAIR forward
-    launch_pack_input(in, P<float>(ctx->u32), P<half_t>(ctx->u16), B, C, H, W, ctx->den_clamp, st);
-    run_denoiser(ctx, P<half_t>(ctx->u16), P<float>(ctx->u32), out, ctx->act, B, H, W, st);
+    launch_pack_input(in, P<float>(ctx->u32), B, C, H, W, ctx->den_clamp, st);
+    run_denoiser(ctx, P<float>(ctx->u32), out, ctx->act, B, H, W, st);
   };
   const double eta = p.alpha_s * (double)n * p.sp_nl * 0.5;                         // proj_l1_ball, r = 1
   const double eps = std::sqrt((double)n * (1.0 - p.sp_nl)) * p.alpha_n * p.gaussian_nl;  // proj_l2_ball, r = 1
@@ -791,7 +790,6 @@ void solver_setup(pnp_ctx* ctx, int method, const pnp_params* params, int B, int
     ensure(ctx, ctx->d, fb);
     ensure(ctx, ctx->c1, fb);
   }
-  ensure_padded(ctx, ctx->u16, B, H, W, 4, 1, ctx->stream);
   ensure(ctx, ctx->partials,
          (size_t)B * std::max(partial_tiles(H, W) * C, chunk_count((size_t)C * H * W)) * 4 * sizeof(double));
   ensure(ctx, ctx->metrics, (size_t)B * std::max(ctx->cap, 1) * kMetrics * sizeof(double));
@@ -913,8 +911,8 @@ int pnp_destroy(pnp_ctx* ctx) {
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   DevBuf* bufs[] = {&ctx->head_w, &ctx->head_b, &ctx->body_w, &ctx->body_b, &ctx->tail_w, &ctx->tail_b,
                     &ctx->taps_fwd, &ctx->taps_adj, &ctx->mask, &ctx->x[0], &ctx->x[1], &ctx->y, &ctx->s,
-                    &ctx->w, &ctx->xobs, &ctx->xtrue, &ctx->u32, &ctx->u16, &ctx->act[0], &ctx->act[1],
-                    &ctx->partials, &ctx->metrics, &ctx->theta, &ctx->scr_u32, &ctx->scr_u16,
+                    &ctx->w, &ctx->xobs, &ctx->xtrue, &ctx->u32, &ctx->act[0], &ctx->act[1],
+                    &ctx->partials, &ctx->metrics, &ctx->theta, &ctx->scr_u32,
                     &ctx->scr_act[0], &ctx->scr_act[1], &ctx->scr_part, &ctx->scr_theta,
                     &ctx->z, &ctx->p, &ctx->t, &ctx->dense_fwd, &ctx->dense_adj, &ctx->ssim_scr,
                     &ctx->taps64, &ctx->y1, &ctx->d, &ctx->c1, &ctx->dg_words, &ctx->dg_flag, &ctx->dg_rank, &ctx->dg_scan, &ctx->dg_noise,
@@ -1350,10 +1348,9 @@ int pnp_op_denoise(pnp_ctx* ctx, const float* x, float* out, int B, int C, int H
     if (C != ctx->den_C) fail(ctx, PNP_E_ARG, "denoiser has %d channels, input has %d", ctx->den_C, C);
     hipStream_t st = pick_stream(ctx, stream);
     ensure(ctx, ctx->scr_u32, (size_t)B * C * H * W * sizeof(float));
-    ensure_padded(ctx, ctx->scr_u16, B, H, W, 4, 1, st);
-    launch_pack_input(x, P<float>(ctx->scr_u32), P<half_t>(ctx->scr_u16), B, C, H, W, ctx->den_clamp, st);
+    launch_pack_input(x, P<float>(ctx->scr_u32), B, C, H, W, ctx->den_clamp, st);
     check_launch(ctx, "pack_input");
-    run_denoiser(ctx, P<half_t>(ctx->scr_u16), P<float>(ctx->scr_u32), out, ctx->scr_act, B, H, W, st);
+    run_denoiser(ctx, P<float>(ctx->scr_u32), out, ctx->scr_act, B, H, W, st);
   });
 }
 

@@ -12,7 +12,7 @@
 // Hidden activations are fp16 NHWC64 images with a zero border of s.pad = 2 pixels (each
 // pixel one 128-B line).
 //
-//   conv_head      C -> 64, from the padded NHWC4 fp16 input
+//   conv_head      C -> 64, from the fp32 NCHW input u32 (fp16 conversion in the halo fill)
 //   conv_body_v3   64 -> 64, one layer per launch
 //   conv_tail      64 -> C + residual + clamp, fp32 NCHW out
 // (conv32.hip holds the fp32-operand path, PNP_PREC_FP32.)
@@ -1373,12 +1373,16 @@ template __global__ void conv_body_w2_kernel<1>(const half_t* __restrict__, half
                                                 const float* __restrict__, ConvShape);
 
 // ------------------------------------------------------------------------------------
-// Head layer C -> 64 (basic_models.py:16,27-28).  Input: padded NHWC4 fp16 (8 B/pixel).
-// K = 9 taps x 4 channels = 36, padded to 48 = 3 K-steps of 16: k = 4*tap + ch.
+// Head layer C -> 64 (basic_models.py:16,27-28).  Input: the fp32 NCHW denoiser input u32
+// (the same buffer the tail's residual reads), converted to fp16 (round to nearest even, as
+// every fp16 cast here) while the halo is written to LDS as one 8-B quad per pixel (channels
+// past C and pixels outside the image 0 = the conv's zero padding).  K = 9 taps x 4
+// channels = 36, padded to 48 = 3 K-steps of 16: k = 4*tap + ch.
 // ------------------------------------------------------------------------------------
-// W2: split weights (W_hi + W_lo, PNP_PREC_FP16W2), two MFMAs per product.
-template <bool W2>
-__global__ __launch_bounds__(256) void conv_head_kernel(const half_t* __restrict__ in4,
+// W2: split weights (W_hi + W_lo, PNP_PREC_FP16W2), two MFMAs per product.  NC = C when it
+// is a compile-time 1 or 3, 0 = runtime C <= kMaxC (channel index clamped, extra lanes 0).
+template <bool W2, int NC>
+__global__ __launch_bounds__(256) void conv_head_kernel(const float* __restrict__ in32, int Crt,
                                                          half_t* __restrict__ out,
                                                          const uint4* __restrict__ wpk,
                                                          const uint4* __restrict__ wpk_lo,
@@ -1401,19 +1405,33 @@ __global__ __launch_bounds__(256) void conv_head_kernel(const half_t* __restrict
     for (int r = 0; r < 16; ++r) bias_r[m][r] = bias[32 * m + 16 * h + r];
 
   // the next tile's halo is loaded into registers while this tile computes (2 pixels per thread)
-  const int Wp4 = s.W + 2;                    // u16: NHWC4 with a one-pixel zero border
-  uint2 pre[2];
+  constexpr int CM = NC ? NC : kMaxC;
+  const int C = NC ? NC : Crt;
+  const size_t plane = (size_t)s.H * s.W;
+  float pre[2][CM];
+  bool pin[2];
   auto load_halo = [&](int tt) {
     int pb_, pty, ptx;
     decode_tile(tt < s.tiles ? tt : s.tiles - 1, s, pb_, pty, ptx);
-    const uint2* base = reinterpret_cast<const uint2*>(in4) + ((size_t)pb_ * (s.H + 2) + pty) * Wp4 + ptx;
+    const float* base = in32 + (size_t)pb_ * C * plane;
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       const int p = tid + 256 * k;
       const int pl = p < kHaloPix ? p : kHaloPix - 1;
       const int pr = pl / kHaloW, pc = pl - pr * kHaloW;
-      pre[k] = base[(size_t)pr * Wp4 + pc];
+      const int gy = pty - 1 + pr, gx = ptx - 1 + pc;
+      pin[k] = gy >= 0 && gy < s.H && gx >= 0 && gx < s.W;
+      const size_t o = pin[k] ? (size_t)gy * s.W + gx : 0;
+#pragma unroll
+      for (int c = 0; c < CM; ++c) pre[k][c] = base[(size_t)(NC ? c : min(c, C - 1)) * plane + o];
     }
+  };
+  auto quad = [&](int k) {
+    _Float16 h[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) h[c] = (c < CM && (NC || c < C) && pin[k]) ? (_Float16)pre[k][c < CM ? c : 0] : (_Float16)0;
+    return make_uint2((uint32_t)__builtin_bit_cast(uint16_t, h[0]) | ((uint32_t)__builtin_bit_cast(uint16_t, h[1]) << 16),
+                      (uint32_t)__builtin_bit_cast(uint16_t, h[2]) | ((uint32_t)__builtin_bit_cast(uint16_t, h[3]) << 16));
   };
   if (blockIdx.x < s.tiles) load_halo(blockIdx.x);
   for (int t = blockIdx.x; t < s.tiles; t += gridDim.x) {
@@ -1422,7 +1440,7 @@ __global__ __launch_bounds__(256) void conv_head_kernel(const half_t* __restrict
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < 2; ++k)
-      if (tid + 256 * k < kHaloPix) hl[tid + 256 * k] = pre[k];
+      if (tid + 256 * k < kHaloPix) hl[tid + 256 * k] = quad(k);
     __syncthreads();
     load_halo(t + gridDim.x);
     floatx16 acc00 = {}, acc01 = {}, acc10 = {}, acc11 = {};
@@ -1756,15 +1774,18 @@ hipError_t conv_kernels_init() {
   return hipSuccess;
 }
 
-void launch_conv_head(const half_t* in4, half_t* out, const void* w, const void* w_lo, const float* bias,
+void launch_conv_head(const float* in32, int C, half_t* out, const void* w, const void* w_lo, const float* bias,
                       const ConvShape& s, int act, int num_cus, int blocks_per_cu, hipStream_t st) {
   const int grid = s.tiles < num_cus * blocks_per_cu ? s.tiles : num_cus * blocks_per_cu;
-  if (w_lo)
-    hipLaunchKernelGGL(conv_head_kernel<true>, dim3(grid), dim3(256), 0, st, in4, out, (const uint4*)w,
-                       (const uint4*)w_lo, bias, s, act);
-  else
-    hipLaunchKernelGGL(conv_head_kernel<false>, dim3(grid), dim3(256), 0, st, in4, out, (const uint4*)w,
-                       (const uint4*)nullptr, bias, s, act);
+#define HEAD(W2V, NCV)                                                                                        \
+  hipLaunchKernelGGL((conv_head_kernel<W2V, NCV>), dim3(grid), dim3(256), 0, st, in32, C, out, (const uint4*)w, \
+                     (const uint4*)w_lo, bias, s, act)
+  if (w_lo) {
+    if (C == 3) HEAD(true, 3); else if (C == 1) HEAD(true, 1); else HEAD(true, 0);
+  } else {
+    if (C == 3) HEAD(false, 3); else if (C == 1) HEAD(false, 1); else HEAD(false, 0);
+  }
+#undef HEAD
 }
 
 // Two body layers per launch: conv_body_x8 (16x16x32 MFMAs, w16_*: pack_body_weights16);

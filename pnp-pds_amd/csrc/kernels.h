@@ -20,7 +20,7 @@ void pack_body_weights16(const float* W, uint16_t* out);   // v_mfma_f32_16x16x3
 void pack_head_weights(const float* W, int C, uint16_t* out);
 void pack_tail_weights(const float* W, int C, uint16_t* out);
 // w_lo (nullable): the split weights' low halves (PNP_PREC_FP16W2), packed like w
-void launch_conv_head(const half_t* in4, half_t* out, const void* w, const void* w_lo, const float* bias,
+void launch_conv_head(const float* in32, int C, half_t* out, const void* w, const void* w_lo, const float* bias,
                       const ConvShape& s, int act, int num_cus, int blocks_per_cu, hipStream_t st);
 // one 64 -> 64 layer; ablate != 0 only in the PNP_PROFILING build (profiling, results wrong)
 void launch_conv_body(const half_t* in, half_t* out, const void* w, const float* bias, const ConvShape& s,
@@ -71,7 +71,7 @@ int match_taps(int Rd, const uint32_t* fwd_cols, const uint32_t* adj_cols);
 // Column-major dense table W[ox + Rd][oy + Rd] -> the (Rd+1) x (2Rd+1) x 2 float2 pairs rb_stencil reads.
 void pack_tap_pairs(int Rd, const float* W, float* out);
 
-void launch_k1(int kind, const float* x, const float* y, const float* s, float* u32, half_t* u16, float* w,
+void launch_k1(int kind, const float* x, const float* y, const float* s, float* u32, float* w,
                const OpDesc& op, int B, int C, int H, int W, float gamma1, int clamp_in, int method_b,
                hipStream_t st);
 // Returns the number of per-image (min, max) partials of xn it wrote to mm ([B][chunks][2]
@@ -153,7 +153,7 @@ void launch_metrics(const float* xn, const float* xo, const float* xt, double* p
                     size_t n, int it, int cap, hipStream_t st, const int* itp = nullptr);
 // graph replays: the iteration number (metrics row) lives in device memory, advanced per iteration
 void launch_it_advance(int* itp, hipStream_t st);
-void launch_pack_input(const float* x, float* u32, half_t* u16, int B, int C, int H, int W, int clamp_in,
+void launch_pack_input(const float* x, float* u32, int B, int C, int H, int W, int clamp_in,
                        hipStream_t st);
 
 }  // namespace pnp

@@ -2,7 +2,7 @@
 // PnP-PDS iteration (iteration.py:48-63), for gfx950.
 //
 // State arrays are fp32 B x C x H x W (NCHW).  One iteration is
-//   K1  primal_pre : u = [clamp](x - g1 * Phi^T y)            -> u32 (NCHW) + u16 (padded NHWC4)
+//   K1  primal_pre : u = [clamp](x - g1 * Phi^T y)            -> u32 (NCHW; the denoiser's input)
 //                    (B) w = s - g1 * y
 //   L1  l1_select  : (B) per-image l1-ball threshold theta       (operators.py:94-100)
 //   D   denoiser   : x+ = D(u)                                    (conv.hip)
@@ -67,8 +67,7 @@ __device__ __forceinline__ void stencil4(const float* lds, int LW, int R, const 
 template <int KIND>
 __global__ __launch_bounds__(256) void k1_primal_pre(const float* __restrict__ x, const float* __restrict__ y,
                                                       const float* __restrict__ s, float* __restrict__ u32,
-                                                      half_t* __restrict__ u16, float* __restrict__ w,
-                                                      OpDesc op, int C, int H, int W, int tiles_x,
+                                                      float* __restrict__ w, OpDesc op, int C, int H, int W, int tiles_x,
                                                       float gamma1, int clamp_in, int method_b) {
   __shared__ float lds[kLdsW * kLdsW];
   const int tile = blockIdx.x, b = blockIdx.y;
@@ -104,7 +103,6 @@ __global__ __launch_bounds__(256) void k1_primal_pre(const float* __restrict__ x
   for (int r = 0; r < 4; ++r) {
     const int i = i0 + 4 * tg + r, j = j0 + tx;
     if (i >= H || j >= W) continue;
-    half4_t h4 = {0, 0, 0, 0};
 #pragma unroll
     for (int c = 0; c < kMaxC; ++c) {
       if (c >= C) break;
@@ -112,10 +110,8 @@ __global__ __launch_bounds__(256) void k1_primal_pre(const float* __restrict__ x
       float u = x[idx] - gamma1 * g[c][r];
       if (clamp_in) u = fminf(fmaxf(u, 0.f), 1.f);
       u32[idx] = u;
-      h4[c] = (half_t)u;
       if (method_b) w[idx] = s[idx] - gamma1 * y[idx];
     }
-    *reinterpret_cast<half4_t*>(u16 + (((size_t)b * (H + 2) + i + 1) * (W + 2) + j + 1) * 4) = h4;
   }
 }
 
@@ -267,14 +263,12 @@ __device__ __forceinline__ void st4(float* __restrict__ p, float4 v, int nv) {
 }
 __device__ __forceinline__ float f4get(const float4& v, int k) { return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w; }
 
-// K1: thread = one pixel column of 4 rows (consecutive lanes on consecutive pixels, so each
-// 8-B NHWC4 store of u16 is part of one contiguous 512-B wave store).  NC = C when it is a
-// compile-time 1 or 3 (all channels' loads in flight together), 0 = runtime C <= 4.
+// K1: thread = one pixel column of 4 rows (consecutive lanes on consecutive pixels).  NC = C
+// when it is a compile-time 1 or 3 (all channels' loads in flight together), 0 = runtime C <= 4.
 template <int KIND, int NC>
 __global__ __launch_bounds__(256) void k1_elem(const float* __restrict__ x, const float* __restrict__ y,
                                                 const float* __restrict__ s, float* __restrict__ u32,
-                                                half_t* __restrict__ u16, float* __restrict__ w,
-                                                const uint8_t* __restrict__ mask, int Crt, int H, int W, int tiles_x,
+                                                float* __restrict__ w, const uint8_t* __restrict__ mask, int Crt, int H, int W, int tiles_x,
                                                 float gamma1, int clamp_in, int method_b) {
   constexpr int CM = NC ? NC : kMaxC;
   const int C = NC ? NC : Crt;
@@ -309,7 +303,6 @@ __global__ __launch_bounds__(256) void k1_elem(const float* __restrict__ x, cons
       if (r >= nr) break;
       const int i = i0 + r;
       const size_t pix = (size_t)i * W + j;
-      half4_t h4 = {0, 0, 0, 0};
 #pragma unroll
       for (int c = 0; c < CM; ++c) {
         if (c >= C) break;
@@ -318,10 +311,8 @@ __global__ __launch_bounds__(256) void k1_elem(const float* __restrict__ x, cons
         float u = xv[r][c] - gamma1 * g;
         if (clamp_in) u = fminf(fmaxf(u, 0.f), 1.f);
         u32[o] = u;
-        h4[c] = (half_t)u;
         if (MB) w[o] = sv[r][c] - gamma1 * yv[r][c];
       }
-      *reinterpret_cast<half4_t*>(u16 + (((size_t)b * (H + 2) + i + 1) * (W + 2) + j + 1) * 4) = h4;
     }
   };
   if (method_b) body(std::true_type{});
@@ -766,24 +757,13 @@ __global__ __launch_bounds__(256) void gkl_kernel(const float* __restrict__ x, c
   }
 }
 
-// Denoiser input packing for pnp_op_denoise: u32 = [clamp](x), u16 = padded NHWC4 fp16.
+// Denoiser input for pnp_op_denoise: u32 = [clamp](x) (the head converts it to fp16).
 __global__ __launch_bounds__(256) void pack_input_kernel(const float* __restrict__ x, float* __restrict__ u32,
-                                                          half_t* __restrict__ u16, int B, int C, int H, int W,
-                                                          int clamp_in) {
-  const size_t plane = (size_t)H * W;
-  const size_t total = (size_t)B * plane;
-  for (size_t p = (size_t)blockIdx.x * 256 + threadIdx.x; p < total; p += (size_t)gridDim.x * 256) {
-    const size_t b = p / plane, k = p - b * plane;
-    const int i = (int)(k / W), j = (int)(k - (size_t)i * W);
-    half4_t h4 = {0, 0, 0, 0};
-    for (int c = 0; c < C; ++c) {
-      const size_t idx = (b * C + c) * plane + k;
-      float u = x[idx];
-      if (clamp_in) u = fminf(fmaxf(u, 0.f), 1.f);
-      u32[idx] = u;
-      h4[c] = (half_t)u;
-    }
-    *reinterpret_cast<half4_t*>(u16 + ((b * (H + 2) + i + 1) * (W + 2) + j + 1) * 4) = h4;
+                                                          size_t total, int clamp_in) {
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
+    float u = x[i];
+    if (clamp_in) u = fminf(fmaxf(u, 0.f), 1.f);
+    u32[i] = u;
   }
 }
 
@@ -1031,19 +1011,18 @@ struct RbRows {
   __device__ __forceinline__ size_t ix(int r) const { return base + (size_t)(r < rows_left ? r : 0) * W; }
 };
 
-// K1: u = [clamp](x - g1 Phi^T y) -> u32 and its channel of the NHWC4 fp16 denoiser input
-// u16 (2-byte stores); B (MB): w = s - g1 y.  Block = one (plane, 64 x 64 tile).  B's y comes
+// K1: u = [clamp](x - g1 Phi^T y) -> u32 (the denoiser's input; its head converts to fp16);
+// B (MB): w = s - g1 y.  Block = one (plane, 64 x 64 tile).  B's y comes
 // from the halo in LDS (it is the stencil's input), so K1 reads y once.
 template <class T, bool MB>
 __global__ __launch_bounds__(256) void k1_blur_rb(const float* __restrict__ x, const float* __restrict__ y,
                                                    const float* __restrict__ s, float* __restrict__ u32,
-                                                   half_t* __restrict__ u16, float* __restrict__ w,
-                                                   const f2_t* __restrict__ wd_adj, int C, int H, int W, int tiles_x,
-                                                   int tiles, float gamma1, int clamp_in) {
+                                                   float* __restrict__ w, const f2_t* __restrict__ wd_adj, int H, int W,
+                                                   int tiles_x, int tiles, float gamma1, int clamp_in) {
   using G = TapGeom<T>;
   __shared__ float lds[G::N];
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
-  const int bc = blockIdx.x / tiles, b = bc / C, c = bc - b * C;
+  const int bc = blockIdx.x / tiles;                    // plane (image, channel)
   int i0, j0;
   rb_tile_origin(blockIdx.x - bc * tiles, tiles_x, i0, j0);
   const int j = j0 + 2 * tx;
@@ -1080,14 +1059,13 @@ __global__ __launch_bounds__(256) void k1_blur_rb(const float* __restrict__ x, c
     }
 #pragma unroll
     for (int k = 0; k < kRbBatch; ++k) {
-      const int r = rb + k, i = i0 + ty * kRbRows + r;
+      const int r = rb + k;
       f2_t uo, wo;
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         float uu = xv[k][q] - gamma1 * g[r][q];
         if (clamp_in) uu = fminf(fmaxf(uu, 0.f), 1.f);
         uo[q] = uu;
-        if (q < rw.nv(r)) u16[(((size_t)b * (H + 2) + i + 1) * (W + 2) + j + q + 1) * 4 + c] = (half_t)uu;
         if (MB) wo[q] = sv[k][q] - gamma1 * yc[r * G::LW + q];
       }
       const bool vec = al && rw.nv(r) == 2;
@@ -1628,23 +1606,22 @@ inline TileGrid tile_grid(int H, int W) {
 static bool rb_ok(const OpDesc& op, int C) { return op.kind == OP_BLUR && op.dense_fwd && op.Rd > 0 && C >= 1; }
 
 template <class T>
-static void launch_k1_rb(hipStream_t st, const float* x, const float* y, const float* s, float* u32, half_t* u16,
-                         float* w, const OpDesc& op, int B, int C, int H, int W, float gamma1, int clamp_in,
-                         int method_b) {
+static void launch_k1_rb(hipStream_t st, const float* x, const float* y, const float* s, float* u32, float* w,
+                         const OpDesc& op, int B, int C, int H, int W, float gamma1, int clamp_in, int method_b) {
   const int tx = (W + kRbW - 1) / kRbW, tiles = tx * ((H + kRbH - 1) / kRbH);
   if (method_b)
-    hipLaunchKernelGGL((k1_blur_rb<T, true>), dim3(B * C * tiles), dim3(256), 0, st, x, y, s, u32, u16, w,
-                       reinterpret_cast<const f2_t*>(op.dense_adj), C, H, W, tx, tiles, gamma1, clamp_in);
+    hipLaunchKernelGGL((k1_blur_rb<T, true>), dim3(B * C * tiles), dim3(256), 0, st, x, y, s, u32, w,
+                       reinterpret_cast<const f2_t*>(op.dense_adj), H, W, tx, tiles, gamma1, clamp_in);
   else
-    hipLaunchKernelGGL((k1_blur_rb<T, false>), dim3(B * C * tiles), dim3(256), 0, st, x, y, s, u32, u16, w,
-                       reinterpret_cast<const f2_t*>(op.dense_adj), C, H, W, tx, tiles, gamma1, clamp_in);
+    hipLaunchKernelGGL((k1_blur_rb<T, false>), dim3(B * C * tiles), dim3(256), 0, st, x, y, s, u32, w,
+                       reinterpret_cast<const f2_t*>(op.dense_adj), H, W, tx, tiles, gamma1, clamp_in);
 }
 
-void launch_k1(int kind, const float* x, const float* y, const float* s, float* u32, half_t* u16, float* w,
+void launch_k1(int kind, const float* x, const float* y, const float* s, float* u32, float* w,
                const OpDesc& op, int B, int C, int H, int W, float gamma1, int clamp_in, int method_b,
                hipStream_t st) {
   if (kind == OP_BLUR && rb_ok(op, C)) {
-#define K1RB(TT) launch_k1_rb<TT>(st, x, y, s, u32, u16, w, op, B, C, H, W, gamma1, clamp_in, method_b)
+#define K1RB(TT) launch_k1_rb<TT>(st, x, y, s, u32, w, op, B, C, H, W, gamma1, clamp_in, method_b)
     switch (op.taps_id) {
       case TAPS_BLUR_1: K1RB(Taps_blur_1_Adj); break;
       case TAPS_SQUARE_MINI: K1RB(Taps_square_mini_Adj); break;
@@ -1656,8 +1633,8 @@ void launch_k1(int kind, const float* x, const float* y, const float* s, float* 
   }
   const TileGrid g = tile_grid(H, W);
   dim3 grid(g.tiles, B);
-#define K1_ARGS x, y, s, u32, u16, w, op, C, H, W, g.tiles_x, gamma1, clamp_in, method_b
-#define K1E_ARGS x, y, s, u32, u16, w, op.mask, C, H, W, g.tiles_x, gamma1, clamp_in, method_b
+#define K1_ARGS x, y, s, u32, w, op, C, H, W, g.tiles_x, gamma1, clamp_in, method_b
+#define K1E_ARGS x, y, s, u32, w, op.mask, C, H, W, g.tiles_x, gamma1, clamp_in, method_b
 #define K1E(KD)                                                                              \
   if (C == 3) hipLaunchKernelGGL((k1_elem<KD, 3>), grid, dim3(256), 0, st, K1E_ARGS);        \
   else if (C == 1) hipLaunchKernelGGL((k1_elem<KD, 1>), grid, dim3(256), 0, st, K1E_ARGS);   \
@@ -1866,12 +1843,12 @@ void launch_gkl(const float* x, const float* x0, float* out, size_t count, doubl
   hipLaunchKernelGGL(gkl_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, x0, out, count, gamma, alpha);
 }
 
-void launch_pack_input(const float* x, float* u32, half_t* u16, int B, int C, int H, int W, int clamp_in,
-                       hipStream_t st) {
-  size_t blocks = ((size_t)B * H * W + 255) / 256;
+void launch_pack_input(const float* x, float* u32, int B, int C, int H, int W, int clamp_in, hipStream_t st) {
+  const size_t total = (size_t)B * C * H * W;
+  size_t blocks = (total + 255) / 256;
   if (blocks > 16384) blocks = 16384;
-  hipLaunchKernelGGL(pack_input_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, u32, u16, B, C, H, W,
-                     clamp_in);
+  if (blocks == 0) return;
+  hipLaunchKernelGGL(pack_input_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, u32, total, clamp_in);
 }
 
 }  // namespace pnp
