@@ -934,7 +934,10 @@ __device__ __forceinline__ void rb_fill_batch(float* lds, int i0, int j0, int H,
 // TPC i, so the column's wrap is resolved once and each row step is an add and one
 // conditional wrap (the element-wise gather above re-derives row and column and wraps both
 // for every element).  Loads in batches of kRbFill rows, then their LDS stores.
-template <class G, class FA>
+#ifndef PNP_RB1_FILL
+#define PNP_RB1_FILL 8       // A/B builds only
+#endif
+template <class G, int NB = PNP_RB1_FILL, class FA>
 __device__ __forceinline__ void rb_fill_cols(float* lds, int i0, int j0, int H, int W, FA&& la) {
   constexpr int TPC = 256 / G::LW;                   // threads per column (row stride)
   constexpr int NI = (G::LH + TPC - 1) / TPC;        // rows per thread (the last may be past LH)
@@ -949,10 +952,10 @@ __device__ __forceinline__ void rb_fill_cols(float* lds, int i0, int j0, int H, 
   gi += gi < 0 ? H : 0;
   gi -= gi >= H ? H : 0;
 #pragma unroll
-  for (int i0b = 0; i0b < NI; i0b += kRbFill) {
-    float a[kRbFill];
+  for (int i0b = 0; i0b < NI; i0b += NB) {
+    float a[NB];
 #pragma unroll
-    for (int i = 0; i < kRbFill; ++i) {
+    for (int i = 0; i < NB; ++i) {
       if (i0b + i < NI) {
         a[i] = la(min(max(gi, 0), H - 1) * W + gj);
         gi += TPC;
@@ -960,7 +963,7 @@ __device__ __forceinline__ void rb_fill_cols(float* lds, int i0, int j0, int H, 
       }
     }
 #pragma unroll
-    for (int i = 0; i < kRbFill; ++i) {
+    for (int i = 0; i < NB; ++i) {
       const int ly = ly0 + TPC * (i0b + i);
       if (i0b + i < NI && (G::LH % TPC == 0 || ly < G::LH)) lds[ly * G::LW + lx] = a[i];
     }
@@ -993,7 +996,11 @@ __device__ __forceinline__ void st2g(float* __restrict__ p, size_t idx, const f2
 #ifndef PNP_RB_BATCH
 #define PNP_RB_BATCH 2       // A/B builds only
 #endif
-constexpr int kRbBatch = PNP_RB_BATCH;                   // epilogue rows whose loads are in flight together (2: 0.351 ms K2, 4: 0.366, 1 per pixel before: 0.392)
+constexpr int kRbBatch = PNP_RB_BATCH;                   // K2 epilogue rows whose loads are in flight together (2: 0.351 ms K2, 4: 0.366, 1 per pixel before: 0.392)
+#ifndef PNP_RB1_BATCH
+#define PNP_RB1_BATCH 8      // A/B builds only
+#endif
+constexpr int kRb1Batch = PNP_RB1_BATCH;                 // K1: all 8 rows' loads in flight (2: 0.173 ms, 4: 0.170, 8: 0.167)
 
 // Epilogue rows of a thread: rows i0 + 8ty + r, columns j, j + 1 (nv(r) valid of 2); the
 // per-row index and count are recomputed (two registers live instead of sixteen).
@@ -1049,16 +1056,16 @@ __global__ __launch_bounds__(256) void k1_blur_rb(const float* __restrict__ x, c
 #endif
   const float* yc = lds + (ty * kRbRows + G::R) * G::LW + 2 * tx + G::R - G::kOff;   // y at (row 0, col j)
 #pragma unroll
-  for (int rb = 0; rb < kRbRows; rb += kRbBatch) {   // the loads of kRbBatch rows in flight together
-    f2_t xv[kRbBatch], sv[kRbBatch];
+  for (int rb = 0; rb < kRbRows; rb += kRb1Batch) {   // the loads of kRb1Batch rows in flight together
+    f2_t xv[kRb1Batch], sv[kRb1Batch];
 #pragma unroll
-    for (int k = 0; k < kRbBatch; ++k) {
+    for (int k = 0; k < kRb1Batch; ++k) {
       const bool vec = al && rw.nv(rb + k) == 2;
       xv[k] = ld2g(x, rw.ix(rb + k), rw.nv(rb + k), vec);
       if (MB) sv[k] = ld2g(s, rw.ix(rb + k), rw.nv(rb + k), vec);
     }
 #pragma unroll
-    for (int k = 0; k < kRbBatch; ++k) {
+    for (int k = 0; k < kRb1Batch; ++k) {
       const int r = rb + k;
       f2_t uo, wo;
 #pragma unroll
