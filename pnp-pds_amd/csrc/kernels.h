@@ -26,7 +26,7 @@ void launch_conv_head(const float* in32, int C, half_t* out, const void* w, cons
 void launch_conv_body(const half_t* in, half_t* out, const void* w, const float* bias, const ConvShape& s,
                       int act, int num_cus, int ablate, hipStream_t st);
 #ifdef PNP_PROFILING
-constexpr int kTuneAblate = 3;   // pnp_set_tuning key of the profiling build (not in include/pnppds.h)
+constexpr int kTuneAblate = 99;   // pnp_set_tuning key of the profiling build (not in include/pnppds.h)
 #endif
 void launch_conv_tail(const half_t* in, const float* xin, float* xout, const void* w, const void* w_lo,
                       const float* bias, const ConvShape& s, int C, int residual_sign, int clamp_out, int num_cus,

@@ -28,7 +28,7 @@ PRECISIONS = {"fp16": PREC_FP16, "fp32": PREC_FP32, "fp16w2": PREC_FP16W2}
 TUNE_DENOISE_CHUNK = 1
 TUNE_BODY_LAYERS = 2
 TUNE_GRAPH = 3
-TUNE_ABLATE = 3          # profiling build only (make PROFILING=1, lib_prof/): not in include/pnppds.h
+TUNE_ABLATE = 99         # profiling build only (make PROFILING=1, lib_prof/): not in include/pnppds.h
 
 
 class PnpError(RuntimeError):
