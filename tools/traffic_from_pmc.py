@@ -17,7 +17,7 @@ import csv
 import json
 import re
 
-WIDE_READ = ("conv_body_f2", "conv_body", "conv_head", "conv_tail")
+WIDE_READ = ("conv_body_f2", "conv_body", "conv_tail")   # conv_head reads fp32 u32 4 B per lane (r02)
 
 
 def short(name):
