@@ -10,7 +10,10 @@
 // border).  Head input: the fp32 NCHW u32 image K1 writes (clamped denoiser input), read
 // with bounds checks.  Tail output: x+ in fp32 NCHW, with the residual (+x / x - n) and clamp.
 //
-// One kernel template for the three layer kinds.  Tile: 8 output rows x 32 columns, all
+// conv32_kernel serves the head and the body; the tail (64 -> C, C <= 4) has its own VALU
+// kernel (conv32_tail_kernel below): on the MFMA its C rows padded to 32 wasted 29/32 of the
+// work (7.95 ms per launch at the metric, 64 % of a 64 -> 64 layer).
+// conv32_kernel tile: 8 output rows x 32 columns, all
 // output channels; 4 waves, wave w owns tile rows 2w and 2w+1 (two 32-pixel N-tiles) and
 // every 32-channel M-tile.  The 10 x 34 input halo is staged in LDS with a pixel pitch of
 // CIN + 1 floats, so the 32 lanes of a ds_read_b32 (32 consecutive pixels, one channel)
@@ -25,19 +28,20 @@ constexpr int kC32Pitch64 = kWidth + 1;   // LDS floats per halo pixel (64-chann
 constexpr int kC32Pitch4 = kMaxC + 1;     // (head: C <= 4 channels)
 constexpr int kC32Lds = kHaloPix * kC32Pitch64 * 4;   // 88400 B
 
-template <int MODE>   // 0 = head (C -> 64), 1 = body (64 -> 64), 2 = tail (64 -> C)
+template <int MODE>   // 0 = head (C -> 64), 1 = body (64 -> 64)
 struct C32Traits {
   static constexpr int CIN = MODE == 0 ? kMaxC : kWidth;
   static constexpr int PITCH = CIN + 1;
   static constexpr int CP = CIN / 2;            // MFMA K-steps per tap
-  static constexpr int NM = MODE == 2 ? 1 : 2;  // 32-channel M-tiles
+  static constexpr int NM = 2;                  // 32-channel M-tiles
   static constexpr int KS = 9 * CP;             // K-steps per layer
 };
 
+constexpr int kC32TailQ = kWidth / 4;      // tail: input channel quads
 size_t conv32_weight_floats(int mode) {
   return mode == 0 ? (size_t)C32Traits<0>::KS * C32Traits<0>::NM * 64
        : mode == 1 ? (size_t)C32Traits<1>::KS * C32Traits<1>::NM * 64
-                   : (size_t)C32Traits<2>::KS * C32Traits<2>::NM * 64;
+                   : (size_t)kC32TailQ * 9 * 4 * 4;   // tail: [quad][tap][k][c], c < 4
 }
 
 // PyTorch layout W[cout][cin][3][3] -> [ks][m][lane]: lane l holds A[row l&31][k l>>5] of
@@ -46,6 +50,16 @@ size_t conv32_weight_floats(int mode) {
 // of lane-half h = channel 16h + r) or channel i (tail: the C rows are registers 0..C-1 of
 // lane-half 0); rows and input channels past the layer's are zero.
 void pack_conv32_weights(const float* W, int mode, int cin, int cout, float* out) {
+  if (mode == 2) {   // tail (VALU): out[((q * 9 + tap) * 4 + k) * 4 + c] = W[c][4q + k][tap]
+    for (int q = 0; q < kC32TailQ; ++q)
+      for (int tap = 0; tap < 9; ++tap)
+        for (int k = 0; k < 4; ++k)
+          for (int c = 0; c < 4; ++c) {
+            const int ci = 4 * q + k;
+            out[((q * 9 + tap) * 4 + k) * 4 + c] = (c < cout && ci < cin) ? W[((size_t)c * cin + ci) * 9 + tap] : 0.f;
+          }
+    return;
+  }
   const int CP = mode == 0 ? kMaxC / 2 : kWidth / 2, NM = mode == 2 ? 1 : 2;
   for (int ks = 0; ks < 9 * CP; ++ks) {
     const int tap = ks / CP, cp = ks % CP;
@@ -76,10 +90,7 @@ __global__ __launch_bounds__(256, 1) void conv32_kernel(const float* __restrict_
 #pragma unroll
   for (int m = 0; m < T::NM; ++m)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int co = MODE == 2 ? r : 32 * m + 16 * kk + r;
-      bias_r[m][r] = (MODE == 2 ? (co < C && kk == 0) : true) ? bias[co] : 0.f;
-    }
+    for (int r = 0; r < 16; ++r) bias_r[m][r] = bias[32 * m + 16 * kk + r];
 
   for (int t = blockIdx.x; t < s.tiles; t += gridDim.x) {
     int b, ty0, tx0;
@@ -142,35 +153,105 @@ __global__ __launch_bounds__(256, 1) void conv32_kernel(const float* __restrict_
       }
     }
 
-    // epilogue: lane (col, kk), register r of M-tile m = channel 32m + 16kk + r (tail: channel r, kk = 0)
+    // epilogue: lane (col, kk), register r of M-tile m = channel 32m + 16kk + r
 #pragma unroll
     for (int n = 0; n < 2; ++n) {
       const int y = ty0 + 2 * wave + n, x = tx0 + col;
       if (y >= s.H || x >= s.W) continue;
-      if (MODE == 2) {
-        if (kk != 0) continue;
+      float* o = out + (((size_t)b * Hp + y + 1) * Wp + x + 1) * kWidth + 16 * kk;
 #pragma unroll
-        for (int c = 0; c < kMaxC; ++c) {
-          if (c >= C) break;
-          const size_t o = (((size_t)b * C + c) * s.H + y) * s.W + x;
-          const float net = acc[0][n][c] + bias_r[0][c];
-          float v = residual_sign > 0 ? net + xin[o] : xin[o] - net;
-          if (clamp_out) v = fminf(fmaxf(v, 0.f), 1.f);
-          out[o] = v;
+      for (int m = 0; m < T::NM; ++m)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          float4 v;
+          v.x = act_fn(acc[m][n][4 * q + 0] + bias_r[m][4 * q + 0], ACT);
+          v.y = act_fn(acc[m][n][4 * q + 1] + bias_r[m][4 * q + 1], ACT);
+          v.z = act_fn(acc[m][n][4 * q + 2] + bias_r[m][4 * q + 2], ACT);
+          v.w = act_fn(acc[m][n][4 * q + 3] + bias_r[m][4 * q + 3], ACT);
+          *reinterpret_cast<float4*>(o + 32 * m + 4 * q) = v;
         }
-      } else {
-        float* o = out + (((size_t)b * Hp + y + 1) * Wp + x + 1) * kWidth + 16 * kk;
+    }
+  }
+}
+
+// Tail 64 -> C (basic_models.py:18,35-36) + residual + clamp, fp32 on the VALU: thread = one
+// output pixel of an 8 x 32 tile, all C channels.  The 10 x 34 halo is staged through LDS in
+// two halves of 32 channels, as 8 planes of float4 (channels 4q .. 4q+3) per half, so the 32
+// lanes of a ds_read_b128 group read 512 contiguous bytes; 43.5 KiB per block (3 blocks per
+// CU).  Weights are wave-uniform scalar loads, [quad][tap][k][c]; channel pairs (0,1), (2,3)
+// accumulate as packed FMAs.  The sum over (channel, tap) runs in fp32 like the MFMA form,
+// in a different order.
+constexpr int kC32TailHalf = kC32TailQ / 2;
+template <int NC>
+__global__ __launch_bounds__(256) void conv32_tail_kernel(const float* __restrict__ in, float* __restrict__ out,
+                                                          const float* __restrict__ xin, const float* __restrict__ wv,
+                                                          const float* __restrict__ bias, ConvShape s, int Crt,
+                                                          int residual_sign, int clamp_out) {
+  typedef float f2v __attribute__((ext_vector_type(2)));
+  constexpr int CM = NC ? NC : kMaxC;
+  constexpr int NP = (CM + 1) / 2;           // packed channel pairs
+  const int C = NC ? NC : Crt;
+  __shared__ float4 hq[kC32TailHalf * kHaloPix];
+  const int tid = threadIdx.x, ty = tid >> 5, tx = tid & 31;
+  const int Hp = s.H + 2, Wp = s.W + 2;
+  f2v bias2[NP];
 #pragma unroll
-        for (int m = 0; m < T::NM; ++m)
+  for (int p = 0; p < NP; ++p)
+    bias2[p] = f2v{2 * p < C ? bias[2 * p] : 0.f, 2 * p + 1 < C ? bias[2 * p + 1] : 0.f};
+  for (int t = blockIdx.x; t < s.tiles; t += gridDim.x) {
+    int b, ty0, tx0;
+    {
+      const int per_img = s.tiles_x * s.tiles_y;
+      b = t / per_img;
+      const int r = t - b * per_img, tyy = r / s.tiles_x;
+      ty0 = tyy * kTileH;
+      tx0 = (r - tyy * s.tiles_x) * kTileW;
+    }
+    f2v acc[NP];
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            float4 v;
-            v.x = act_fn(acc[m][n][4 * q + 0] + bias_r[m][4 * q + 0], ACT);
-            v.y = act_fn(acc[m][n][4 * q + 1] + bias_r[m][4 * q + 1], ACT);
-            v.z = act_fn(acc[m][n][4 * q + 2] + bias_r[m][4 * q + 2], ACT);
-            v.w = act_fn(acc[m][n][4 * q + 3] + bias_r[m][4 * q + 3], ACT);
-            *reinterpret_cast<float4*>(o + 32 * m + 4 * q) = v;
-          }
+    for (int p = 0; p < NP; ++p) acc[p] = f2v{0.f, 0.f};
+    for (int h = 0; h < 2; ++h) {
+      __syncthreads();                       // the previous half's / tile's readers are done
+      for (int i = tid; i < kHaloPix * kC32TailHalf; i += 256) {
+        const int p = i >> 3, q = i & 7;
+        const int pr = p / kHaloW, pc = p - pr * kHaloW;
+        const int yp = ty0 + pr, xp = tx0 + pc;   // padded coordinates of the halo origin (ty0 - 1, tx0 - 1)
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (yp < Hp && xp < Wp)
+          v = *reinterpret_cast<const float4*>(in + (((size_t)b * Hp + yp) * Wp + xp) * kWidth + 4 * (8 * h + q));
+        hq[q * kHaloPix + p] = v;
+      }
+      __syncthreads();
+      const float4* base = hq + ty * kHaloW + tx;
+      for (int q = 0; q < kC32TailHalf; ++q) {
+        const float* wq = wv + (size_t)(8 * h + q) * 9 * 16;
+#pragma unroll 1
+        for (int dy = 0; dy < 3; ++dy)       // one tap row per pass: 48 weight SGPRs live, not 144
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx) {
+          const int tap = 3 * dy + dx;
+          const float4 v = base[q * kHaloPix + dy * kHaloW + dx];
+          const float vk[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int p = 0; p < NP; ++p) {
+              const f2v w2 = *reinterpret_cast<const f2v*>(wq + (tap * 4 + k) * 4 + 2 * p);
+              acc[p] = __builtin_elementwise_fma(w2, f2v{vk[k], vk[k]}, acc[p]);
+            }
+        }
+      }
+    }
+    const int y = ty0 + ty, x = tx0 + tx;
+    if (y < s.H && x < s.W) {
+#pragma unroll
+      for (int c = 0; c < CM; ++c) {
+        if (c >= C) break;
+        const size_t o = (((size_t)b * C + c) * s.H + y) * s.W + x;
+        const float net = acc[c >> 1][c & 1] + bias2[c >> 1][c & 1];
+        float v = residual_sign > 0 ? net + xin[o] : xin[o] - net;
+        if (clamp_out) v = fminf(fmaxf(v, 0.f), 1.f);
+        out[o] = v;
       }
     }
   }
@@ -178,8 +259,7 @@ __global__ __launch_bounds__(256, 1) void conv32_kernel(const float* __restrict_
 
 hipError_t conv32_kernels_init() {
   for (const void* k : {(const void*)conv32_kernel<0, 0>, (const void*)conv32_kernel<0, 1>,
-                        (const void*)conv32_kernel<1, 0>, (const void*)conv32_kernel<1, 1>,
-                        (const void*)conv32_kernel<2, 0>}) {
+                        (const void*)conv32_kernel<1, 0>, (const void*)conv32_kernel<1, 1>}) {
     const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kC32Lds);
     if (e != hipSuccess) return e;
   }
@@ -193,17 +273,23 @@ size_t act32_bytes(int B, int H, int W) {
 void launch_conv32(int mode, const float* in, float* out, const float* xin, const float* w, const float* bias,
                    const ConvShape& s, int C, int act, int residual_sign, int clamp_out, int num_cus,
                    hipStream_t st) {
-  const int cap = mode == 0 ? 4 * num_cus : num_cus;   // body/tail: 88 KB of LDS, one workgroup per CU
+  if (mode == 2) {                                      // tail: 43.5 KB of LDS, 3 workgroups per CU
+    const int grid = s.tiles < 3 * num_cus ? s.tiles : 3 * num_cus;
+#define C32T(NCV) hipLaunchKernelGGL((conv32_tail_kernel<NCV>), dim3(grid), dim3(256), 0, st, in, out, xin, w, bias, s, C, \
+                                     residual_sign, clamp_out)
+    if (C == 3) C32T(3); else if (C == 1) C32T(1); else C32T(0);
+#undef C32T
+    return;
+  }
+  const int cap = mode == 0 ? 4 * num_cus : num_cus;   // body: 88 KB of LDS, one workgroup per CU
   const int grid = s.tiles < cap ? s.tiles : cap;
   const size_t lds = mode == 0 ? (size_t)kHaloPix * kC32Pitch4 * 4 : (size_t)kC32Lds;
 #define C32(M, A) hipLaunchKernelGGL((conv32_kernel<M, A>), dim3(grid), dim3(256), lds, st, in, out, xin, w, bias, s, \
                                      C, residual_sign, clamp_out)
   if (mode == 0) {
     if (act == 0) C32(0, 0); else C32(0, 1);
-  } else if (mode == 1) {
-    if (act == 0) C32(1, 0); else C32(1, 1);
   } else {
-    C32(2, 0);
+    if (act == 0) C32(1, 0); else C32(1, 1);
   }
 #undef C32
 }
