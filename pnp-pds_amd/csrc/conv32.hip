@@ -92,17 +92,54 @@ __global__ __launch_bounds__(256, 1) void conv32_kernel(const float* __restrict_
 #pragma unroll
     for (int r = 0; r < 16; ++r) bias_r[m][r] = bias[32 * m + 16 * kk + r];
 
+  auto decode = [&](int t, int& b, int& ty0, int& tx0) {
+    const int per_img = s.tiles_x * s.tiles_y;
+    b = t / per_img;
+    const int r = t - b * per_img, ty = r / s.tiles_x;
+    ty0 = ty * kTileH;
+    tx0 = (r - ty * s.tiles_x) * kTileW;
+  };
+  // Body: the next tile's halo is loaded into registers during this tile's last tap (whose
+  // next-tap weight registers are free then) and written to LDS after the tile's barrier, so
+  // only the LDS writes of the fill stay exposed (one workgroup per CU: nothing else hides it).
+#ifndef C32_NO_PREFETCH
+  constexpr bool kPrefetch = MODE == 1;
+#else
+  constexpr bool kPrefetch = false;
+#endif
+  constexpr int kPre = (kHaloPix * 16 + 255) / 256;   // float4 per thread
+  float4 pre[kPrefetch ? kPre : 1];
+  auto load_pre = [&](int tt) {
+    int pb, pty, ptx;
+    decode(tt, pb, pty, ptx);
+#pragma unroll
+    for (int k = 0; k < kPre; ++k) {
+      const int i = tid + 256 * k;
+      const int p = min(i >> 4, kHaloPix - 1), q = i & 15;
+      const int pr = p / kHaloW, pc = p - pr * kHaloW;
+      const int yp = pty + pr, xp = ptx + pc;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (yp < Hp && xp < Wp) v = *reinterpret_cast<const float4*>(in + (((size_t)pb * Hp + yp) * Wp + xp) * kWidth + 4 * q);
+      pre[kPrefetch ? k : 0] = v;
+    }
+  };
+  bool have_pre = false;
+
   for (int t = blockIdx.x; t < s.tiles; t += gridDim.x) {
     int b, ty0, tx0;
-    {
-      const int per_img = s.tiles_x * s.tiles_y;
-      b = t / per_img;
-      const int r = t - b * per_img, ty = r / s.tiles_x;
-      ty0 = ty * kTileH;
-      tx0 = (r - ty * s.tiles_x) * kTileW;
-    }
+    decode(t, b, ty0, tx0);
     __syncthreads();                       // previous tile's readers are done with the halo
-    if (MODE == 0) {                       // gather C channels of the NCHW input, zero outside
+    if (kPrefetch && have_pre) {
+#pragma unroll
+      for (int k = 0; k < kPre; ++k) {
+        const int i = tid + 256 * k;
+        if (i < kHaloPix * 16) {
+          float* d = hl + (i >> 4) * T::PITCH + 4 * (i & 15);
+          const float4 v = pre[kPrefetch ? k : 0];
+          d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+        }
+      }
+    } else if (MODE == 0) {                // gather C channels of the NCHW input, zero outside
       for (int i = tid; i < kHaloPix * kMaxC; i += 256) {
         const int p = i / kMaxC, c = i - p * kMaxC;
         const int pr = p / kHaloW, pc = p - pr * kHaloW;
@@ -130,11 +167,7 @@ __global__ __launch_bounds__(256, 1) void conv32_kernel(const float* __restrict_
     float wc[T::CP * T::NM], wn[T::CP * T::NM];
 #pragma unroll
     for (int j = 0; j < T::CP * T::NM; ++j) wc[j] = wpk[j * 64 + lane];
-    for (int tap = 0; tap < 9; ++tap) {
-      if (tap + 1 < 9) {                  // next tap's A fragments, in flight during this tap
-#pragma unroll
-        for (int j = 0; j < T::CP * T::NM; ++j) wn[j] = wpk[((tap + 1) * T::CP * T::NM + j) * 64 + lane];
-      }
+    auto do_tap = [&](int tap) {
       const int dy = tap / 3, dx = tap - 3 * dy;
       const float* h0 = hl + ((2 * wave + dy) * kHaloW + col + dx) * T::PITCH + kk;
       const float* h1 = h0 + kHaloW * T::PITCH;
@@ -147,11 +180,20 @@ __global__ __launch_bounds__(256, 1) void conv32_kernel(const float* __restrict_
           acc[m][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(wc[cp * T::NM + m], b1, acc[m][1], 0, 0, 0);
         }
       }
-      if (tap + 1 < 9) {
+    };
+    for (int tap = 0; tap < 8; ++tap) {
 #pragma unroll
-        for (int j = 0; j < T::CP * T::NM; ++j) wc[j] = wn[j];
-      }
+      for (int j = 0; j < T::CP * T::NM; ++j) wn[j] = wpk[((tap + 1) * T::CP * T::NM + j) * 64 + lane];   // in flight during this tap
+      do_tap(tap);
+#pragma unroll
+      for (int j = 0; j < T::CP * T::NM; ++j) wc[j] = wn[j];
     }
+    have_pre = false;
+    if (kPrefetch && t + (int)gridDim.x < s.tiles) {
+      load_pre(t + gridDim.x);
+      have_pre = true;
+    }
+    do_tap(8);
 
     // epilogue: lane (col, kk), register r of M-tile m = channel 32m + 16kk + r
 #pragma unroll
