@@ -109,13 +109,17 @@ def synthetic_batch(B, C, H, W, seed):
 
 
 def images_per_launch(B, H, W, chunk, fp32=False):
-    """Mirror of capi.hip denoise_chunk() / run_denoiser32(): images per conv launch."""
+    """Mirror of capi.hip denoise_chunk() / split_passes(): mean images per conv launch (the
+    activation budget is an eighth of the card's HBM; the batch is split into equal passes)."""
     if chunk > 0:
-        return min(chunk, B)
-    if fp32:
-        return max(1, min(int(16e9 // (2.0 * (H + 2) * (W + 2) * 64 * 4)), B))
-    per_img = 2.0 * (H + 4) * (W + 4) * 64 * 2
-    return max(1, min(int(8e9 // per_img), B))
+        m = min(chunk, B)
+    else:
+        import torch
+        budget = torch.cuda.get_device_properties(0).total_memory / 8
+        per_img = 2.0 * (H + 2) * (W + 2) * 64 * 4 if fp32 else 2.0 * (H + 4) * (W + 4) * 64 * 2
+        m = max(1, min(int(budget // per_img), B))
+    passes = -(-B // m)
+    return B / passes
 
 
 def conv_flops_per_launch(m, H, W):

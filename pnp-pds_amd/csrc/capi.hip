@@ -41,6 +41,7 @@ struct ProfEntry {
 struct pnp_ctx {
   int device = 0;
   int num_cus = 256;
+  double act_budget = 36e9;   // denoiser activation bytes per pass: totalGlobalMem / 8
   hipStream_t stream = nullptr;
   std::string err;
   std::vector<DevBuf*> owned;
@@ -269,18 +270,28 @@ bool use_pair(pnp_ctx* ctx, int mb, int W) {
   return strips >= cus && strips * 5 >= rounds * cus * 4;
 }
 
+// Images per denoiser pass.  The two ping-pong activation buffers may take an eighth of the
+// card's HBM (36 GB of the MI355X's 288 GB: cfg5's 64 x 1024^2 shard, 17.3 GB, is one pass),
+// and a batch that needs several passes is split into equal ones: a small remainder pass
+// has fewer 32-column strips than CUs and falls back to one body layer per launch (cfg5
+// with the former 8 GB budget: passes of 29 + 29 + 6 images, the 6-image pass on one-layer
+// launches).  Per-image results do not depend on the split (test_batch_equals_single_images).
+int split_passes(int B, double per_img, double budget) {
+  const int m = std::max(1, std::min((int)std::floor(budget / per_img), B));
+  const int passes = (B + m - 1) / m;
+  return (B + passes - 1) / passes;
+}
+
 int denoise_chunk(pnp_ctx* ctx, int B, int H, int W) {
   if (ctx->den_chunk > 0) return std::min(ctx->den_chunk, B);
   const double per_img = 2.0 * (H + 2 * kActPad) * (W + 2 * kActPad) * kWidth * sizeof(half_t);
-  const int m = (int)std::floor(8e9 / per_img);
-  return std::max(1, std::min(m, B));
+  return split_passes(B, per_img, ctx->act_budget);
 }
 
 // fp32-operand forward (PNP_PREC_FP32): u32 (NCHW, clamped input) -> xout, conv32.hip.
 void run_denoiser32(pnp_ctx* ctx, const float* u32, float* xout, int B, int H, int W, hipStream_t st) {
   const double per_img = 2.0 * act32_bytes(1, H, W);
-  const int m = ctx->den_chunk > 0 ? std::min(ctx->den_chunk, B)
-                                   : std::max(1, std::min((int)std::floor(16e9 / per_img), B));
+  const int m = ctx->den_chunk > 0 ? std::min(ctx->den_chunk, B) : split_passes(B, per_img, ctx->act_budget);
   for (int i = 0; i < 2; ++i) {                 // one-pixel zero border, zeroed once per geometry
     const long long geom = ((long long)m << 40) ^ ((long long)H << 20) ^ (long long)W;
     ensure(ctx, ctx->act32[i], act32_bytes(m, H, W));
@@ -893,6 +904,7 @@ int pnp_create(int device, pnp_ctx** out) {
         fail(ctx, PNP_E_UNSUPPORTED, "device %d is %s; this library is built for gfx950 only", device,
              prop.gcnArchName);
       ctx->num_cus = prop.multiProcessorCount;
+      ctx->act_budget = (double)prop.totalGlobalMem / 8;
       HIPCHK(ctx, hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
       HIPCHK(ctx, conv_kernels_init());
       HIPCHK(ctx, conv32_kernels_init());

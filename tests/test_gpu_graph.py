@@ -68,3 +68,15 @@ def test_graph_mode_rejects_bad_values(gpu_ctx):
     from pnppds._lib import PnpError
     with pytest.raises(PnpError):
         gpu_ctx.set_graph(2)
+
+
+def test_denoise_passes_same_bits():
+    """The denoiser's images-per-pass split (auto: the HBM budget, evenly split; forced: 3 -> passes
+    of 3, 3, 1; 1) leaves every image's result unchanged: x, s and all metric rows."""
+    ctx, m, prm, x0, xo, xt = _setup("A_blur", 7)
+    ref = ctx.run(m, prm, x0, xo, xt, 4)
+    for chunk in (3, 1):
+        ctx.set_denoise_chunk(chunk)
+        got = ctx.run(m, prm, x0, xo, xt, 4)
+        for a, b in zip(ref[:5], got[:5]):
+            np.testing.assert_array_equal(a, b)
