@@ -1082,6 +1082,39 @@ __global__ __launch_bounds__(256) void k1_blur_rb(const float* __restrict__ x, c
   }
 }
 
+// Standalone Phi / Phi^T of the blur (pnp_op_phi / pnp_op_adj_phi, comparisonB-2's x-step,
+// the comparison methods): out = stencil(x) [+ add] on K1's register-blocked tiles (T: the
+// forward or the adjoint tap pattern).  Block = one (plane, 64 x 64 tile).
+template <class T, bool ADD>
+__global__ __launch_bounds__(256) void k0_blur_rb(const float* __restrict__ x, float* __restrict__ out,
+                                                   const float* __restrict__ add, const f2_t* __restrict__ wd, int H,
+                                                   int W, int tiles_x, int tiles) {
+  using G = TapGeom<T>;
+  __shared__ float lds[G::N];
+  const int tx = threadIdx.x & 31;
+  const int bc = blockIdx.x / tiles;
+  int i0, j0;
+  rb_tile_origin(blockIdx.x - bc * tiles, tiles_x, i0, j0);
+  const size_t pb = (size_t)bc * H * W;
+  const bool al = (W & 1) == 0;
+  RbRows rw;
+  rw.init(pb, i0, j0 + 2 * tx, H, W);
+  const float* xp = x + pb;
+  rb_fill_cols<G>(lds, i0, j0, H, W, [&](int k) { return xp[k]; });
+  __syncthreads();
+  f2_t g[kRbRows];
+  rb_stencil<T>(lds, wd, g);
+  if (ADD) {
+    f2_t av[kRbRows];
+#pragma unroll
+    for (int r = 0; r < kRbRows; ++r) av[r] = ld2g(add, rw.ix(r), rw.nv(r), al && rw.nv(r) == 2);
+#pragma unroll
+    for (int r = 0; r < kRbRows; ++r) g[r] += av[r];
+  }
+#pragma unroll
+  for (int r = 0; r < kRbRows; ++r) st2g(out, rw.ix(r), g[r], rw.nv(r), al && rw.nv(r) == 2);
+}
+
 // K2 halo fill of 2 xn - xo (Phi's argument) that also accumulates the metric sums of the
 // tile's own pixels from the same loads: e2 = sum (xn - xo)^2, n2 = sum xo^2 (c_n,
 // iteration.py:187) and t2 = sum (xt - xn)^2 (PSNR, :188; x_true loaded for those pixels
@@ -1610,7 +1643,11 @@ inline TileGrid tile_grid(int H, int W) {
   return g;
 }
 
-static bool rb_ok(const OpDesc& op, int C) { return op.kind == OP_BLUR && op.dense_fwd && op.Rd > 0 && C >= 1; }
+// The register-blocked kernels wrap the halo once (rb_gather): images at least Rd on a side.
+// Smaller ones (np.pad 'wrap' repeats the image) take the modulo-wrapped stencil4 kernels.
+static bool rb_ok(const OpDesc& op, int C, int H, int W) {
+  return op.kind == OP_BLUR && op.dense_fwd && op.dense_adj && op.Rd > 0 && C >= 1 && H >= op.Rd && W >= op.Rd;
+}
 
 template <class T>
 static void launch_k1_rb(hipStream_t st, const float* x, const float* y, const float* s, float* u32, float* w,
@@ -1627,7 +1664,7 @@ static void launch_k1_rb(hipStream_t st, const float* x, const float* y, const f
 void launch_k1(int kind, const float* x, const float* y, const float* s, float* u32, float* w,
                const OpDesc& op, int B, int C, int H, int W, float gamma1, int clamp_in, int method_b,
                hipStream_t st) {
-  if (kind == OP_BLUR && rb_ok(op, C)) {
+  if (kind == OP_BLUR && rb_ok(op, C, H, W)) {
 #define K1RB(TT) launch_k1_rb<TT>(st, x, y, s, u32, w, op, B, C, H, W, gamma1, clamp_in, method_b)
     switch (op.taps_id) {
       case TAPS_BLUR_1: K1RB(Taps_blur_1_Adj); break;
@@ -1702,7 +1739,7 @@ int launch_k2(int kind, int method, const float* xn, const float* xo, float* y, 
               int record, float* mm, hipStream_t st) {
   const TileGrid g = tile_grid(H, W);
   if (!record) mm = nullptr;
-  if (kind == OP_BLUR && rb_ok(op, C)) {
+  if (kind == OP_BLUR && rb_ok(op, C, H, W)) {
 #define K2RB(TT) launch_k2_rb<TT>(method, st, xn, xo, y, xobs, xtrue, s, w, theta, partials, op, B, C, H, W, \
                                   g.tiles_x, g.tiles, gamma2, gkl_gamma, gkl_alpha, record, mm)
     switch (op.taps_id) {
@@ -1763,7 +1800,7 @@ int match_taps(int Rd, const uint32_t* fwd_cols, const uint32_t* adj_cols) {
 }
 
 int k2_partials(const OpDesc& op, int C, int H, int W) {
-  return rb_ok(op, C) ? tile_grid(H, W).tiles * C : tile_grid(H, W).tiles;
+  return rb_ok(op, C, H, W) ? tile_grid(H, W).tiles * C : tile_grid(H, W).tiles;
 }
 
 void launch_k3(int method, float* y, const float* xobs, const double* partials, const OpDesc& op, int B, int C,
@@ -1808,8 +1845,34 @@ void launch_l1_select(const float* v, float* theta, void* scratch, int B, size_t
   hipLaunchKernelGGL((l1_pick_kernel<0, 9, false, true>), dim3(B), dim3(64), 0, st, scr, theta, eta);
 }
 
+template <class T>
+static void launch_k0_rb(hipStream_t st, const float* x, float* out, const float* add, const void* wd, int BC, int H,
+                         int W) {
+  const int tx = (W + kRbW - 1) / kRbW, tiles = tx * ((H + kRbH - 1) / kRbH);
+  const f2_t* w = reinterpret_cast<const f2_t*>(wd);
+  if (add) hipLaunchKernelGGL((k0_blur_rb<T, true>), dim3(BC * tiles), dim3(256), 0, st, x, out, add, w, H, W, tx, tiles);
+  else hipLaunchKernelGGL((k0_blur_rb<T, false>), dim3(BC * tiles), dim3(256), 0, st, x, out, add, w, H, W, tx, tiles);
+}
+
 void launch_op_phi(int kind, int adj, const float* x, float* out, const OpDesc& op, int BC, int H, int W,
                    hipStream_t st, const float* add) {
+  if (kind == OP_BLUR && rb_ok(op, 1, H, W)) {
+#define K0RB(TF, TA)                                                           \
+  if (adj) launch_k0_rb<TA>(st, x, out, add, op.dense_adj, BC, H, W);          \
+  else launch_k0_rb<TF>(st, x, out, add, op.dense_fwd, BC, H, W);
+    switch (op.taps_id) {
+      case TAPS_BLUR_1: K0RB(Taps_blur_1_Fwd, Taps_blur_1_Adj) break;
+      case TAPS_SQUARE_MINI: K0RB(Taps_square_mini_Fwd, Taps_square_mini_Adj) break;
+      default:
+        switch (op.Rd) {
+          case 2: K0RB(DenseTaps<2>, DenseTaps<2>) break;
+          case 4: K0RB(DenseTaps<4>, DenseTaps<4>) break;
+          default: K0RB(DenseTaps<8>, DenseTaps<8>)
+        }
+    }
+#undef K0RB
+    return;
+  }
   const TileGrid g = tile_grid(H, W);
   dim3 grid(g.tiles, BC);
 #define PHI_ARGS x, out, add, op, H, W, g.tiles_x

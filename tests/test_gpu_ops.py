@@ -56,6 +56,27 @@ def test_random_sampling(gpu_ctx, torch_cuda, golden_ops, tag, r, key):
     np.testing.assert_array_equal(out, g[f"phi_{key}_{tag}"].astype(np.float32))
 
 
+@pytest.mark.parametrize("shape,kernel", [((2, 3, 37, 53), "blur_1"), ((1, 1, 6, 7), "blur_1"),
+                                          ((1, 3, 8, 9), "blur_1"), ((2, 1, 40, 24), "dense5")])
+def test_blur_phi_adj_shapes(gpu_ctx, torch_cuda, shape, kernel):
+    """pnp_op_phi / pnp_op_adj_phi (the register-blocked k0 kernel, and the modulo-wrapped
+    stencil for images smaller than the taps' radius) against the FFT oracle: odd widths,
+    images smaller than the 19x19 kernel (np.pad 'wrap' repeats them), a dense 5x5 kernel."""
+    from pnppds import _lib
+    from pnppds.operators import load_blur_kernel
+    rng = np.random.default_rng(7)
+    h = load_blur_kernel("blur_1") if kernel == "blur_1" else rng.random((5, 5)) / 12.5
+    x = rng.random(shape).astype(np.float32)
+    gpu_ctx.set_operator(_lib.OP_BLUR, h=h)
+    dx = dev(torch_cuda, x)
+    B, C, H, W = shape
+    for adj, ref in ((False, O.blur), (True, O.adj_blur)):
+        dy = torch_cuda.empty_like(dx)
+        gpu_ctx.op_phi(dx.data_ptr(), dy.data_ptr(), B, C, H, W, adj=adj)
+        out = host(torch_cuda, dy, gpu_ctx)
+        np.testing.assert_allclose(out, ref(x, h), atol=3e-6, rtol=0)
+
+
 def test_blur_adjointness_full_size(gpu_ctx, torch_cuda):
     """<Φx, z> == <x, Φᵀz> at the metric's image size (size-independent property)."""
     from pnppds import _lib
