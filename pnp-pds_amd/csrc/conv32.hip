@@ -74,13 +74,8 @@ void pack_conv32_weights(const float* W, int mode, int cin, int cout, float* out
   }
 }
 
-#ifndef C32_WAVES
-#define C32_WAVES 4         // waves per workgroup: 4 (two tile rows each) or 8 (one row each, two per SIMD)
-#endif
-constexpr int kC32Waves = C32_WAVES, kC32Threads = 64 * kC32Waves, kC32Rows = 8 / kC32Waves;
-
 template <int MODE, int ACT>
-__global__ __launch_bounds__(kC32Threads, 1) void conv32_kernel(const float* __restrict__ in, float* __restrict__ out,
+__global__ __launch_bounds__(256, 1) void conv32_kernel(const float* __restrict__ in, float* __restrict__ out,
                                                         const float* __restrict__ xin,
                                                         const float* __restrict__ wpk,
                                                         const float* __restrict__ bias, ConvShape s, int C,
@@ -91,16 +86,11 @@ __global__ __launch_bounds__(kC32Threads, 1) void conv32_kernel(const float* __r
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int col = lane & 31, kk = lane >> 5;
   const int Hp = s.H + 2, Wp = s.W + 2;    // fp32 activations: one-pixel border
-  // 8 waves: no registers to spare for the bias; it is read at the epilogue instead
-  constexpr bool kBiasRegs = kC32Waves == 4;
-  float bias_r[T::NM][kBiasRegs ? 16 : 1];
-  if constexpr (kBiasRegs) {
+  float bias_r[T::NM][16];
 #pragma unroll
-    for (int m = 0; m < T::NM; ++m)
+  for (int m = 0; m < T::NM; ++m)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) bias_r[m][r] = bias[32 * m + 16 * kk + r];
-  }
-  auto bias_at = [&](int m, int r) { return kBiasRegs ? bias_r[m][kBiasRegs ? r : 0] : bias[32 * m + 16 * kk + r]; };
+    for (int r = 0; r < 16; ++r) bias_r[m][r] = bias[32 * m + 16 * kk + r];
 
   auto decode = [&](int t, int& b, int& ty0, int& tx0) {
     const int per_img = s.tiles_x * s.tiles_y;
@@ -117,14 +107,14 @@ __global__ __launch_bounds__(kC32Threads, 1) void conv32_kernel(const float* __r
 #else
   constexpr bool kPrefetch = false;
 #endif
-  constexpr int kPre = (kHaloPix * 16 + kC32Threads - 1) / kC32Threads;   // float4 per thread
+  constexpr int kPre = (kHaloPix * 16 + 255) / 256;   // float4 per thread
   float4 pre[kPrefetch ? kPre : 1];
   auto load_pre = [&](int tt) {
     int pb, pty, ptx;
     decode(tt, pb, pty, ptx);
 #pragma unroll
     for (int k = 0; k < kPre; ++k) {
-      const int i = tid + kC32Threads * k;
+      const int i = tid + 256 * k;
       const int p = min(i >> 4, kHaloPix - 1), q = i & 15;
       const int pr = p / kHaloW, pc = p - pr * kHaloW;
       const int yp = pty + pr, xp = ptx + pc;
@@ -142,7 +132,7 @@ __global__ __launch_bounds__(kC32Threads, 1) void conv32_kernel(const float* __r
     if (kPrefetch && have_pre) {
 #pragma unroll
       for (int k = 0; k < kPre; ++k) {
-        const int i = tid + kC32Threads * k;
+        const int i = tid + 256 * k;
         if (i < kHaloPix * 16) {
           float* d = hl + (i >> 4) * T::PITCH + 4 * (i & 15);
           const float4 v = pre[kPrefetch ? k : 0];
@@ -150,7 +140,7 @@ __global__ __launch_bounds__(kC32Threads, 1) void conv32_kernel(const float* __r
         }
       }
     } else if (MODE == 0) {                // gather C channels of the NCHW input, zero outside
-      for (int i = tid; i < kHaloPix * kMaxC; i += kC32Threads) {
+      for (int i = tid; i < kHaloPix * kMaxC; i += 256) {
         const int p = i / kMaxC, c = i - p * kMaxC;
         const int pr = p / kHaloW, pc = p - pr * kHaloW;
         const int y = ty0 - 1 + pr, x = tx0 - 1 + pc;
@@ -159,7 +149,7 @@ __global__ __launch_bounds__(kC32Threads, 1) void conv32_kernel(const float* __r
         hl[p * T::PITCH + c] = v;
       }
     } else {                               // padded NHWC64: 16 float4 per pixel
-      for (int i = tid; i < kHaloPix * 16; i += kC32Threads) {
+      for (int i = tid; i < kHaloPix * 16; i += 256) {
         const int p = i >> 4, q = i & 15;
         const int pr = p / kHaloW, pc = p - pr * kHaloW;
         const int yp = ty0 + pr, xp = tx0 + pc;   // padded coordinates of the halo origin (ty0 - 1, tx0 - 1)
@@ -171,32 +161,26 @@ __global__ __launch_bounds__(kC32Threads, 1) void conv32_kernel(const float* __r
     }
     __syncthreads();
 
-    floatx16 acc[T::NM][kC32Rows];
+    floatx16 acc[T::NM][2];
 #pragma unroll
-    for (int m = 0; m < T::NM; ++m)
-#pragma unroll
-      for (int n = 0; n < kC32Rows; ++n) acc[m][n] = floatx16{};
+    for (int m = 0; m < T::NM; ++m) acc[m][0] = acc[m][1] = floatx16{};
     float wc[T::CP * T::NM], wn[T::CP * T::NM];
 #pragma unroll
     for (int j = 0; j < T::CP * T::NM; ++j) wc[j] = wpk[j * 64 + lane];
     auto do_tap = [&](int tap) {
       const int dy = tap / 3, dx = tap - 3 * dy;
-      const float* h0 = hl + ((kC32Rows * wave + dy) * kHaloW + col + dx) * T::PITCH + kk;
+      const float* h0 = hl + ((2 * wave + dy) * kHaloW + col + dx) * T::PITCH + kk;
+      const float* h1 = h0 + kHaloW * T::PITCH;
 #pragma unroll
       for (int cp = 0; cp < T::CP; ++cp) {
-        float bv[kC32Rows];
+        const float b0 = h0[2 * cp], b1 = h1[2 * cp];
 #pragma unroll
-        for (int n = 0; n < kC32Rows; ++n) bv[n] = h0[n * kHaloW * T::PITCH + 2 * cp];
-#pragma unroll
-        for (int m = 0; m < T::NM; ++m)
-#pragma unroll
-          for (int n = 0; n < kC32Rows; ++n)
-            acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(wc[cp * T::NM + m], bv[n], acc[m][n], 0, 0, 0);
+        for (int m = 0; m < T::NM; ++m) {
+          acc[m][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(wc[cp * T::NM + m], b0, acc[m][0], 0, 0, 0);
+          acc[m][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(wc[cp * T::NM + m], b1, acc[m][1], 0, 0, 0);
+        }
       }
     };
-#ifdef C32_UNROLL_TAPS       // A/B builds only
-#pragma unroll
-#endif
     for (int tap = 0; tap < 8; ++tap) {
 #pragma unroll
       for (int j = 0; j < T::CP * T::NM; ++j) wn[j] = wpk[((tap + 1) * T::CP * T::NM + j) * 64 + lane];   // in flight during this tap
@@ -213,8 +197,8 @@ __global__ __launch_bounds__(kC32Threads, 1) void conv32_kernel(const float* __r
 
     // epilogue: lane (col, kk), register r of M-tile m = channel 32m + 16kk + r
 #pragma unroll
-    for (int n = 0; n < kC32Rows; ++n) {
-      const int y = ty0 + kC32Rows * wave + n, x = tx0 + col;
+    for (int n = 0; n < 2; ++n) {
+      const int y = ty0 + 2 * wave + n, x = tx0 + col;
       if (y >= s.H || x >= s.W) continue;
       float* o = out + (((size_t)b * Hp + y + 1) * Wp + x + 1) * kWidth + 16 * kk;
 #pragma unroll
@@ -222,10 +206,10 @@ __global__ __launch_bounds__(kC32Threads, 1) void conv32_kernel(const float* __r
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           float4 v;
-          v.x = act_fn(acc[m][n][4 * q + 0] + bias_at(m, 4 * q + 0), ACT);
-          v.y = act_fn(acc[m][n][4 * q + 1] + bias_at(m, 4 * q + 1), ACT);
-          v.z = act_fn(acc[m][n][4 * q + 2] + bias_at(m, 4 * q + 2), ACT);
-          v.w = act_fn(acc[m][n][4 * q + 3] + bias_at(m, 4 * q + 3), ACT);
+          v.x = act_fn(acc[m][n][4 * q + 0] + bias_r[m][4 * q + 0], ACT);
+          v.y = act_fn(acc[m][n][4 * q + 1] + bias_r[m][4 * q + 1], ACT);
+          v.z = act_fn(acc[m][n][4 * q + 2] + bias_r[m][4 * q + 2], ACT);
+          v.w = act_fn(acc[m][n][4 * q + 3] + bias_r[m][4 * q + 3], ACT);
           *reinterpret_cast<float4*>(o + 32 * m + 4 * q) = v;
         }
     }
@@ -342,7 +326,7 @@ void launch_conv32(int mode, const float* in, float* out, const float* xin, cons
   const int cap = mode == 0 ? 4 * num_cus : num_cus;   // body: 88 KB of LDS, one workgroup per CU
   const int grid = s.tiles < cap ? s.tiles : cap;
   const size_t lds = mode == 0 ? (size_t)kHaloPix * kC32Pitch4 * 4 : (size_t)kC32Lds;
-#define C32(M, A) hipLaunchKernelGGL((conv32_kernel<M, A>), dim3(grid), dim3(kC32Threads), lds, st, in, out, xin, w, bias, s, \
+#define C32(M, A) hipLaunchKernelGGL((conv32_kernel<M, A>), dim3(grid), dim3(256), lds, st, in, out, xin, w, bias, s, \
                                      C, residual_sign, clamp_out)
   if (mode == 0) {
     if (act == 0) C32(0, 0); else C32(0, 1);
