@@ -167,33 +167,50 @@ __global__ __launch_bounds__(256, 1) void conv32_kernel(const float* __restrict_
     float wc[T::CP * T::NM], wn[T::CP * T::NM];
 #pragma unroll
     for (int j = 0; j < T::CP * T::NM; ++j) wc[j] = wpk[j * 64 + lane];
-    auto do_tap = [&](int tap) {
+    auto do_tap = [&](int tap, const float (&w)[T::CP * T::NM]) {
       const int dy = tap / 3, dx = tap - 3 * dy;
       const float* h0 = hl + ((2 * wave + dy) * kHaloW + col + dx) * T::PITCH + kk;
       const float* h1 = h0 + kHaloW * T::PITCH;
+      // B values read PD = 2 K-steps ahead, the order pinned by a scheduling barrier per K-step
+      // (the compiler's own schedule read them one MFMA ahead: 5.34 vs 5.27 ms per layer at cfg4;
+      // PD = 1 / 4: 5.27 / 5.28)
+      constexpr int PD = 2;
+      float q0[PD + 1], q1[PD + 1];
+#pragma unroll
+      for (int i = 0; i < PD; ++i) { q0[i] = h0[2 * i]; q1[i] = h1[2 * i]; }
 #pragma unroll
       for (int cp = 0; cp < T::CP; ++cp) {
-        const float b0 = h0[2 * cp], b1 = h1[2 * cp];
+        if (cp + PD < T::CP) {
+          q0[(cp + PD) % (PD + 1)] = h0[2 * (cp + PD)];
+          q1[(cp + PD) % (PD + 1)] = h1[2 * (cp + PD)];
+        }
+        const float b0 = q0[cp % (PD + 1)], b1 = q1[cp % (PD + 1)];
 #pragma unroll
         for (int m = 0; m < T::NM; ++m) {
-          acc[m][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(wc[cp * T::NM + m], b0, acc[m][0], 0, 0, 0);
-          acc[m][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(wc[cp * T::NM + m], b1, acc[m][1], 0, 0, 0);
+          acc[m][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(w[cp * T::NM + m], b0, acc[m][0], 0, 0, 0);
+          acc[m][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(w[cp * T::NM + m], b1, acc[m][1], 0, 0, 0);
         }
+        __builtin_amdgcn_sched_barrier(0);
       }
     };
-    for (int tap = 0; tap < 8; ++tap) {
+    auto load_w = [&](float (&w)[T::CP * T::NM], int tap) {   // in flight during the tap before
 #pragma unroll
-      for (int j = 0; j < T::CP * T::NM; ++j) wn[j] = wpk[((tap + 1) * T::CP * T::NM + j) * 64 + lane];   // in flight during this tap
-      do_tap(tap);
-#pragma unroll
-      for (int j = 0; j < T::CP * T::NM; ++j) wc[j] = wn[j];
+      for (int j = 0; j < T::CP * T::NM; ++j) w[j] = wpk[(tap * T::CP * T::NM + j) * 64 + lane];
+    };
+    // Taps in pairs: the two weight sets swap roles instead of being copied (a copy of 64
+    // registers per tap, into AGPRs beside the MFMAs reading them: 5.27 vs 5.02 ms per layer at cfg4)
+    for (int tap = 0; tap < 8; tap += 2) {
+      load_w(wn, tap + 1);
+      do_tap(tap, wc);
+      load_w(wc, tap + 2);
+      do_tap(tap + 1, wn);
     }
     have_pre = false;
     if (kPrefetch && t + (int)gridDim.x < s.tiles) {
       load_pre(t + gridDim.x);
       have_pre = true;
     }
-    do_tap(8);
+    do_tap(8, wc);
 
     // epilogue: lane (col, kk), register r of M-tile m = channel 32m + 16kk + r
 #pragma unroll
