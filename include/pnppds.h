@@ -126,7 +126,7 @@ int pnp_set_precision(pnp_ctx* ctx, int precision);
 
 /* Performance knobs (no effect on results).
  * PNP_TUNE_DENOISE_CHUNK: images per denoiser pass (0 = auto: the whole batch, unless its
- * activation ping-pong pair would exceed 8 GB (fp16) / 16 GB (fp32)).                */
+ * activation ping-pong pair would exceed an eighth of the device's memory; then equal passes). */
 enum pnp_tuning_key {
   PNP_TUNE_DENOISE_CHUNK = 1,
   PNP_TUNE_BODY_LAYERS = 2,  /* 64->64 layers per launch: 0 = auto (default: 2 when the batch has

@@ -255,9 +255,8 @@ void ensure_act(pnp_ctx* ctx, DevBuf (&act)[2], int B, int H, int W, hipStream_t
   for (int i = 0; i < 2; ++i) ensure_padded(ctx, act[i], B, H, W, kWidth, kActPad, st);
 }
 
-// Images per denoiser pass.  Auto: the whole batch, unless its two fp16 activation
-// images (2 x B x (H+2)(W+2) x 128 B) would exceed 8 GB.  (Passes sized to stay in the
-// 256 MB Infinity Cache measured no faster at 256x256: conv_body is not HBM-bound.)
+// Images per denoiser pass: see denoise_chunk / split_passes below.  (Passes sized to stay in
+// the 256 MB Infinity Cache measured no faster at 256x256: conv_body is not HBM-bound.)
 // Two body layers per launch (conv_body_f2) when its strips fill the chip: one workgroup per
 // 32-column strip walks the strip's rows serially, so a batch with fewer strips than CUs (B = 1
 // at 256^2: 8 strips, 0.23 ms per layer pair) runs one layer per launch over 8 x 32 tiles
