@@ -17,11 +17,13 @@ synthetic RGB 256x256 images per GPU.  The other configurations are BASELINE.jso
 Images are independent, so ranks process disjoint shards with no data-path collective (weak
 scaling).  ``value`` = image-iterations/s over the whole job (sum over ranks / max rank time).
 
-Also reported: ``roofline`` of the dominant kernel (conv_body, HBM-bound at 288 FLOP/B:
-algorithmic bytes / HIP-event duration vs 8 TB/s, MFMA fraction alongside, ``traffic`` =
-PMC-measured bytes per launch from the committed profile), HBM fractions of the fused
-prox/operator kernels, PSNR delta vs the CPU oracle on image 0, and ``cpu_baseline``: the
-oracle restatement of the reference's test_iter timed on this host (rank 0, N=1 only).
+Also reported: ``roofline`` of the dominant kernel (at the metric conv_body_x8, two 64->64
+layers per launch, MFMA-bound at 576 FLOP/B: algorithmic FLOPs / HIP-event duration vs the
+2.5 PF dense fp16 peak, the HBM side alongside, ``traffic`` = PMC-measured bytes per launch
+from the committed profile; a one-layer launch is 288 FLOP/B and reported against HBM), HBM
+fractions of the fused prox/operator kernels (also against an in-house float4 copy kernel),
+PSNR delta vs the CPU oracle on image 0, and ``cpu_baseline``: the oracle restatement of the
+reference's test_iter timed on this host (rank 0, N=1 only).
 """
 import argparse
 import json

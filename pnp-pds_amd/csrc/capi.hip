@@ -82,8 +82,11 @@ struct pnp_ctx {
 
   // scratch for single ops
   DevBuf scr_u32, scr_act[2], scr_part, scr_theta;
-  DevBuf act32[2];   // fp32 hidden activations (PNP_PREC_FP32), shared by the solver and pnp_op_denoise
-  DevBuf l1_scr;     // l1-ball select histograms + per-image state (launch_l1_select)
+  DevBuf act32[2];   // fp32 hidden activations (PNP_PREC_FP32) of the solver
+  DevBuf l1_scr;     // l1-ball select histograms + per-image state (launch_l1_select) of the solver
+  // the stream-parameterised single ops (pnp_op_*) keep their own stateful scratch, so they never
+  // share zero-border or cleared-bin buffers with the solver across streams or graph replays
+  DevBuf scr_act32[2], scr_l1;
 
   // graph replay of the iteration launches (small batches): PNP_TUNE_GRAPH
   int graph_mode = 0;          // 0 off (default), 1 on
@@ -148,13 +151,14 @@ int guarded(pnp_ctx* ctx, F&& f) {
 void ensure(pnp_ctx* ctx, DevBuf& b, size_t bytes, bool zero = false) {
   if (bytes == 0) bytes = 16;
   if (b.p && b.bytes >= bytes) return;
+  // before the grow path: its stream sync and hipFree would invalidate the capture
+  if (ctx->capturing) fail(ctx, PNP_E_STATE, "allocation inside a graph capture");
   if (b.p) {
     HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
     HIPCHK(ctx, hipFree(b.p));
     b.p = nullptr;
     b.bytes = 0;
   }
-  if (ctx->capturing) fail(ctx, PNP_E_STATE, "allocation inside a graph capture");
   hipError_t e = hipMalloc(&b.p, bytes);
   if (e != hipSuccess) fail(ctx, PNP_E_OOM, "hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
   ctx->gen++;
@@ -288,15 +292,16 @@ int denoise_chunk(pnp_ctx* ctx, int B, int H, int W) {
 }
 
 // fp32-operand forward (PNP_PREC_FP32): u32 (NCHW, clamped input) -> xout, conv32.hip.
-void run_denoiser32(pnp_ctx* ctx, const float* u32, float* xout, int B, int H, int W, hipStream_t st) {
+void run_denoiser32(pnp_ctx* ctx, const float* u32, float* xout, DevBuf (&act32)[2], int B, int H, int W,
+                    hipStream_t st) {
   const double per_img = 2.0 * act32_bytes(1, H, W);
   const int m = ctx->den_chunk > 0 ? std::min(ctx->den_chunk, B) : split_passes(B, per_img, ctx->act_budget);
   for (int i = 0; i < 2; ++i) {                 // one-pixel zero border, zeroed once per geometry
     const long long geom = ((long long)m << 40) ^ ((long long)H << 20) ^ (long long)W;
-    ensure(ctx, ctx->act32[i], act32_bytes(m, H, W));
-    if (ctx->act32[i].geom != geom) {
-      HIPCHK(ctx, hipMemsetAsync(ctx->act32[i].p, 0, act32_bytes(m, H, W), st));
-      ctx->act32[i].geom = geom;
+    ensure(ctx, act32[i], act32_bytes(m, H, W));
+    if (act32[i].geom != geom) {
+      HIPCHK(ctx, hipMemsetAsync(act32[i].p, 0, act32_bytes(m, H, W), st));
+      act32[i].geom = geom;
     }
   }
   const int C = ctx->den_C, nbody = ctx->den_depth - 2;
@@ -308,21 +313,21 @@ void run_denoiser32(pnp_ctx* ctx, const float* u32, float* xout, int B, int H, i
     float* xo = xout + (size_t)b0 * C * H * W;
     {
       ProfScope ps(ctx, "conv32_head", st);
-      launch_conv32(0, xin, P<float>(ctx->act32[0]), nullptr, P<float>(ctx->head_w32), P<float>(ctx->head_b), s, C,
+      launch_conv32(0, xin, P<float>(act32[0]), nullptr, P<float>(ctx->head_w32), P<float>(ctx->head_b), s, C,
                     ctx->den_act, 1, 0, ctx->num_cus, st);
       check_launch(ctx, "conv32_head");
     }
     int cur = 0;
     for (int l = 0; l < nbody; ++l, cur ^= 1) {
       ProfScope ps(ctx, "conv32_body", st);
-      launch_conv32(1, P<float>(ctx->act32[cur]), P<float>(ctx->act32[cur ^ 1]), nullptr,
+      launch_conv32(1, P<float>(act32[cur]), P<float>(act32[cur ^ 1]), nullptr,
                     P<float>(ctx->body_w32) + (size_t)l * wb, P<float>(ctx->body_b) + l * kWidth, s, C, ctx->den_act,
                     1, 0, ctx->num_cus, st);
       check_launch(ctx, "conv32_body");
     }
     {
       ProfScope ps(ctx, "conv32_tail", st);
-      launch_conv32(2, P<float>(ctx->act32[cur]), xo, xin, P<float>(ctx->tail_w32), P<float>(ctx->tail_b), s, C,
+      launch_conv32(2, P<float>(act32[cur]), xo, xin, P<float>(ctx->tail_w32), P<float>(ctx->tail_b), s, C,
                     ctx->den_act, ctx->den_residual, ctx->den_clamp, ctx->num_cus, st);
       check_launch(ctx, "conv32_tail");
     }
@@ -334,7 +339,7 @@ void run_denoiser(pnp_ctx* ctx, const float* u32, float* xout, DevBuf (&act)[2],
                   int W, hipStream_t st) {
   if (!ctx->den_ready) fail(ctx, PNP_E_STATE, "denoiser not set (pnp_set_denoiser)");
   if (ctx->prec == PNP_PREC_FP32) {
-    run_denoiser32(ctx, u32, xout, B, H, W, st);
+    run_denoiser32(ctx, u32, xout, &act[0] == &ctx->act[0] ? ctx->act32 : ctx->scr_act32, B, H, W, st);
     return;
   }
   const int m = denoise_chunk(ctx, B, H, W);
@@ -392,11 +397,17 @@ void run_denoiser(pnp_ctx* ctx, const float* u32, float* xout, DevBuf (&act)[2],
   }
 }
 
-// l1-ball threshold per image into theta (scratch grown and zeroed on demand)
-void l1_select(pnp_ctx* ctx, const float* v, float* theta, int B, size_t n, double eta, hipStream_t st) {
+// l1-ball threshold per image into theta.  The scratch (histogram bins every launch leaves
+// cleared) is grown and zeroed on demand on the stream that uses it: the solver's (ctx->l1_scr,
+// ctx->stream) or a single op's (ctx->scr_l1, the caller's stream).
+void l1_select(pnp_ctx* ctx, DevBuf& scr, const float* v, float* theta, int B, size_t n, double eta,
+               hipStream_t st) {
   const size_t need = l1_select_scratch_bytes(B);
-  if (!ctx->l1_scr.p || ctx->l1_scr.bytes < need) ensure(ctx, ctx->l1_scr, need, true);
-  launch_l1_select(v, theta, ctx->l1_scr.p, B, n, eta, st);
+  if (!scr.p || scr.bytes < need) {
+    ensure(ctx, scr, need);
+    HIPCHK(ctx, hipMemsetAsync(scr.p, 0, scr.bytes, st));
+  }
+  launch_l1_select(v, theta, scr.p, B, n, eta, st);
 }
 
 // -------- one solver iteration -------------------------------------------------------
@@ -440,7 +451,7 @@ void solver_iteration(pnp_ctx* ctx) {
   if (mb) {
     ProfScope ps(ctx, "l1_select", st);
     const double eta = p.alpha_s * (double)n * p.sp_nl * p.r * 0.5;   // operators.py:96
-    l1_select(ctx, P<float>(ctx->w), P<float>(ctx->theta), B, n, eta, st);
+    l1_select(ctx, ctx->l1_scr, P<float>(ctx->w), P<float>(ctx->theta), B, n, eta, st);
     check_launch(ctx, "l1_select");
   }
   run_denoiser(ctx, P<float>(ctx->u32), xn, ctx->act, B, H, W, st);
@@ -504,7 +515,7 @@ void solver_iteration_admm(pnp_ctx* ctx) {
     const double eta = p.alpha_s * (double)n * p.sp_nl * 0.5;               // operators.py:96, r = 1
     for (int i = 0; i < p.m2; ++i) {
       launch_lincomb(w, 0.0, sv, 1.0 - g, pp, -g, y, -g, z, g, N, st);       // s - (Phi x + s - z + y) / g1
-      l1_select(ctx, w, P<float>(ctx->theta), B, n, eta, st);
+      l1_select(ctx, ctx->l1_scr, w, P<float>(ctx->theta), B, n, eta, st);
       launch_shrink(w, sv, P<float>(ctx->theta), B, n, st);
     }
     check_launch(ctx, "admm_s_step");
@@ -557,7 +568,7 @@ void solver_iteration_cmp(pnp_ctx* ctx) {
   const double eta = p.alpha_s * (double)n * p.sp_nl * 0.5;                         // proj_l1_ball, r = 1
   const double eps = std::sqrt((double)n * (1.0 - p.sp_nl)) * p.alpha_n * p.gaussian_nl;  // proj_l2_ball, r = 1
   auto l1proj = [&](const float* in, float* out) {
-    l1_select(ctx, in, P<float>(ctx->theta), B, n, eta, st);
+    l1_select(ctx, ctx->l1_scr, in, P<float>(ctx->theta), B, n, eta, st);
     launch_shrink(in, out, P<float>(ctx->theta), B, n, st);
   };
   auto metrics = [&] {
@@ -618,7 +629,7 @@ void solver_iteration_cmp(pnp_ctx* ctx) {
       const int mb = m == PNP_METHOD_B_HTV;
       if (mb) {
         lin(w, 0.0, sv, 1.0, y, -p.gamma1);
-        l1_select(ctx, w, P<float>(ctx->theta), B, n, eta, st);
+        l1_select(ctx, ctx->l1_scr, w, P<float>(ctx->theta), B, n, eta, st);
       }
       launch_tv_dual(xn, xo, y1, p.gamma2, B, C, H, W, st);
       launch_k2(od.kind, mb ? PNP_METHOD_B : PNP_METHOD_A, xn, xo, y, xobs, xt, sv, w, P<float>(ctx->theta),
@@ -928,7 +939,7 @@ int pnp_destroy(pnp_ctx* ctx) {
                     &ctx->z, &ctx->p, &ctx->t, &ctx->dense_fwd, &ctx->dense_adj, &ctx->ssim_scr,
                     &ctx->taps64, &ctx->y1, &ctx->d, &ctx->c1, &ctx->dg_words, &ctx->dg_flag, &ctx->dg_rank, &ctx->dg_scan, &ctx->dg_noise,
                     &ctx->dg_img, &ctx->dg_draws, &ctx->dg_first, &ctx->dg_status,
-                    &ctx->head_w32, &ctx->body_w32, &ctx->tail_w32, &ctx->act32[0], &ctx->act32[1], &ctx->l1_scr, &ctx->ssim_mm, &ctx->head_wlo, &ctx->body_wlo, &ctx->tail_wlo, &ctx->body_w16};
+                    &ctx->head_w32, &ctx->body_w32, &ctx->tail_w32, &ctx->act32[0], &ctx->act32[1], &ctx->l1_scr, &ctx->scr_act32[0], &ctx->scr_act32[1], &ctx->scr_l1, &ctx->ssim_mm, &ctx->head_wlo, &ctx->body_wlo, &ctx->tail_wlo, &ctx->body_w16};
   for (DevBuf* b : bufs) release(*b);
   graph_release(ctx);
   release(ctx->it_dev);
@@ -979,8 +990,8 @@ int pnp_set_precision(pnp_ctx* ctx, int precision) {
   return guarded(ctx, [&] {
     if (precision != PNP_PREC_FP16 && precision != PNP_PREC_FP32 && precision != PNP_PREC_FP16W2)
       fail(ctx, PNP_E_UNSUPPORTED, "precision %d not supported", precision);
+    if (ctx->prec != precision) ctx->gen++;   // a captured graph holds the other precision's kernels
     ctx->prec = precision;
-    ctx->gen++;
   });
 }
 
@@ -1333,7 +1344,7 @@ int pnp_op_proj_l1_ball(pnp_ctx* ctx, const float* x, float* out, int B, int64_t
     ensure(ctx, ctx->scr_theta, (size_t)B * sizeof(float));
     const double eta = alpha_s * (double)n * sp_nl * r * 0.5;    // operators.py:96
     hipStream_t st = pick_stream(ctx, stream);
-    l1_select(ctx, x, P<float>(ctx->scr_theta), B, (size_t)n, eta, st);
+    l1_select(ctx, ctx->scr_l1, x, P<float>(ctx->scr_theta), B, (size_t)n, eta, st);
     check_launch(ctx, "l1_select");
     launch_shrink(x, out, P<float>(ctx->scr_theta), B, (size_t)n, st);
     check_launch(ctx, "shrink");

@@ -345,650 +345,6 @@ constexpr int kF2Lds = kF2Mid + 8 * kF2MidPlane;               // 163840 B: all 
 
 __device__ __forceinline__ int f2_slot(int row) { return (row + 1 + 18 * 64) % kF2Ring; }   // row >= -1 - 18*64
 
-#if defined(F2_STAMPS) && !defined(F2_STREAM_KERNEL)
-#define F2_STREAM_KERNEL
-#endif
-#ifdef F2_STREAM_KERNEL
-// ---- A/B and diagnostic builds only (tools/build_ab.sh -DF2_STREAM_KERNEL): the one-wave-
-// per-SIMD form of the same schedule, one software-pipelined MFMA stream per wave and step
-// (2.29-2.34 ms per pair vs conv_body_f8's 2.24). ----
-#ifndef F2_PREFETCH
-#define F2_PREFETCH 2
-#endif
-#ifndef F2_L1_ROWS
-#define F2_L1_ROWS 1
-#endif
-#ifndef F2_EPI_PARTS
-#define F2_EPI_PARTS 4
-#endif
-constexpr int kF2EpiParts = F2_EPI_PARTS;  // 2 or 4: epilogue parts per N-tile (8 or 4 channels each)
-constexpr int kF2L1Rows = F2_L1_ROWS;      // halo rows DMA'd per step by each layer-l wave (of 8)
-// One wave's MFMA stream for a step: G groups of NT N-tiles against one chunk-planar ring
-// (PLANE bytes per chunk plane), acc[g][n] = sum_ks A[ks] B_gn[ks].  The stream runs through
-// the group boundaries without a bubble: B fragments are read F2_PREFETCH K-steps ahead
-// across them (one wave per SIMD: nothing else hides an LDS read's latency), the
-// accumulators are per group (AGPRs are free here), and group g's epilogue runs in
-// kF2EpiParts parts per N-tile, epi(g, n, q) at K-step 2 + kF2EpiParts n + q of group g+1, so
-// that each K-step's VALU fits beside its MFMAs (one wave per SIMD: MI355X_MICROARCH.md).
-// side(fs) is called once per K-step (the halo DMA pieces go there).
-// ad[g][n][dy]: byte address of the lane's pixel in tap row dy of N-tile n of group g,
-// chunk h; K-step ks = 4 tap + sub reads chunk 2 sub + h of tap column dx = +16 dx bytes.
-template <int G, int NT, int PLANE, class Epi, class Side>
-__device__ __forceinline__ void f2_stream(const half8_t (&wA)[kBodyKSteps], const unsigned char* ring,
-                                          const int (&ad)[G][NT][3], floatx16 (&acc)[G][NT], Epi&& epi,
-                                          Side&& side) {
-  constexpr int KS = kBodyKSteps, T = G * KS, D = F2_PREFETCH;
-  auto ldB = [&](int fs, int n) {
-    const int g = fs / KS, ks = fs - g * KS;
-    const int tap = ks >> 2, sub = ks & 3, dy = tap / 3, dx = tap - 3 * dy;
-    return *reinterpret_cast<const half8_t*>(ring + ad[g][n][dy] + (2 * sub * PLANE + 16 * dx));
-  };
-  half8_t fb[D + 1][NT];
-#pragma unroll
-  for (int d = 0; d < D; ++d)
-#pragma unroll
-    for (int n = 0; n < NT; ++n) fb[d][n] = ldB(d, n);
-#pragma unroll
-  for (int fs = 0; fs < T; ++fs) {
-    const int g = fs / KS, ks = fs - g * KS;
-    if (fs + D < T) {
-#pragma unroll
-      for (int n = 0; n < NT; ++n) fb[(fs + D) % (D + 1)][n] = ldB(fs + D, n);
-    }
-#pragma unroll
-    for (int n = 0; n < NT; ++n)
-      acc[g][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wA[ks], fb[fs % (D + 1)][n],
-                                                         ks == 0 ? floatx16{} : acc[g][n], 0, 0, 0);
-    if (g > 0 && ks >= 2 && ks < 2 + kF2EpiParts * NT) epi(g - 1, (ks - 2) / kF2EpiParts, (ks - 2) % kF2EpiParts);
-    side(fs);
-    __builtin_amdgcn_sched_barrier(0);       // keep the reads D K-steps ahead of their MFMAs
-  }
-  side(T);                                   // (end of the MFMA stream)
-#pragma unroll
-  for (int n = 0; n < NT; ++n)
-#pragma unroll
-    for (int q = 0; q < kF2EpiParts; ++q) epi(G - 1, n, q);
-}
-
-#ifdef F2_STAMPS
-// Diagnostic build only (tools/f2_stamps.py): per wave, cycles summed over the steps of
-// [0] step setup, [1] MFMA stream, [2] last group's epilogue, [3] DMA wait, [4] barrier wait,
-// [5] steps.  Written to a buffer nothing else reads; never in the product library.
-__device__ unsigned long long f2_stamp_buf[1024 * 4 * 8];
-#define F2_STAMP(k)                                              \
-  do {                                                           \
-    const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
-    st_acc[k] += now_ - st_t;                                    \
-    st_t = now_;                                                 \
-  } while (0)
-#else
-#define F2_STAMP(k) ((void)0)
-#endif
-
-template <int ACT>
-__global__ __launch_bounds__(256, 1) void conv_body_f2_kernel(const half_t* __restrict__ in,
-                                                               half_t* __restrict__ out,
-                                                               const uint4* __restrict__ w1,
-                                                               const float* __restrict__ b1,
-                                                               const uint4* __restrict__ w2,
-                                                               const float* __restrict__ b2, ConvShape s,
-                                                               int strips_x, int nstrips, int sb) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  unsigned char* ring = smem;
-  unsigned char* mid = smem + kF2Mid;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int layer = wave >> 1, m = wave & 1;
-  const int h = lane >> 5, col = lane & 31;
-  const uint4* wsrc = layer ? w2 : w1;
-  half8_t wA[kBodyKSteps];
-#pragma unroll
-  for (int ks = 0; ks < kBodyKSteps; ++ks)
-    wA[ks] = *reinterpret_cast<const half8_t*>(reinterpret_cast<const unsigned char*>(wsrc) +
-                                               ((ks * 2 + m) * 64 + lane) * 16);
-  float bl[16];
-#pragma unroll
-  for (int r = 0; r < 16; ++r) bl[r] = (layer ? b2 : b1)[32 * m + 16 * h + r];
-  const unsigned img_bytes = (unsigned)(s.Hp * s.Wp) * 128u;
-
-  // The workgroup's strips k = 0 .. K-1 (strip blockIdx.x + k gridDim.x) form one stream of
-  // global rows: row r of strip k is global row k S + r, S = 8 sb >= H + 1, so rows H .. S-1
-  // of a strip (zero) are also the zero row -1 of the next, and the steps run on across strip
-  // boundaries without a prologue or a drain per strip.
-  const int S = 8 * sb;
-  const int K = (nstrips - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
-  auto geom = [&](int k) {                               // (image, first column) of strip k
-    const int st = min(blockIdx.x + k * gridDim.x, (unsigned)nstrips - 1);
-    const int b = st / strips_x;
-    return SGeom{b, (st - b * strips_x) * kTileW};
-  };
-  int kJ = 0, jb = 0;                                    // step J = kJ sb + jb: strip kJ, row block jb
-  // strips kJ-1, kJ, kJ+1 (no divisions in the steps); plain ints picked by value (a select
-  // of addresses would keep them in scratch memory)
-  int gpb, gpx, gcb, gcx, gnb, gnx;
-  {
-    const SGeom g0 = geom(0), g1 = geom(1);
-    gpb = gcb = g0.b;
-    gpx = gcx = g0.x0;
-    gnb = g1.b;
-    gnx = g1.x0;
-  }
-  auto pick = [&](int k) {
-    const int pb = gpb, px = gpx, cb = gcb, cx = gcx, nb = gnb, nx = gnx;
-    return SGeom{k > kJ ? nb : (k < kJ ? pb : cb), k > kJ ? nx : (k < kJ ? px : cx)};
-  };
-  auto locate = [&](int R, int kJ, int& k, int& r) {    // global row -> (strip, row), |strip - kJ| <= 1
-    k = kJ;
-    r = R - kJ * S;
-    if (r < 0) { --k; r += S; } else if (r >= S) { ++k; r -= S; }
-  };
-  // DMA state of one input row: descriptor of its strip's image (none = zeros), lane offset
-  __amdgpu_buffer_rsrc_t dsrc;
-  unsigned dvo;
-  unsigned char* ddst;
-  auto dma_at = [&](int R, int kJ) {                     // lane c < 36: padded column x0 + c
-    int k, r;
-    locate(R, kJ, k, r);
-    const bool valid = R >= 0 && k < K;
-    const SGeom G = pick(k);
-    dsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(in + (size_t)G.b * s.Hp * s.Wp * kWidth), (short)0,
-                                             valid ? (int)img_bytes : 0, 0x00020000);
-    dvo = (unsigned)(((r + s.pad) * s.Wp + G.x0 + lane) * 128);   // rows past the image read 0 (OOB)
-    ddst = ring + f2_slot(R) * (kF2InW * 16);
-  };
-  auto dma_plane = [&](int c) {
-    if (lane < kF2InW)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(dsrc, (__attribute__((address_space(3))) void*)(ddst + c * kF2InPlane),
-                                               16, dvo + 16 * c, 0, 0, 0);   // an imm offset would move the LDS side too
-  };
-  // prologue: input rows -1 .. 8 (ring rows 0 .. 9); intermediate row -1 (ring row 0) = 0
-  for (int r = wave; r < 10; r += 4) {
-    dma_at(r - 1, 0);
-#pragma unroll 1
-    for (int c = 0; c < 8; ++c) dma_plane(c);
-  }
-  for (int q = tid; q < 8 * kF2MidW; q += 256) {
-    const int c = q / kF2MidW, p = q - c * kF2MidW;
-    *reinterpret_cast<v4i_t*>(mid + c * kF2MidPlane + p * 16) = v4i_t{0, 0, 0, 0};
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
-#ifdef F2_STAMPS
-  unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0}, st_t = __builtin_amdgcn_s_memtime();
-#endif
-  for (int J = 0; J <= K * sb; ++J) {
-    // The next step's new input rows 8J+9 .. 8J+16 (8 DMA pieces per row, one per chunk
-    // plane): waves 0-1 (layer l, 36 more MFMAs per step) kF2L1Rows rows each, waves 2-3 the rest.
-    const int row0 = 8 * J + 9 + (layer ? 2 * kF2L1Rows + (4 - kF2L1Rows) * m : kF2L1Rows * m);
-    auto piece = [&](int i) {                            // piece i: plane i & 7 of row row0 + (i >> 3)
-      if ((i & 7) == 0) dma_at(row0 + (i >> 3), kJ);
-      dma_plane(i & 7);
-    };
-    if (layer == 0) {
-      const int x0 = gcx;
-      if (J < K * sb && 8 * jb < s.H) {
-        // intermediate rows 8jb .. 8jb+7 of strip kJ: N-tile k < 8 = row 8jb+k, columns 1 .. 32 of
-        // the ring; N-tile 8 = the strip halo, columns 0 and 33 of the 8 rows (16 pixels, lanes
-        // 16-31 repeat lanes 0-15 and store nothing); 3 groups of 3.  Row-aligned tiles keep
-        // every 16-lane group of a fragment read on consecutive pixels.
-        int ad[3][3][3], prow[3][3], pcol[3][3];
-        {
-          int sl = f2_slot(8 * J - 1);                   // input rows 8J-1 .. 8J+8: ring slots stepped
-          int rowoff[10];
-#pragma unroll
-          for (int q = 0; q < 10; ++q) {
-            rowoff[q] = sl * (kF2InW * 16);
-            sl = sl == kF2Ring - 1 ? 0 : sl + 1;
-          }
-          const int hr = (col & 15) >> 1, hc = (col & 1) ? kF2MidW - 1 : 0;   // the halo tile's pixel
-#pragma unroll
-          for (int g = 0; g < 3; ++g)
-#pragma unroll
-            for (int n = 0; n < 3; ++n) {
-              const int k = 3 * g + n;
-              prow[g][n] = k < 8 ? k : hr;
-              pcol[g][n] = k < 8 ? 1 + col : hc;
-#pragma unroll
-              for (int dy = 0; dy < 3; ++dy) {
-                // row k - 1 + dy: uniform for the row tiles; the halo tile's row is per lane
-                int ro = rowoff[0];
-#pragma unroll
-                for (int q = 1; q < 10; ++q)
-                  if (k == 8) ro = hr + dy == q ? rowoff[q] : ro;
-                ad[g][n][dy] = h * kF2InPlane + (k < 8 ? rowoff[k + dy] : ro) + pcol[g][n] * 16;
-              }
-            }
-        }
-        floatx16 acc[3][3];
-        half8_t stage;
-        F2_STAMP(0);
-        f2_stream<3, 3, kF2InPlane>(
-            wA, ring, ad, acc,
-            [&](int g, int n, int q) {           // part q: rows 8 hf + NV sub .. of the accumulator
-              constexpr int PH = kF2EpiParts / 2, NV = 8 / PH;
-              const int hf = q / PH, sub = q % PH;
-              bias_act_s<ACT, NV>(stage, sub, acc[g][n], 8 * hf, bl + 8 * hf);
-              if (sub != PH - 1 || (3 * g + n == 8 && col >= 16)) return;
-              const int x = x0 - 1 + pcol[g][n];
-              const bool inside = 8 * jb + prow[g][n] < s.H && x >= 0 && x < s.W;
-              *reinterpret_cast<half8_t*>(mid + (4 * m + 2 * h + hf) * kF2MidPlane +
-                                          (f2_slot(8 * J + prow[g][n]) * kF2MidW + pcol[g][n]) * 16) =
-                  inside ? stage : half8_t{};   // zero outside the image: the next layer's padding
-            },
-            [&](int fs) {
-              if ((fs & 3) == 2 && (fs >> 2) < 8 * kF2L1Rows) piece(fs >> 2);
-              if (fs == 3 * kBodyKSteps) F2_STAMP(1);
-            });
-        F2_STAMP(2);
-      } else {
-        // a block below the image (or past the last strip): zero rows, no MFMAs
-#pragma unroll 1
-        for (int i = 0; i < 8 * kF2L1Rows; ++i) piece(i);
-        for (int q = lane; q < 8 * kF2MidW * 4; q += 64) {   // 8 rows x 34 pixels x this M-tile's 4 planes
-          const int c = q / (8 * kF2MidW), p = q - c * (8 * kF2MidW), rr = p / kF2MidW, pc = p - rr * kF2MidW;
-          *reinterpret_cast<v4i_t*>(mid + (4 * m + c) * kF2MidPlane + (f2_slot(8 * J + rr) * kF2MidW + pc) * 16) =
-              v4i_t{0, 0, 0, 0};
-        }
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMAs have landed
-      F2_STAMP(3);
-    } else {
-      if (J > 0) {
-        // global output rows 8J-9 .. 8J-2 (N-tile t = row 8J-9+t, pixel = column), 2 groups of 4
-        // mid rows 8J-10 .. 8J-1: ring slots stepped from the first (no per-row modulo)
-        int ad[2][4][3];
-        {
-          const int lb = h * kF2MidPlane + col * 16;
-          int sl = f2_slot(8 * J - 10);
-          int rowoff[10];
-#pragma unroll
-          for (int q = 0; q < 10; ++q) {
-            rowoff[q] = sl * (kF2MidW * 16);
-            sl = sl == kF2Ring - 1 ? 0 : sl + 1;
-          }
-#pragma unroll
-          for (int g = 0; g < 2; ++g)
-#pragma unroll
-            for (int n = 0; n < 4; ++n)
-#pragma unroll
-              for (int dy = 0; dy < 3; ++dy) ad[g][n][dy] = lb + rowoff[4 * g + n + dy];
-        }
-        // output rows 8J-9+t (none: stores dropped): strip and row of the first, then row by row
-        __amdgpu_buffer_rsrc_t ors[8];
-        {
-          int k, r;
-          locate(8 * J - 9, kJ, k, r);
-          const bool first = 8 * J - 9 >= 0;
-#pragma unroll
-          for (int t = 0; t < 8; ++t) {
-            if (t > 0 && ++r == S) { r = 0; ++k; }
-            const bool ok = (first || t >= 9 - 8 * J) && k < K && r < s.H;
-            const SGeom G = pick(k);
-            half_t* row = out + (((size_t)G.b * s.Hp + r + s.pad) * s.Wp + G.x0 + s.pad) * kWidth;
-            ors[t] = __builtin_amdgcn_make_buffer_rsrc(ok ? (void*)row : (void*)out, (short)0,
-                                                       ok ? min(kTileW, s.W - G.x0) * 128 : 0, 0x00020000);
-          }
-        }
-        floatx16 acc[2][4];
-        half8_t stage;
-        F2_STAMP(0);
-        f2_stream<2, 4, kF2MidPlane>(
-            wA, mid, ad, acc,
-            [&](int g, int n, int q) {
-              constexpr int PH = kF2EpiParts / 2, NV = 8 / PH;
-              const int hf = q / PH, sub = q % PH;
-              bias_act_s<ACT, NV>(stage, sub, acc[g][n], 8 * hf, bl + 8 * hf);
-              if (sub != PH - 1) return;
-              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i_t, stage), ors[4 * g + n],
-                                                     (unsigned)(col * 128 + 64 * m + 32 * h + 16 * hf), 0, 0);
-            },
-            [&](int fs) {
-              if (fs < 8 * (4 - kF2L1Rows)) piece(fs);   // every piece before the first store
-              if (fs == 2 * kBodyKSteps) F2_STAMP(1);
-            });
-        F2_STAMP(2);
-        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // the DMAs (older than the 16 stores) landed
-        F2_STAMP(3);
-      } else {
-#pragma unroll 1
-        for (int i = 0; i < 8 * (4 - kF2L1Rows); ++i) piece(i);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-    }
-    __syncthreads();
-    F2_STAMP(4);
-#ifdef F2_STAMPS
-    st_acc[5] += 1;
-#endif
-    if (++jb == sb) {
-      jb = 0;
-      ++kJ;
-      gpb = gcb;
-      gpx = gcx;
-      gcb = gnb;
-      gcx = gnx;
-      const SGeom g = geom(kJ + 1);
-      gnb = g.b;
-      gnx = g.x0;
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#ifdef F2_STAMPS
-  if (lane == 0 && blockIdx.x < 1024)
-    for (int k = 0; k < 6; ++k) f2_stamp_buf[(blockIdx.x * 4 + wave) * 8 + k] = st_acc[k];
-#endif
-}
-
-template __global__ void conv_body_f2_kernel<0>(const half_t* __restrict__, half_t* __restrict__,
-                                                const uint4* __restrict__, const float* __restrict__,
-                                                const uint4* __restrict__, const float* __restrict__, ConvShape,
-                                                int, int, int);
-template __global__ void conv_body_f2_kernel<1>(const half_t* __restrict__, half_t* __restrict__,
-                                                const uint4* __restrict__, const float* __restrict__,
-                                                const uint4* __restrict__, const float* __restrict__, ConvShape,
-                                                int, int, int);
-#endif  // F2_STREAM_KERNEL
-
-// ------------------------------------------------------------------------------------
-// Body layer with split weights (PNP_PREC_FP16W2): W = W_hi + W_lo, both fp16 (W_lo =
-// fp16(W - W_hi), subnormals kept: the f16 MFMA inputs do not flush them, probed in
-// tools/probes/mfma_f16_denorm.hip), fp16 activations, fp32 accumulation: every product is
-// a * W_hi + a * W_lo in the same accumulator, so the weights carry ~22 significant bits.
-// Why: with fp16-rounded weights the Poisson method's slow primal steps integrate the
-// rounded network's deterministic error (0.19 dB after 3000 iterations of ours-C), while
-// fp16 activations alone stay within 0.001 dB (profiles/r02/precision_drift.txt).
-// Twice the MFMAs of conv_body_v3.  The hi halves stay in registers (144 VGPRs, as in v3);
-// the lo halves of both M-tiles (72 KiB) sit in LDS for the launch, one A-fragment read per
-// K-step; with them the halo ring is 2 deep (2 x 44 KiB: tile t+1's DMA runs during tile t)
-// and the LDS is exactly 160 KiB.  4 waves, one per SIMD: wave w owns channels
-// 32m..32m+31 (m = w & 1) of tile rows 4(w>>1) .. +3 (four N-tiles, 64 accumulators); per
-// K-step 4 B fragments + 1 lo A fragment, 8 MFMAs.  The epilogue stores 2 x 16 B per lane
-// and N-tile straight from registers.
-#ifdef F2_F8_KERNEL   // A/B builds only: the same schedule on 32x32x16 MFMAs
-// ------------------------------------------------------------------------------------
-// conv_body_f8: the f2 schedule (two body layers per launch, strips streamed 8 rows per step,
-// chunk-planar rings, LDS-DMA halo rows) on 8 waves, two per SIMD, so each SIMD carries one
-// layer-l and one layer-l+1 wave (waves w and w+4 share a SIMD) and each hides the other's
-// fragment-read latency, epilogues and DMA issue instead of software pipelining inside one
-// wave.  Wave w: layer w >> 2, M-tile w & 1, half (w >> 1) & 1 of the step's N-tiles:
-//   layer l,   half 0: the strip-halo tile + rows 0-3 (groups {1, 2}, {halo, 0}, {3});
-//   layer l,   half 1: rows 4-7 ({4, 5}, {6, 7});
-//   layer l+1, half h: output rows 4h .. 4h+3 of the step ({0, 1}, {2, 3} + 4h).
-// A group's epilogue follows its K-loop.  256 registers per wave (VGPR + AGPR): 144 for the
-// weights, 2 N-tiles of accumulators per group.  Same K order and roundings as conv_body_v3.
-// ------------------------------------------------------------------------------------
-template <int NT, int PLANE, class Side>
-__device__ __forceinline__ void f8_kloop(const half8_t (&wA)[kBodyKSteps], const unsigned char* ring,
-                                         const int (&ad)[NT][3], floatx16 (&acc)[NT], Side&& side) {
-  auto ldB = [&](int ks, int n) {
-    const int tap = ks >> 2, sub = ks & 3, dy = tap / 3, dx = tap - 3 * dy;
-    return *reinterpret_cast<const half8_t*>(ring + ad[n][dy] + (2 * sub * PLANE + 16 * dx));
-  };
-#ifndef F8_PREFETCH
-#define F8_PREFETCH 2
-#endif
-  constexpr int D = F8_PREFETCH;
-  half8_t fb[D + 1][NT];
-#pragma unroll
-  for (int d = 0; d < D; ++d)
-#pragma unroll
-    for (int n = 0; n < NT; ++n) fb[d][n] = ldB(d, n);
-#pragma unroll
-  for (int ks = 0; ks < kBodyKSteps; ++ks) {
-    if (ks + D < kBodyKSteps) {
-#pragma unroll
-      for (int n = 0; n < NT; ++n) fb[(ks + D) % (D + 1)][n] = ldB(ks + D, n);
-    }
-#pragma unroll
-    for (int n = 0; n < NT; ++n)
-      acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(wA[ks], fb[ks % (D + 1)][n], ks == 0 ? floatx16{} : acc[n],
-                                                      0, 0, 0);
-    side(ks);
-#ifndef F8_NO_SCHED_BARRIER
-    __builtin_amdgcn_sched_barrier(0);
-#endif
-  }
-}
-
-template <int ACT>
-__global__ __launch_bounds__(512, 1) void conv_body_f8_kernel(const half_t* __restrict__ in,
-                                                               half_t* __restrict__ out,
-                                                               const uint4* __restrict__ w1,
-                                                               const float* __restrict__ b1,
-                                                               const uint4* __restrict__ w2,
-                                                               const float* __restrict__ b2, ConvShape s,
-                                                               int strips_x, int nstrips, int sb) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  unsigned char* ring = smem;
-  unsigned char* mid = smem + kF2Mid;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int layer = wave >> 2, m = wave & 1, half = (wave >> 1) & 1;
-  const int h = lane >> 5, col = lane & 31;
-  const uint4* wsrc = layer ? w2 : w1;
-  half8_t wA[kBodyKSteps];
-#pragma unroll
-  for (int ks = 0; ks < kBodyKSteps; ++ks)
-    wA[ks] = *reinterpret_cast<const half8_t*>(reinterpret_cast<const unsigned char*>(wsrc) +
-                                               ((ks * 2 + m) * 64 + lane) * 16);
-  float bl[16];
-#pragma unroll
-  for (int r = 0; r < 16; ++r) bl[r] = (layer ? b2 : b1)[32 * m + 16 * h + r];
-  const unsigned img_bytes = (unsigned)(s.Hp * s.Wp) * 128u;
-
-  const int S = 8 * sb;
-  const int K = (nstrips - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
-  auto geom = [&](int k) {
-    const int st = min(blockIdx.x + k * gridDim.x, (unsigned)nstrips - 1);
-    const int b = st / strips_x;
-    return SGeom{b, (st - b * strips_x) * kTileW};
-  };
-  int kJ = 0, jb = 0;
-  int gpb, gpx, gcb, gcx, gnb, gnx;
-  {
-    const SGeom g0 = geom(0), g1 = geom(1);
-    gpb = gcb = g0.b;
-    gpx = gcx = g0.x0;
-    gnb = g1.b;
-    gnx = g1.x0;
-  }
-  auto pick = [&](int k) {
-    const int pb = gpb, px = gpx, cb = gcb, cx = gcx, nb = gnb, nx = gnx;
-    return SGeom{k > kJ ? nb : (k < kJ ? pb : cb), k > kJ ? nx : (k < kJ ? px : cx)};
-  };
-  auto locate = [&](int R, int kJ, int& k, int& r) {
-    k = kJ;
-    r = R - kJ * S;
-    if (r < 0) { --k; r += S; } else if (r >= S) { ++k; r -= S; }
-  };
-  __amdgpu_buffer_rsrc_t dsrc;
-  unsigned dvo;
-  unsigned char* ddst;
-  auto dma_at = [&](int R, int kJ) {
-    int k, r;
-    locate(R, kJ, k, r);
-    const bool valid = R >= 0 && k < K;
-    const SGeom G = pick(k);
-    dsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(in + (size_t)G.b * s.Hp * s.Wp * kWidth), (short)0,
-                                             valid ? (int)img_bytes : 0, 0x00020000);
-    dvo = (unsigned)(((r + s.pad) * s.Wp + G.x0 + lane) * 128);
-    ddst = ring + f2_slot(R) * (kF2InW * 16);
-  };
-  auto dma_plane = [&](int c) {
-    if (lane < kF2InW)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(dsrc, (__attribute__((address_space(3))) void*)(ddst + c * kF2InPlane),
-                                               16, dvo + 16 * c, 0, 0, 0);
-  };
-  for (int r = wave; r < 10; r += 8) {
-    dma_at(r - 1, 0);
-#pragma unroll 1
-    for (int c = 0; c < 8; ++c) dma_plane(c);
-  }
-  for (int q = tid; q < 8 * kF2MidW; q += 512) {
-    const int c = q / kF2MidW, p = q - c * kF2MidW;
-    *reinterpret_cast<v4i_t*>(mid + c * kF2MidPlane + p * 16) = v4i_t{0, 0, 0, 0};
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
-  for (int J = 0; J <= K * sb; ++J) {
-    // this wave's DMA row of the next step: input row 8J+9+wave, one piece per chunk plane,
-    // issued during the wave's first group
-#ifdef F8_DMA_SKEW
-    // 64 pieces (row, plane): waves on the SIMDs with 8 N-tiles per step (w & 2) take 12,
-    // the others (9 N-tiles) 4
-    const int pcnt = (wave & 2) ? 12 : 4;
-    const int pbeg = (wave & 2) ? 16 + 12 * ((wave & 1) + 2 * (wave >> 2)) : 4 * ((wave & 1) + 2 * (wave >> 2));
-    auto side = [&](int ks) {
-      if ((ks % 3) == 1 && ks / 3 < pcnt) {
-        const int id = pbeg + ks / 3;
-        if (ks / 3 == 0 || (id & 7) == 0) dma_at(8 * J + 9 + (id >> 3), kJ);
-        dma_plane(id & 7);
-      }
-    };
-#else
-    auto side = [&](int ks) {
-      if (ks == 1) dma_at(8 * J + 9 + wave, kJ);
-      if ((ks & 3) == 1 && (ks >> 2) < 8) dma_plane(ks >> 2);
-    };
-#endif
-    auto noside = [](int) {};
-    if (layer == 0) {
-      const int x0 = gcx;
-      if (J < K * sb && 8 * jb < s.H) {
-        int sl = f2_slot(8 * J - 1);
-        int rowoff[10];
-#pragma unroll
-        for (int q = 0; q < 10; ++q) {
-          rowoff[q] = sl * (kF2InW * 16);
-          sl = sl == kF2Ring - 1 ? 0 : sl + 1;
-        }
-        const int hr = (col & 15) >> 1, hc = (col & 1) ? kF2MidW - 1 : 0;
-        // N-tile k: row tile k < 8 (columns 1..32) or the halo tile (k == 8)
-        auto group = [&](auto ntc, int k0, int k1, bool first) {
-          constexpr int NT = decltype(ntc)::value;
-          int ad[NT][3], prow[NT], pcol[NT];
-#pragma unroll
-          for (int n = 0; n < NT; ++n) {
-            const int k = n == 0 ? k0 : k1;
-            prow[n] = k < 8 ? k : hr;
-            pcol[n] = k < 8 ? 1 + col : hc;
-#pragma unroll
-            for (int dy = 0; dy < 3; ++dy) {
-              int ro = rowoff[0];
-#pragma unroll
-              for (int q = 1; q < 10; ++q) ro = prow[n] + dy == q ? rowoff[q] : ro;
-              ad[n][dy] = h * kF2InPlane + ro + pcol[n] * 16;
-            }
-          }
-          floatx16 acc[NT];
-          if (first) f8_kloop<NT, kF2InPlane>(wA, ring, ad, acc, side);
-          else f8_kloop<NT, kF2InPlane>(wA, ring, ad, acc, noside);
-#pragma unroll
-          for (int n = 0; n < NT; ++n) {
-            const int k = n == 0 ? k0 : k1;
-            if (k == 8 && col >= 16) continue;
-            const int pc = pcol[n], pr = prow[n], x = x0 - 1 + pc;
-            const bool inside = 8 * jb + pr < s.H && x >= 0 && x < s.W;
-            half8_t v0 = bias_act8<ACT>(acc[n], 0, bl), v1 = bias_act8<ACT>(acc[n], 8, bl + 8);
-            if (!inside) { v0 = half8_t{}; v1 = half8_t{}; }   // the next layer's zero padding
-            unsigned char* d = mid + (4 * m + 2 * h) * kF2MidPlane + (f2_slot(8 * J + pr) * kF2MidW + pc) * 16;
-            *reinterpret_cast<half8_t*>(d) = v0;
-            *reinterpret_cast<half8_t*>(d + kF2MidPlane) = v1;
-          }
-        };
-        using I1 = std::integral_constant<int, 1>;
-        using I2 = std::integral_constant<int, 2>;
-        if (half == 0) {                                 // (the halo group after the DMA has landed)
-          group(I2{}, 1, 2, true);
-          group(I2{}, 8, 0, false);
-          group(I1{}, 3, 3, false);
-        } else {
-          group(I2{}, 4, 5, true);
-          group(I2{}, 6, 7, false);
-        }
-      } else {
-        // a block below the image (or past the last strip): zero rows 4 half .. 4 half + 3, no MFMAs
-#pragma unroll 1
-        for (int ks = 0; ks < kBodyKSteps; ++ks) side(ks);
-        for (int q = lane; q < 4 * kF2MidW * 4; q += 64) {
-          const int c = q / (4 * kF2MidW), p = q - c * (4 * kF2MidW), rr = p / kF2MidW, pc = p - rr * kF2MidW;
-          *reinterpret_cast<v4i_t*>(mid + (4 * m + c) * kF2MidPlane +
-                                    (f2_slot(8 * J + 4 * half + rr) * kF2MidW + pc) * 16) = v4i_t{0, 0, 0, 0};
-        }
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMAs have landed
-    } else {
-      if (J > 0) {
-        // output rows 8J-9 + 4 half + t, t = 0..3, in two groups of two
-        int sl = f2_slot(8 * J - 10 + 4 * half);
-        int rowoff[6];
-#pragma unroll
-        for (int q = 0; q < 6; ++q) {
-          rowoff[q] = sl * (kF2MidW * 16);
-          sl = sl == kF2Ring - 1 ? 0 : sl + 1;
-        }
-        const int lb = h * kF2MidPlane + col * 16;
-        auto group = [&](int t0, bool first) {
-          int ad[2][3];
-#pragma unroll
-          for (int n = 0; n < 2; ++n)
-#pragma unroll
-            for (int dy = 0; dy < 3; ++dy) ad[n][dy] = lb + rowoff[t0 + n + dy];
-          floatx16 acc[2];
-          if (first) f8_kloop<2, kF2MidPlane>(wA, mid, ad, acc, side);
-          else f8_kloop<2, kF2MidPlane>(wA, mid, ad, acc, noside);
-#pragma unroll
-          for (int n = 0; n < 2; ++n) {
-            const int R = 8 * J - 9 + 4 * half + t0 + n;
-            int k, r;
-            locate(R, kJ, k, r);
-            const bool ok = R >= 0 && k < K && r < s.H;
-            const SGeom G = pick(k);
-            half_t* row = out + (((size_t)G.b * s.Hp + r + s.pad) * s.Wp + G.x0 + s.pad) * kWidth;
-            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-                ok ? (void*)row : (void*)out, (short)0, ok ? min(kTileW, s.W - G.x0) * 128 : 0, 0x00020000);
-            const half8_t v0 = bias_act8<ACT>(acc[n], 0, bl), v1 = bias_act8<ACT>(acc[n], 8, bl + 8);
-            const unsigned off = (unsigned)(col * 128 + 64 * m + 32 * h);
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i_t, v0), rs, off, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i_t, v1), rs, off + 16, 0, 0);
-          }
-        };
-        group(0, true);
-        group(2, false);
-        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // the DMAs (older than the 8 stores) landed
-      } else {
-#pragma unroll 1
-        for (int ks = 0; ks < kBodyKSteps; ++ks) side(ks);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-    }
-    __syncthreads();
-    if (++jb == sb) {
-      jb = 0;
-      ++kJ;
-      gpb = gcb;
-      gpx = gcx;
-      gcb = gnb;
-      gcx = gnx;
-      const SGeom g = geom(kJ + 1);
-      gnb = g.b;
-      gnx = g.x0;
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-template __global__ void conv_body_f8_kernel<0>(const half_t* __restrict__, half_t* __restrict__,
-                                                const uint4* __restrict__, const float* __restrict__,
-                                                const uint4* __restrict__, const float* __restrict__, ConvShape,
-                                                int, int, int);
-template __global__ void conv_body_f8_kernel<1>(const half_t* __restrict__, half_t* __restrict__,
-                                                const uint4* __restrict__, const float* __restrict__,
-                                                const uint4* __restrict__, const float* __restrict__, ConvShape,
-                                                int, int, int);
-#endif  // F2_F8_KERNEL
 
 // ------------------------------------------------------------------------------------
 // conv_body_x8: conv_body_f8's schedule on v_mfma_f32_16x16x32_f16 (MI355X_MICROARCH.md:
@@ -1277,6 +633,20 @@ template __global__ void conv_body_x8_kernel<1>(const half_t* __restrict__, half
                                                 int, int, int);
 
 // ------------------------------------------------------------------------------------
+// Body layer with split weights (PNP_PREC_FP16W2): W = W_hi + W_lo, both fp16 (W_lo =
+// fp16(W - W_hi), subnormals kept: the f16 MFMA inputs do not flush them, probed in
+// tools/probes/mfma_f16_denorm.hip), fp16 activations, fp32 accumulation: every product is
+// a * W_hi + a * W_lo in the same accumulator, so the weights carry ~22 significant bits.
+// Why: with fp16-rounded weights the Poisson method's slow primal steps integrate the
+// rounded network's deterministic error (0.19 dB after 3000 iterations of ours-C), while
+// fp16 activations alone stay within 0.001 dB (profiles/r02/precision_drift.txt).
+// Twice the MFMAs of conv_body_v3.  The hi halves stay in registers (144 VGPRs, as in v3);
+// the lo halves of both M-tiles (72 KiB) sit in LDS for the launch, one A-fragment read per
+// K-step; with them the halo ring is 2 deep (2 x 44 KiB: tile t+1's DMA runs during tile t)
+// and the LDS is exactly 160 KiB.  4 waves, one per SIMD: wave w owns channels
+// 32m..32m+31 (m = w & 1) of tile rows 4(w>>1) .. +3 (four N-tiles, 64 accumulators); per
+// K-step 4 B fragments + 1 lo A fragment, 8 MFMAs.  The epilogue stores 2 x 16 B per lane
+// and N-tile straight from registers.
 constexpr int kW2Halo = 44 * 1024;
 constexpr int kW2Lo = 2 * kW2Halo;
 constexpr int kW2Lds = kW2Lo + kBodyWBytes;                    // 163840 B
@@ -1752,14 +1122,7 @@ hipError_t conv_kernels_init() {
     e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kV3Lds);
     if (e != hipSuccess) return e;
   }
-  for (const void* k : {
-#ifdef F2_STREAM_KERNEL
-           (const void*)conv_body_f2_kernel<0>, (const void*)conv_body_f2_kernel<1>,
-#endif
-#ifdef F2_F8_KERNEL
-           (const void*)conv_body_f8_kernel<0>, (const void*)conv_body_f8_kernel<1>,
-#endif
-           (const void*)conv_body_x8_kernel<0>, (const void*)conv_body_x8_kernel<1>}) {
+  for (const void* k : {(const void*)conv_body_x8_kernel<0>, (const void*)conv_body_x8_kernel<1>}) {
     e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kF2Lds);
     if (e != hipSuccess) return e;
   }
@@ -1788,9 +1151,9 @@ void launch_conv_head(const float* in32, int C, half_t* out, const void* w, cons
 #undef HEAD
 }
 
-// Two body layers per launch: conv_body_x8 (16x16x32 MFMAs, w16_*: pack_body_weights16);
-// A/B builds: -DF2_F8_KERNEL (conv_body_f8, 32x32x16, w32_*) or -DF2_STREAM_KERNEL
-// (conv_body_f2_kernel, one wave per SIMD).
+// Two body layers per launch: conv_body_x8 (16x16x32 MFMAs, w16_*: pack_body_weights16).
+// (The round-2 A/B variants on 32x32x16 fragments, w32_*: conv_body_f2 / conv_body_f8, are in
+// git history before round 3; DESIGN.md §3 keeps their measurements.)
 void launch_conv_body_f2(const half_t* in, half_t* out, const void* w16_1, const void* w16_2, const void* w32_1,
                          const void* w32_2, const float* b1, const float* b2, const ConvShape& s, int act,
                          int num_cus, hipStream_t st) {
@@ -1800,16 +1163,8 @@ void launch_conv_body_f2(const half_t* in, half_t* out, const void* w16_1, const
 #define F2_LAUNCH(KERN, NT, W1, W2)                                                                              \
   hipLaunchKernelGGL((KERN), dim3(grid), dim3(NT), kF2Lds, st, in, out, (const uint4*)(W1), b1, (const uint4*)(W2), \
                      b2, s, strips_x, nstrips, sb)
-#if defined(F2_STREAM_KERNEL)
-  if (act == 0) F2_LAUNCH(conv_body_f2_kernel<0>, 256, w32_1, w32_2);
-  else F2_LAUNCH(conv_body_f2_kernel<1>, 256, w32_1, w32_2);
-#elif defined(F2_F8_KERNEL)
-  if (act == 0) F2_LAUNCH(conv_body_f8_kernel<0>, 512, w32_1, w32_2);
-  else F2_LAUNCH(conv_body_f8_kernel<1>, 512, w32_1, w32_2);
-#else
   if (act == 0) F2_LAUNCH(conv_body_x8_kernel<0>, 512, w16_1, w16_2);
   else F2_LAUNCH(conv_body_x8_kernel<1>, 512, w16_1, w16_2);
-#endif
 #undef F2_LAUNCH
   (void)w16_1; (void)w16_2; (void)w32_1; (void)w32_2;
 }
@@ -1860,10 +1215,3 @@ void launch_conv_tail(const half_t* in, const float* xin, float* xout, const voi
 }
 
 }  // namespace pnp
-
-#ifdef F2_STAMPS
-extern "C" int pnp_diag_f2_stamps(unsigned long long* host, int n) {
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(pnp::f2_stamp_buf), (size_t)n * sizeof(unsigned long long), 0,
-                             hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
-}
-#endif

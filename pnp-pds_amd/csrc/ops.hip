@@ -907,37 +907,15 @@ __device__ __forceinline__ void rb_gather(int i0, int j0, int H, int W, F&& load
   }
 }
 
-// Halo fill: batches of kRbFill elements per thread (the loads of a batch in flight
-// together, then their LDS stores), so few registers are live and 6 blocks fit per CU.  val(a, b) combines the values of the two source
-// planes (b is unused for one-plane fills).
-#ifndef PNP_RB_FILL
-#define PNP_RB_FILL 8        // A/B builds only
-#endif
-constexpr int kRbFill = PNP_RB_FILL;
-template <class G, int K0, class FA, class FB, class FV>
-__device__ __forceinline__ void rb_fill_batch(float* lds, int i0, int j0, int H, int W, FA&& la, FB&& lb, FV&& val) {
-  constexpr int K1 = K0 + kRbFill < G::NF ? K0 + kRbFill : G::NF;
-  float a[kRbFill], b[kRbFill];
-  rb_gather<G, K0, K1>(i0, j0, H, W, [&](int k, int idx) {
-    a[k] = la(idx);
-    b[k] = lb(idx);
-  });
-#pragma unroll
-  for (int k = K0; k < K1; ++k) {
-    const int q = threadIdx.x + 256 * k;
-    if (G::N % 256 == 0 || q < G::N) lds[q] = val(a[k - K0], b[k - K0]);
-  }
-  if constexpr (K1 < G::NF) rb_fill_batch<G, K1>(lds, i0, j0, H, W, la, lb, val);
-}
+// Halo fills: batches of kRbFill elements per thread (the loads of a batch in flight
+// together, then their LDS stores), so few registers are live and 6 blocks fit per CU.
+constexpr int kRbFill = 8;
 
 // Column-wise halo fill (K1): thread t < TPC LW owns LDS column t % LW and rows t / LW +
 // TPC i, so the column's wrap is resolved once and each row step is an add and one
 // conditional wrap (the element-wise gather above re-derives row and column and wraps both
 // for every element).  Loads in batches of kRbFill rows, then their LDS stores.
-#ifndef PNP_RB1_FILL
-#define PNP_RB1_FILL 8       // A/B builds only
-#endif
-template <class G, int NB = PNP_RB1_FILL, class FA>
+template <class G, int NB = kRbFill, class FA>
 __device__ __forceinline__ void rb_fill_cols(float* lds, int i0, int j0, int H, int W, FA&& la) {
   constexpr int TPC = 256 / G::LW;                   // threads per column (row stride)
   constexpr int NI = (G::LH + TPC - 1) / TPC;        // rows per thread (the last may be past LH)
@@ -1038,22 +1016,10 @@ __global__ __launch_bounds__(256) void k1_blur_rb(const float* __restrict__ x, c
   RbRows rw;
   rw.init(pb, i0, j, H, W);
   const float* yp = y + pb;
-#ifndef K1_ABL_FILL   // diagnostic builds only (results wrong)
-#ifdef K1_FILL_ELEM
-  rb_fill_batch<G, 0>(lds, i0, j0, H, W, [&](int k) { return yp[k]; }, [](int) { return 0.f; },
-                      [](float a, float) { return a; });
-#else
   rb_fill_cols<G>(lds, i0, j0, H, W, [&](int k) { return yp[k]; });
-#endif
-#endif
   __syncthreads();
   f2_t g[kRbRows];
-#ifndef K1_ABL_STENCIL
   rb_stencil<T>(lds, wd_adj, g);
-#else
-#pragma unroll
-  for (int r = 0; r < kRbRows; ++r) g[r] = f2_t{lds[threadIdx.x + r], 0.f};
-#endif
   const float* yc = lds + (ty * kRbRows + G::R) * G::LW + 2 * tx + G::R - G::kOff;   // y at (row 0, col j)
 #pragma unroll
   for (int rb = 0; rb < kRbRows; rb += kRb1Batch) {   // the loads of kRb1Batch rows in flight together
@@ -1173,67 +1139,6 @@ __device__ __forceinline__ void rb_fill_k2(float* lds, int i0, int j0, int H, in
   if constexpr (K1 < G::NF) rb_fill_k2<G, K1>(lds, i0, j0, H, W, xnp, xop, xtp, record, e2, n2, t2, lo, hi);
 }
 
-// Column-wise form of rb_fill_k2 (see rb_fill_cols): the column's wrap and "inside the tile"
-// test are resolved once per thread, the rows stepped.
-template <class G>
-__device__ __forceinline__ void rb_fill_k2_cols(float* lds, int i0, int j0, int H, int W, const float* xnp,
-                                                const float* xop, const float* xtp, bool record, double& e2,
-                                                double& n2, double& t2, float& lo, float& hi) {
-  constexpr int TPC = 256 / G::LW;
-  constexpr int NI = (G::LH + TPC - 1) / TPC;
-  const int tid = threadIdx.x;
-  if (tid >= TPC * G::LW) return;
-  const int lx = tid % G::LW, ly0 = tid / G::LW;
-  const int uj = j0 - G::R + G::kOff + lx;              // unwrapped column
-  int gj = uj;
-  gj += gj < 0 ? W : 0;
-  gj -= gj >= W ? W : 0;
-  gj = min(max(gj, 0), W - 1);
-  const bool colin = record && uj >= j0 && uj < min(j0 + kRbW, W);
-  const int ie = min(i0 + kRbH, H);
-  int ui = i0 - G::R + ly0;                             // unwrapped row
-  int gi = ui;
-  gi += gi < 0 ? H : 0;
-  gi -= gi >= H ? H : 0;
-#pragma unroll
-  for (int i0b = 0; i0b < NI; i0b += kRbFill) {
-    float a[kRbFill], bb[kRbFill], t[kRbFill];
-    bool in[kRbFill];
-#pragma unroll
-    for (int i = 0; i < kRbFill; ++i) {
-      if (i0b + i < NI) {
-        const int idx = min(max(gi, 0), H - 1) * W + gj;
-        a[i] = xnp[idx];
-        bb[i] = xop[idx];
-        in[i] = colin && ui >= i0 && ui < ie && (G::LH % TPC == 0 || ly0 + TPC * (i0b + i) < G::LH);
-        t[i] = (in[i] && xtp) ? xtp[idx] : 0.f;
-        ui += TPC;
-        gi += TPC;
-        gi -= gi >= H ? H : 0;
-      }
-    }
-    float be = 0.f, bn = 0.f, bt = 0.f;
-#pragma unroll
-    for (int i = 0; i < kRbFill; ++i) {
-      if (i0b + i < NI) {
-        const int ly = ly0 + TPC * (i0b + i);
-        const float av = a[i], bv = bb[i];
-        if (G::LH % TPC == 0 || ly < G::LH) lds[ly * G::LW + lx] = 2.f * av - bv;
-        const float d = in[i] ? av - bv : 0.f, o = in[i] ? bv : 0.f;
-        const float tt = in[i] ? t[i] - av : 0.f;
-        be = fmaf(d, d, be);
-        bn = fmaf(o, o, bn);
-        bt = fmaf(tt, tt, bt);
-        lo = in[i] ? fminf(lo, av) : lo;
-        hi = in[i] ? fmaxf(hi, av) : hi;
-      }
-    }
-    e2 += be;
-    n2 += bn;
-    t2 += bt;
-  }
-}
-
 // K2: v = y + g2 (Phi(2x+ - x) [+ 2 s+ - s]), s+ = shrink(w, theta) (B), the GKL prox (C),
 // per-cell partial sums.  Block = one (plane, 64 x 64 tile).  The metric sums come from the
 // fill's own loads of xn / xo (plus x_true for the tile's pixels) and are reduced before the
@@ -1268,13 +1173,8 @@ __global__ __launch_bounds__(256) void k2_blur_rb(const float* __restrict__ xn, 
   {
     double e2 = 0, n2 = 0, t2 = 0;
     float lo = __builtin_inff(), hi = -__builtin_inff();
-#ifdef K2_FILL_COLS   // measured 0.30 vs 0.28 ms (more live registers per batch): kept for A/B only
-    rb_fill_k2_cols<G>(lds, i0, j0, H, W, xn + (size_t)bc * plane, xo + (size_t)bc * plane,
-                       xtrue ? xtrue + (size_t)bc * plane : nullptr, record != 0, e2, n2, t2, lo, hi);
-#else
     rb_fill_k2<G>(lds, i0, j0, H, W, xn + (size_t)bc * plane, xo + (size_t)bc * plane,
                   xtrue ? xtrue + (size_t)bc * plane : nullptr, record != 0, e2, n2, t2, lo, hi);
-#endif
     if (record) {                            // reduced here, so no fill value stays live past the fill
       e2 = wave_sum(e2);
       n2 = wave_sum(n2);

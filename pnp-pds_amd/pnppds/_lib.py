@@ -190,6 +190,7 @@ class Context:
         self.h = h
         self._denoiser_key = None
         self._operator_key = None
+        self.precision = PRECISIONS["fp16"]   # the library's default (pnp_set_precision)
 
     # -- plumbing --
     def _check(self, rc):
@@ -227,6 +228,7 @@ class Context:
         precision, models/denoiser.py:37; about a tenth of the throughput)."""
         code = PRECISIONS[precision] if isinstance(precision, str) else int(precision)
         self._check(self.lib.pnp_set_precision(self.h, code))
+        self.precision = code
 
     def set_denoise_chunk(self, images: int):
         """Images per denoiser pass (0 = auto).  Performance only."""

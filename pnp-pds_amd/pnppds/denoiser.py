@@ -31,11 +31,16 @@ class Denoiser:
         B, Cc, H, W = x.shape
         ctx = get_ctx()
         self.configure(ctx)
+        prev = ctx.precision               # this call's precision only: the shared context keeps its own
         ctx.set_precision(self.precision)
-        dx = to_device(x)
-        dy = to_device(np.empty(x.shape, np.float32))
-        ctx.op_denoise(dx.data_ptr(), dy.data_ptr(), B, Cc, H, W)
-        return from_device(dy, ctx)
+        try:
+            dx = to_device(x)
+            dy = to_device(np.empty(x.shape, np.float32))
+            ctx.op_denoise(dx.data_ptr(), dy.data_ptr(), B, Cc, H, W)
+            return from_device(dy, ctx)
+        finally:
+            if prev != ctx.precision:
+                ctx.set_precision(prev)
 
     def denoise(self, x):
         x = np.asarray(x)

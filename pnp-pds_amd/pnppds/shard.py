@@ -53,8 +53,11 @@ def test_iter_sharded(x_0, x_obsrv, x_true, *args, runner=None, gather="rank0", 
     may be shared (C, H, W) arrays, broadcast to every image as in test_iter_batch.
 
     gather="rank0" (default): rank 0 returns the whole batch's results, the other ranks
-    None (one gather to one host: at cfg5 the whole batch's x and s are 13 GB, which must
-    not be replicated on every rank).  gather="none": every rank returns
+    **None** (one gather to one host, so the results are not replicated on every rank).
+    Peak host memory on rank 0: gather_object pickles every shard, so rank 0 holds the
+    world's pickled shards plus the concatenated result, about 2-3x the batch's result bytes
+    (cfg5, 512 x RGB 1024^2: x and s are 13 GB, so up to ~40 GB on rank 0).  For batches of
+    that size use gather="none" and write each shard from its own rank.  gather="none": every rank returns
     (its shard's results, (lo, hi)) and nothing crosses ranks.  `runner` defaults to
     pnppds.iteration.test_iter_batch (the device solver); tests substitute the CPU oracle
     to check the sharding alone."""

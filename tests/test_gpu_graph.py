@@ -80,3 +80,46 @@ def test_denoise_passes_same_bits():
         got = ctx.run(m, prm, x0, xo, xt, 4)
         for a, b in zip(ref[:5], got[:5]):
             np.testing.assert_array_equal(a, b)
+
+
+def test_op_denoise_between_graph_replays_fp32():
+    """pnp_op_denoise at fp32 on another image size between two graph-replayed
+    solver_iterate calls (ours-C, fp32 operands) must not disturb the solver's fp32 activation
+    borders: the single op has its own scratch pair, so the replay gives the direct bits."""
+    import torch
+    ctx, m, prm, x0, xo, xt = _setup("C_rs", 1)
+    B, Cc, H, W = x0.shape
+    xs = torch.rand(2, Cc, H + 24, W + 8, device="cuda")
+    ys = torch.empty_like(xs)
+    out = {}
+    for mode in (0, 1):
+        ctx.set_graph(mode)
+        ctx.solver_setup(m, prm, B, Cc, H, W, 8)
+        ctx.solver_load(x0, xo, xt)
+        ctx.solver_iterate(4)
+        ctx.op_denoise(xs.data_ptr(), ys.data_ptr(), 2, Cc, H + 24, W + 8)
+        ctx.solver_iterate(4)
+        out[mode] = ctx.solver_fetch()
+    for a, b in zip(out[0], out[1]):
+        np.testing.assert_array_equal(a, b)
+
+
+def test_op_l1_ball_side_stream_fresh_context():
+    """on a fresh context pnp_op_proj_l1_ball on a caller stream zeroes its own
+    histogram scratch on that stream (not on the context's stream), so the first call is right."""
+    import torch
+    from oracle import pnp_oracle as O
+    from pnppds import _lib
+    rng = np.random.default_rng(5)
+    v = rng.standard_normal((3, 3 * 64 * 64)).astype(np.float32) * 0.1
+    want = np.stack([O.proj_l1_ball(v[b].astype(np.float64), 0.95, 0.1, 0.8) for b in range(3)])
+    s = torch.cuda.Stream()
+    for _ in range(3):
+        ctx = _lib.Context(0)
+        dv = torch.from_numpy(v).cuda()
+        do = torch.empty_like(dv)
+        torch.cuda.synchronize()
+        ctx.op_proj_l1_ball(dv.data_ptr(), do.data_ptr(), 3, v.shape[1], 0.95, 0.1, 0.8, stream=s.cuda_stream)
+        s.synchronize()
+        np.testing.assert_allclose(do.cpu().numpy(), want, atol=2e-6)
+        ctx.close()
