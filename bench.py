@@ -110,7 +110,7 @@ def synthetic_batch(B, C, H, W, seed):
     return out
 
 
-def images_per_launch(B, H, W, chunk, fp32=False):
+def images_per_launch(B, H, W, chunk, fp32=False, x3=False):
     """Mirror of capi.hip denoise_chunk() / split_passes(): mean images per conv launch (the
     activation budget is an eighth of the card's HBM; the batch is split into equal passes)."""
     if chunk > 0:
@@ -118,7 +118,7 @@ def images_per_launch(B, H, W, chunk, fp32=False):
     else:
         import torch
         budget = torch.cuda.get_device_properties(0).total_memory / 8
-        per_img = 2.0 * (H + 2) * (W + 2) * 64 * 4 if fp32 else 2.0 * (H + 4) * (W + 4) * 64 * 2
+        per_img = 2.0 * (H + 2) * (W + 2) * 64 * 4 if fp32 else (4.0 if x3 else 2.0) * (H + 4) * (W + 4) * 64 * 2
         m = max(1, min(int(budget // per_img), B))
     passes = -(-B // m)
     return B / passes
@@ -249,7 +249,7 @@ def main():
     ap.add_argument("--size", type=int, default=0, help="image side (0 = the config's)")
     ap.add_argument("--op", default="", choices=["", "blur", "Id", "random_sampling"],
                     help="override the config's degradation operator (profiling the elementwise K1/K2)")
-    ap.add_argument("--precision", default="auto", choices=["auto", "fp16", "fp16w2", "fp32"],
+    ap.add_argument("--precision", default="auto", choices=["auto", "fp16", "fp16w2", "fp16x3", "fp32"],
                     help="denoiser operands: auto = the solver's policy (fp32 for the Poisson methods, "
                          "fp16 otherwise; pnppds.iteration.FP32_METHODS)")
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU-baseline work")
@@ -360,6 +360,7 @@ def main():
             "ms_per_step": round(1e3 * t_el / K, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None,
             "dtype": {"fp16": "fp16-mfma/fp32-acc+state", "fp16w2": "fp16-mfma(split fp16 hi+lo weights)/fp32-acc+state",
+                      "fp16x3": "fp16-mfma(split fp16 hi+lo activations and weights, 3 MFMAs)/fp32-acc+state",
                       "fp32": "fp32-mfma/fp32-state"}[args.precision],
             "data": f"synthetic structured images, x_obs from the device observation pipeline (main.py:49-64: "
                     f"{cfg['op']}, sigma={cfg['sigma']}, sp={cfg['sp']}, poisson={cfg['poisson']}, "
@@ -376,12 +377,13 @@ def main():
             line["kernel_ms"] = kt
             line["kernel_calls_per_step"] = {k: round(v[1] / K, 2) for k, v in prof.items()}
             fp32 = args.precision == "fp32"
-            kname = {"fp32": "conv32_body", "fp16w2": "conv_body_w2"}.get(args.precision, "conv_body")
+            kname = {"fp32": "conv32_body", "fp16w2": "conv_body_w2", "fp16x3": "conv_body_s3"}.get(args.precision,
+                                                                                                  "conv_body")
             if kname == "conv_body" and "conv_body_f2" in prof:
                 kname = "conv_body_f2"
             if kname in prof:
                 body_ms = prof[kname][0]
-                m = images_per_launch(B, H, W, args.chunk, fp32)
+                m = images_per_launch(B, H, W, args.chunk, fp32, args.precision == "fp16x3")
                 fl = conv_flops_per_launch(m, H, W)
                 by = conv_bytes_per_launch(m, H, W, 4 if fp32 else 2)
                 gbs = by / (body_ms * 1e-3) / 1e9
@@ -392,6 +394,15 @@ def main():
                                         "achieved": round(tfl, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                                         "frac": round(tfl / FP32_PEAK_TFLOPS, 4), "traffic": None,
                                         "bytes_per_launch": by, "flops_per_launch": fl, "hbm_gbs": round(gbs, 1)}
+                elif args.precision == "fp16x3":   # 3 MFMAs per product on hi + lo activations: MFMA roof
+                    by = 2 * by                    # hi + lo images read and written
+                    gbs = by / (body_ms * 1e-3) / 1e9
+                    line["roofline"] = {"kernel": "conv_body_s3 (64->64 3x3, split fp16: 3 fp16 MFMAs per product)",
+                                        "bound": "mfma", "achieved": round(3 * tfl, 1), "peak": FP16_PEAK_TFLOPS,
+                                        "unit": "TFLOP/s (MFMA work, 3x algorithmic)",
+                                        "frac": round(3 * tfl / FP16_PEAK_TFLOPS, 4), "traffic": None,
+                                        "bytes_per_launch": by, "flops_per_launch": fl, "hbm_gbs": round(gbs, 1),
+                                        "algorithmic_tflops": round(tfl, 1)}
                 elif args.precision == "fp16w2":   # 2 MFMAs per product: 576 MFMA-FLOP/B, MFMA roof
                     line["roofline"] = {"kernel": "conv_body_w2 (64->64 3x3, fp16 MFMA, split hi+lo weights)",
                                         "bound": "mfma", "achieved": round(2 * tfl, 1), "peak": FP16_PEAK_TFLOPS,

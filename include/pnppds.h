@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define PNP_ABI_VERSION 3
+#define PNP_ABI_VERSION 4
 
 typedef struct pnp_ctx pnp_ctx;
 
@@ -84,8 +84,12 @@ enum pnp_precision {
   PNP_PREC_FP32 = 1, /* fp32 operands and accumulation (v_mfma_f32_32x32x2_f32): the
                         reference denoiser's own precision (models/denoiser.py:37), the
                         parity fallback; about 1/10 of the fp16 path's throughput     */
-  PNP_PREC_FP16W2 = 2 /* fp16 activations, weights split into fp16 hi + lo halves (two
+  PNP_PREC_FP16W2 = 2,/* fp16 activations, weights split into fp16 hi + lo halves (two
                         MFMAs per product, ~22-bit weights), fp32 accumulation         */
+  PNP_PREC_FP16X3 = 3 /* activations and weights both split into fp16 hi + lo halves,
+                        three fp16 MFMAs per product (hi*hi + hi*lo + lo*hi), fp32
+                        accumulation: near-fp32 results at 1/3 of the fp16 MFMA rate
+                        (ABI 4)                                                      */
 };
 
 /* Scalar parameters of iteration.test_iter (iteration.py:10), same names/meaning. */

@@ -56,7 +56,8 @@ struct pnp_ctx {
   DevBuf head_w, head_b, body_w, body_b, tail_w, tail_b;
   DevBuf body_w16;                       // 16x16x32 MFMA fragments of the body layers (conv_body_x8)
   DevBuf head_w32, body_w32, tail_w32;   // fp32 MFMA fragments (PNP_PREC_FP32)
-  DevBuf head_wlo, body_wlo, tail_wlo;   // fp16 low halves W - fp16(W) (PNP_PREC_FP16W2)
+  DevBuf head_wlo, body_wlo, tail_wlo;   // fp16 low halves W - fp16(W) (PNP_PREC_FP16W2 / FP16X3)
+  DevBuf body_s3h, body_s3l;             // conv_s3 body fragments, hi / lo (PNP_PREC_FP16X3)
 
   // operator
   int op_kind = PNP_OP_ID;
@@ -70,6 +71,7 @@ struct pnp_ctx {
   pnp_params prm{};
   int cur = 0;
   DevBuf x[2], y, s, w, xobs, xtrue, u32, act[2], partials, metrics, theta;
+  DevBuf act_lo[2]; // low halves of the hidden activations (PNP_PREC_FP16X3)
   DevBuf z, p, t;   // comparisonB-2 and the other comparison methods
   DevBuf y1, d, c1; // TV dual [B][2C][H][W]; Poisson-ADMM d and Phi^T 1
   DevBuf ssim_scr;  // SSIM partials (record_ssim)
@@ -81,7 +83,7 @@ struct pnp_ctx {
   uint32_t dg_seed = 0;
 
   // scratch for single ops
-  DevBuf scr_u32, scr_act[2], scr_part, scr_theta;
+  DevBuf scr_u32, scr_act[2], scr_act_lo[2], scr_part, scr_theta;
   DevBuf act32[2];   // fp32 hidden activations (PNP_PREC_FP32) of the solver
   DevBuf l1_scr;     // l1-ball select histograms + per-image state (launch_l1_select) of the solver
   // the stream-parameterised single ops (pnp_op_*) keep their own stateful scratch, so they never
@@ -287,7 +289,8 @@ int split_passes(int B, double per_img, double budget) {
 
 int denoise_chunk(pnp_ctx* ctx, int B, int H, int W) {
   if (ctx->den_chunk > 0) return std::min(ctx->den_chunk, B);
-  const double per_img = 2.0 * (H + 2 * kActPad) * (W + 2 * kActPad) * kWidth * sizeof(half_t);
+  const double planes = ctx->prec == PNP_PREC_FP16X3 ? 4.0 : 2.0;   // X3: hi + lo ping-pong pairs
+  const double per_img = planes * (H + 2 * kActPad) * (W + 2 * kActPad) * kWidth * sizeof(half_t);
   return split_passes(B, per_img, ctx->act_budget);
 }
 
@@ -345,6 +348,38 @@ void run_denoiser(pnp_ctx* ctx, const float* u32, float* xout, DevBuf (&act)[2],
   const int m = denoise_chunk(ctx, B, H, W);
   ensure_act(ctx, act, m, H, W, st);
   const int C = ctx->den_C;
+  if (ctx->prec == PNP_PREC_FP16X3) {          // split fp16 (conv_s3.hip): hi images in act, lo in act_lo
+    DevBuf(&alo)[2] = &act[0] == &ctx->act[0] ? ctx->act_lo : ctx->scr_act_lo;
+    ensure_act(ctx, alo, m, H, W, st);
+    for (int b0 = 0; b0 < B; b0 += m) {
+      const int mb = std::min(m, B - b0);
+      ConvShape s = make_conv_shape(mb, H, W);
+      const float* xin = u32 + (size_t)b0 * C * H * W;
+      float* xo = xout + (size_t)b0 * C * H * W;
+      {
+        ProfScope ps(ctx, "conv_head", st);
+        launch_conv_head(xin, C, P<half_t>(act[0]), ctx->head_w.p, ctx->head_wlo.p, P<float>(ctx->head_b), s,
+                         ctx->den_act, ctx->num_cus, 4, st, P<half_t>(alo[0]));
+        check_launch(ctx, "conv_head");
+      }
+      int cur = 0;
+      for (int l = 0; l < ctx->den_depth - 2; ++l, cur ^= 1) {
+        ProfScope ps(ctx, "conv_body_s3", st);
+        launch_conv_s3_body(P<half_t>(act[cur]), P<half_t>(alo[cur]), P<half_t>(act[cur ^ 1]), P<half_t>(alo[cur ^ 1]),
+                            (const char*)ctx->body_s3h.p + (size_t)l * kBodyWBytes,
+                            (const char*)ctx->body_s3l.p + (size_t)l * kBodyWBytes, P<float>(ctx->body_b) + l * kWidth,
+                            s, ctx->den_act, ctx->num_cus, st);
+        check_launch(ctx, "conv_body_s3");
+      }
+      {
+        ProfScope ps(ctx, "conv_tail_s3", st);
+        launch_conv_s3_tail(P<half_t>(act[cur]), P<half_t>(alo[cur]), xin, xo, ctx->tail_w.p, ctx->tail_wlo.p,
+                            P<float>(ctx->tail_b), s, C, ctx->den_residual, ctx->den_clamp, ctx->num_cus, st);
+        check_launch(ctx, "conv_tail_s3");
+      }
+    }
+    return;
+  }
   for (int b0 = 0; b0 < B; b0 += m) {
     const int mb = std::min(m, B - b0);
     ConvShape s = make_conv_shape(mb, H, W);
@@ -918,6 +953,7 @@ int pnp_create(int device, pnp_ctx** out) {
       HIPCHK(ctx, hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
       HIPCHK(ctx, conv_kernels_init());
       HIPCHK(ctx, conv32_kernels_init());
+      HIPCHK(ctx, conv_s3_kernels_init());
     } catch (const PnpError&) {
       g_thread_err = ctx->err;
       delete ctx;
@@ -936,6 +972,7 @@ int pnp_destroy(pnp_ctx* ctx) {
                     &ctx->w, &ctx->xobs, &ctx->xtrue, &ctx->u32, &ctx->act[0], &ctx->act[1],
                     &ctx->partials, &ctx->metrics, &ctx->theta, &ctx->scr_u32,
                     &ctx->scr_act[0], &ctx->scr_act[1], &ctx->scr_part, &ctx->scr_theta,
+                    &ctx->act_lo[0], &ctx->act_lo[1], &ctx->scr_act_lo[0], &ctx->scr_act_lo[1], &ctx->body_s3h, &ctx->body_s3l,
                     &ctx->z, &ctx->p, &ctx->t, &ctx->dense_fwd, &ctx->dense_adj, &ctx->ssim_scr,
                     &ctx->taps64, &ctx->y1, &ctx->d, &ctx->c1, &ctx->dg_words, &ctx->dg_flag, &ctx->dg_rank, &ctx->dg_scan, &ctx->dg_noise,
                     &ctx->dg_img, &ctx->dg_draws, &ctx->dg_first, &ctx->dg_status,
@@ -988,7 +1025,8 @@ int pnp_set_tuning(pnp_ctx* ctx, int key, int value) {
 int pnp_set_precision(pnp_ctx* ctx, int precision) {
   if (!ctx) return PNP_E_ARG;
   return guarded(ctx, [&] {
-    if (precision != PNP_PREC_FP16 && precision != PNP_PREC_FP32 && precision != PNP_PREC_FP16W2)
+    if (precision != PNP_PREC_FP16 && precision != PNP_PREC_FP32 && precision != PNP_PREC_FP16W2 &&
+        precision != PNP_PREC_FP16X3)
       fail(ctx, PNP_E_UNSUPPORTED, "precision %d not supported", precision);
     if (ctx->prec != precision) ctx->gen++;   // a captured graph holds the other precision's kernels
     ctx->prec = precision;
@@ -1038,6 +1076,14 @@ int pnp_set_denoiser(pnp_ctx* ctx, int channels, int depth, int width, const flo
       for (int l = 0; l < depth - 2; ++l, q += n_body)
         pack_body_weights(lo_of(q, (size_t)kWidth * kWidth * 9).data(), bl.data() + (size_t)l * kBodyWBytes / 2);
       pack_tail_weights(lo_of(q, (size_t)channels * kWidth * 9).data(), channels, tl.data());
+      std::vector<uint16_t> sh(bw.size()), sl(bw.size());   // conv_s3 body fragments (PNP_PREC_FP16X3)
+      q = params + n_head;
+      for (int l = 0; l < depth - 2; ++l, q += n_body)
+        pack_body_weights_s3(q, sh.data() + (size_t)l * kBodyWBytes / 2, sl.data() + (size_t)l * kBodyWBytes / 2);
+      ensure(ctx, ctx->body_s3h, sh.size() * 2);
+      ensure(ctx, ctx->body_s3l, sl.size() * 2);
+      HIPCHK(ctx, hipMemcpy(ctx->body_s3h.p, sh.data(), sh.size() * 2, hipMemcpyHostToDevice));
+      HIPCHK(ctx, hipMemcpy(ctx->body_s3l.p, sl.data(), sl.size() * 2, hipMemcpyHostToDevice));
       ensure(ctx, ctx->head_wlo, hl.size() * 2);
       ensure(ctx, ctx->body_wlo, bl.size() * 2);
       ensure(ctx, ctx->tail_wlo, tl.size() * 2);

@@ -749,18 +749,24 @@ template __global__ void conv_body_w2_kernel<1>(const half_t* __restrict__, half
 // past C and pixels outside the image 0 = the conv's zero padding).  K = 9 taps x 4
 // channels = 36, padded to 48 = 3 K-steps of 16: k = 4*tap + ch.
 // ------------------------------------------------------------------------------------
-// W2: split weights (W_hi + W_lo, PNP_PREC_FP16W2), two MFMAs per product.  NC = C when it
-// is a compile-time 1 or 3, 0 = runtime C <= kMaxC (channel index clamped, extra lanes 0).
-template <bool W2, int NC>
+// PREC 1: split weights (W_hi + W_lo, PNP_PREC_FP16W2), two MFMAs per product.  PREC 2
+// (PNP_PREC_FP16X3): the input is split as well (x_hi + x_lo fp16), three MFMAs per product
+// (x_hi W_hi + x_hi W_lo + x_lo W_hi), and the output is written as hi (out) + lo (out_lo)
+// images for conv_s3.hip.  NC = C when it is a compile-time 1 or 3, 0 = runtime C <= kMaxC
+// (channel index clamped, extra lanes 0).
+template <int PREC, int NC>
 __global__ __launch_bounds__(256) void conv_head_kernel(const float* __restrict__ in32, int Crt,
                                                          half_t* __restrict__ out,
+                                                         half_t* __restrict__ out_lo,
                                                          const uint4* __restrict__ wpk,
                                                          const uint4* __restrict__ wpk_lo,
                                                          const float* __restrict__ bias,
                                                          ConvShape s, int act) {
+  constexpr bool W2 = PREC >= 1, X3 = PREC == 2;
   __shared__ __attribute__((aligned(16))) unsigned char wl[kHeadWBytes];
   __shared__ __attribute__((aligned(16))) unsigned char wll[W2 ? kHeadWBytes : 16];
   __shared__ __attribute__((aligned(16))) uint2 hl[kHaloPix];
+  __shared__ __attribute__((aligned(16))) uint2 hlo[X3 ? kHaloPix : 1];
   __shared__ __attribute__((aligned(16))) unsigned char stg_all[4 * 8192];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   unsigned char* stg = stg_all + wave * 8192;
@@ -796,10 +802,14 @@ __global__ __launch_bounds__(256) void conv_head_kernel(const float* __restrict_
       for (int c = 0; c < CM; ++c) pre[k][c] = base[(size_t)(NC ? c : min(c, C - 1)) * plane + o];
     }
   };
-  auto quad = [&](int k) {
+  auto quad = [&](int k, bool lo) {           // lo: the low halves x - fp16(x)
     _Float16 h[4];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) h[c] = (c < CM && (NC || c < C) && pin[k]) ? (_Float16)pre[k][c < CM ? c : 0] : (_Float16)0;
+    for (int c = 0; c < 4; ++c) {
+      const float v = pre[k][c < CM ? c : 0];
+      const _Float16 vh = (_Float16)v;
+      h[c] = (c < CM && (NC || c < C) && pin[k]) ? (lo ? (_Float16)(v - (float)vh) : vh) : (_Float16)0;
+    }
     return make_uint2((uint32_t)__builtin_bit_cast(uint16_t, h[0]) | ((uint32_t)__builtin_bit_cast(uint16_t, h[1]) << 16),
                       (uint32_t)__builtin_bit_cast(uint16_t, h[2]) | ((uint32_t)__builtin_bit_cast(uint16_t, h[3]) << 16));
   };
@@ -810,7 +820,10 @@ __global__ __launch_bounds__(256) void conv_head_kernel(const float* __restrict_
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < 2; ++k)
-      if (tid + 256 * k < kHaloPix) hl[tid + 256 * k] = quad(k);
+      if (tid + 256 * k < kHaloPix) {
+        hl[tid + 256 * k] = quad(k, false);
+        if (X3) hlo[tid + 256 * k] = quad(k, true);
+      }
     __syncthreads();
     load_halo(t + gridDim.x);
     floatx16 acc00 = {}, acc01 = {}, acc10 = {}, acc11 = {};
@@ -826,6 +839,20 @@ __global__ __launch_bounds__(256) void conv_head_kernel(const float* __restrict_
         if (t0 + 1 < 9) q1 = hl[(2 * wave + n + (t0 + 1) / 3) * kHaloW + col + (t0 + 1) % 3];
         uint4 q = make_uint4(q0.x, q0.y, q1.x, q1.y);
         const half8_t bf = *reinterpret_cast<const half8_t*>(&q);
+        if (X3) {                              // x_lo W_hi
+          uint2 r0 = make_uint2(0, 0), r1 = make_uint2(0, 0);
+          if (t0 < 9) r0 = hlo[(2 * wave + n + t0 / 3) * kHaloW + col + t0 % 3];
+          if (t0 + 1 < 9) r1 = hlo[(2 * wave + n + (t0 + 1) / 3) * kHaloW + col + (t0 + 1) % 3];
+          uint4 rq = make_uint4(r0.x, r0.y, r1.x, r1.y);
+          const half8_t bfl = *reinterpret_cast<const half8_t*>(&rq);
+          if (n == 0) {
+            acc00 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, bfl, acc00, 0, 0, 0);
+            acc10 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, bfl, acc10, 0, 0, 0);
+          } else {
+            acc01 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, bfl, acc01, 0, 0, 0);
+            acc11 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, bfl, acc11, 0, 0, 0);
+          }
+        }
         if (n == 0) {
           acc00 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, bf, acc00, 0, 0, 0);
           acc10 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, bf, acc10, 0, 0, 0);
@@ -850,31 +877,46 @@ __global__ __launch_bounds__(256) void conv_head_kernel(const float* __restrict_
     // XOR-swizzled by pixel (conflict-free writes), stored back as full 128-B pixel lines
     // (1 KiB contiguous per instruction) instead of 16-B pieces at a 128-B stride.
 #pragma unroll
-    for (int n = 0; n < 2; ++n) {
-      const floatx16& a0 = n == 0 ? acc00 : acc01;
-      const floatx16& a1 = n == 0 ? acc10 : acc11;
-      unsigned char* px = stg + (n * 32 + col) * 128;
-      const int sw = col & 7;
-      half8_t v[4];
-      if (act == 0) {                         // packed bias + activation (bit-identical to act_fn)
-        v[0] = bias_act8<0>(a0, 0, bias_r[0]); v[1] = bias_act8<0>(a0, 8, bias_r[0] + 8);
-        v[2] = bias_act8<0>(a1, 0, bias_r[1]); v[3] = bias_act8<0>(a1, 8, bias_r[1] + 8);
-      } else {
-        v[0] = bias_act8<1>(a0, 0, bias_r[0]); v[1] = bias_act8<1>(a0, 8, bias_r[0] + 8);
-        v[2] = bias_act8<1>(a1, 0, bias_r[1]); v[3] = bias_act8<1>(a1, 8, bias_r[1] + 8);
-      }
-      *reinterpret_cast<half8_t*>(px + 16 * ((2 * h) ^ sw)) = v[0];          // channels 16h .. +7
-      *reinterpret_cast<half8_t*>(px + 16 * ((2 * h + 1) ^ sw)) = v[1];      // 16h+8 .. +15
-      *reinterpret_cast<half8_t*>(px + 16 * ((4 + 2 * h) ^ sw)) = v[2];      // 32+16h .. +7
-      *reinterpret_cast<half8_t*>(px + 16 * ((5 + 2 * h) ^ sw)) = v[3];      // 32+16h+8 .. +15
-    }
+    for (int part = 0; part < (X3 ? 2 : 1); ++part) {   // X3: hi image, then lo image
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {             // 8 pixels x 8 chunks per instruction
-      const int n = j >> 2, p = 8 * (j & 3) + (lane >> 3), c = lane & 7;
-      const uint4 q = *reinterpret_cast<const uint4*>(stg + (n * 32 + p) * 128 + 16 * (c ^ (p & 7)));
-      const int y = ty0 + 2 * wave + n, x = tx0 + p;
-      if (y < s.H && x < s.W)
-        *reinterpret_cast<uint4*>(out + (((size_t)b * s.Hp + y + s.pad) * s.Wp + x + s.pad) * kWidth + 8 * c) = q;
+      for (int n = 0; n < 2; ++n) {
+        const floatx16& a0 = n == 0 ? acc00 : acc01;
+        const floatx16& a1 = n == 0 ? acc10 : acc11;
+        unsigned char* px = stg + (n * 32 + col) * 128;
+        const int sw = col & 7;
+        half8_t v[4];
+        if (X3) {                               // fp32 bias + activation, then the hi or lo half
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+              const floatx16& a = q < 2 ? a0 : a1;
+              float f = a[8 * (q & 1) + r] + bias_r[q >> 1][8 * (q & 1) + r];
+              f = act == 0 ? fmaxf(f, f * 0.01f) : fmaxf(f, 0.f);
+              const _Float16 fh = (_Float16)f;
+              v[q][r] = part == 0 ? fh : (_Float16)(f - (float)fh);
+            }
+        } else if (act == 0) {                  // packed bias + activation (bit-identical to act_fn)
+          v[0] = bias_act8<0>(a0, 0, bias_r[0]); v[1] = bias_act8<0>(a0, 8, bias_r[0] + 8);
+          v[2] = bias_act8<0>(a1, 0, bias_r[1]); v[3] = bias_act8<0>(a1, 8, bias_r[1] + 8);
+        } else {
+          v[0] = bias_act8<1>(a0, 0, bias_r[0]); v[1] = bias_act8<1>(a0, 8, bias_r[0] + 8);
+          v[2] = bias_act8<1>(a1, 0, bias_r[1]); v[3] = bias_act8<1>(a1, 8, bias_r[1] + 8);
+        }
+        *reinterpret_cast<half8_t*>(px + 16 * ((2 * h) ^ sw)) = v[0];          // channels 16h .. +7
+        *reinterpret_cast<half8_t*>(px + 16 * ((2 * h + 1) ^ sw)) = v[1];      // 16h+8 .. +15
+        *reinterpret_cast<half8_t*>(px + 16 * ((4 + 2 * h) ^ sw)) = v[2];      // 32+16h .. +7
+        *reinterpret_cast<half8_t*>(px + 16 * ((5 + 2 * h) ^ sw)) = v[3];      // 32+16h+8 .. +15
+      }
+      half_t* dst = part == 0 ? out : out_lo;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {             // 8 pixels x 8 chunks per instruction
+        const int n = j >> 2, p = 8 * (j & 3) + (lane >> 3), c = lane & 7;
+        const uint4 q = *reinterpret_cast<const uint4*>(stg + (n * 32 + p) * 128 + 16 * (c ^ (p & 7)));
+        const int y = ty0 + 2 * wave + n, x = tx0 + p;
+        if (y < s.H && x < s.W)
+          *reinterpret_cast<uint4*>(dst + (((size_t)b * s.Hp + y + s.pad) * s.Wp + x + s.pad) * kWidth + 8 * c) = q;
+      }
     }
   }
 }
@@ -1138,15 +1180,17 @@ hipError_t conv_kernels_init() {
 }
 
 void launch_conv_head(const float* in32, int C, half_t* out, const void* w, const void* w_lo, const float* bias,
-                      const ConvShape& s, int act, int num_cus, int blocks_per_cu, hipStream_t st) {
+                      const ConvShape& s, int act, int num_cus, int blocks_per_cu, hipStream_t st, half_t* out_lo) {
   const int grid = s.tiles < num_cus * blocks_per_cu ? s.tiles : num_cus * blocks_per_cu;
-#define HEAD(W2V, NCV)                                                                                        \
-  hipLaunchKernelGGL((conv_head_kernel<W2V, NCV>), dim3(grid), dim3(256), 0, st, in32, C, out, (const uint4*)w, \
-                     (const uint4*)w_lo, bias, s, act)
-  if (w_lo) {
-    if (C == 3) HEAD(true, 3); else if (C == 1) HEAD(true, 1); else HEAD(true, 0);
+#define HEAD(PV, NCV)                                                                                            \
+  hipLaunchKernelGGL((conv_head_kernel<PV, NCV>), dim3(grid), dim3(256), 0, st, in32, C, out, out_lo,              \
+                     (const uint4*)w, (const uint4*)w_lo, bias, s, act)
+  if (out_lo) {
+    if (C == 3) HEAD(2, 3); else if (C == 1) HEAD(2, 1); else HEAD(2, 0);
+  } else if (w_lo) {
+    if (C == 3) HEAD(1, 3); else if (C == 1) HEAD(1, 1); else HEAD(1, 0);
   } else {
-    if (C == 3) HEAD(false, 3); else if (C == 1) HEAD(false, 1); else HEAD(false, 0);
+    if (C == 3) HEAD(0, 3); else if (C == 1) HEAD(0, 1); else HEAD(0, 0);
   }
 #undef HEAD
 }

@@ -1,0 +1,318 @@
+// Split-fp16 ("fp16x3") denoiser body and tail for gfx950: near-fp32 convolutions on the fp16
+// MFMA.  Every operand is carried as an fp16 pair, x = x_hi + x_lo with x_hi = fp16(x) and
+// x_lo = fp16(x - x_hi) (subnormals kept: the f16 MFMA does not flush them), so activations and
+// weights keep ~21-22 significant bits; each product is
+//     a * w  ~  a_hi w_hi + a_hi w_lo + a_lo w_hi          (the a_lo w_lo term is below fp32's ulp)
+// in one fp32 accumulator: three v_mfma_f32_16x16x32_f16 per fp16 product.
+//
+// Why: the reference denoiser runs in fp32 (models/denoiser.py:37).  fp16 operands hold PSNR
+// within 0.01 dB at the metric (ours-A blur, 32-41 dB) but not at high-PSNR regimes: BASELINE
+// config 1 (gray 256^2, Id, 45-50 dB) moves 0.067 dB within 23 iterations, and the Poisson
+// method (ours-C) drifts 0.19 dB over 3000 iterations.  CPU emulation of this scheme on config 1
+// (tools/precision_emu.py): 6e-5 dB against the fp32 oracle, vs 0.06 dB for fp16 operands.
+// The fp32-operand path (conv32.hip, v_mfma_f32_32x32x2_f32, 157 TF peak) does the same job
+// at 1/16 of the fp16 MFMA rate; three fp16 MFMAs per product cost 1/3.
+//
+// Reference: models/basic_models.py:25-38 (simple_CNN.forward), KAIR network_dncnn.py:42-77.
+//
+// Layout.  Hidden activations are two fp16 NHWC64 images (hi, lo) with the same zero border
+// (kActPad) as the fp16 path, 128 B per pixel each.  A workgroup (8 waves, 2 per SIMD, one per
+// CU: the LDS holds three halo buffers) is persistent over 8 x 16 output tiles.  A tile's
+// 10 x 18 input halo sits in LDS as 16 chunk planes (hi chunks 0-7, lo chunks 0-7: plane c
+// holds channels 8(c & 7) .. +7 of every halo pixel, 16 B per pixel), so a B fragment of
+// v_mfma_f32_16x16x32_f16 (16 pixels x 32 channels: lane l reads chunk 4 hs + (l >> 4) of
+// pixel l & 15) is four 256-B runs in planes 256-B apart: conflict-free.  Planes are 192
+// pixels (3072 B): a halo plane is exactly 3 LDS-DMA pieces of 64 pixels (buffer_load ... lds,
+// 16 B per lane), 48 pieces per tile = 6 per wave, all with the same instruction count.  The
+// DMA runs two tiles ahead (3-deep ring).
+//
+// Body (64 -> 64): wave w owns output channels 16 (w & 3) .. +15 of tile rows 4 (w >> 2) .. +3
+// (four N-subtiles of 16 pixels).  Its A fragments, hi and lo, for all 18 K-steps stay in
+// registers for the launch (144 VGPRs); per K-step it reads 4 hi + 4 lo B fragments and issues
+// 12 MFMAs.  The epilogue adds the bias, applies the activation in fp32 and stores the hi and
+// lo halves: lane l holds channels 16 (w & 3) + 4 (l >> 4) .. +3 of one pixel (8 B each).
+// Tail (64 -> C, C <= 4): one 16-row M-tile (rows >= C zero), wave w = tile row w; the
+// epilogue adds the bias and the fp32 residual, clamps, and writes fp32 NCHW.
+#include "kernels.h"
+
+namespace pnp {
+
+namespace {
+
+constexpr int kS3HaloW = kS3TileW + 2;                  // 18
+constexpr int kS3HaloPix = (kS3TileH + 2) * kS3HaloW;   // 180
+constexpr int kS3Plane = 192 * 16;                      // 3072 B: 3 DMA pieces, a multiple of 256 B
+constexpr int kS3Buf = 16 * kS3Plane;                   // 49152 B: 8 hi + 8 lo chunk planes
+constexpr int kS3Lds = 3 * kS3Buf;                      // 147456 B
+constexpr int kS3KSteps = 18;                           // 9 taps x 2 channel halves of 32
+constexpr int kS3Pieces = 6;                            // DMA pieces per wave per tile (48 / 8)
+
+typedef int v2i_t __attribute__((ext_vector_type(2)));
+typedef _Float16 h4_t __attribute__((ext_vector_type(4)));
+
+struct S3Geom {
+  int tiles_x, tiles_y, tiles;
+};
+
+__device__ __forceinline__ void s3_decode(int t, const S3Geom& g, int& b, int& ty0, int& tx0) {
+  const int per = g.tiles_x * g.tiles_y;
+  b = t / per;
+  const int r = t - b * per;
+  const int ty = r / g.tiles_x;
+  ty0 = ty * kS3TileH;
+  tx0 = (r - ty * g.tiles_x) * kS3TileW;
+}
+
+__device__ __forceinline__ int xcd_block_s3(int b, int G) {   // as conv.hip xcd_block
+  return (G & 7) ? b : (b & 7) * (G >> 3) + (b >> 3);
+}
+
+// MODE 0: body 64 -> 64 (hi/lo out).  MODE 1: tail 64 -> C + residual + clamp (fp32 NCHW out).
+template <int MODE, int ACT>
+__global__ __launch_bounds__(512, 1) void conv_s3_kernel(const half_t* __restrict__ in_hi,
+                                                          const half_t* __restrict__ in_lo,
+                                                          half_t* __restrict__ out_hi, half_t* __restrict__ out_lo,
+                                                          const uint4* __restrict__ w_hi,
+                                                          const uint4* __restrict__ w_lo,
+                                                          const float* __restrict__ bias,
+                                                          const float* __restrict__ xin, float* __restrict__ xout,
+                                                          ConvShape s, S3Geom g, int C, int residual_sign,
+                                                          int clamp_out) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int NT = MODE == 0 ? 4 : 1;                 // N-subtiles (tile rows) per wave
+  constexpr int NM = MODE == 0 ? 4 : 1;                 // 16-row M-tiles
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int mt = MODE == 0 ? (wave & 3) : 0;
+  const int row0 = MODE == 0 ? 4 * (wave >> 2) : wave;
+  const int px = lane & 15, grp = lane >> 4;
+
+  half8_t wH[kS3KSteps], wL[kS3KSteps];
+#pragma unroll
+  for (int ks = 0; ks < kS3KSteps; ++ks) {
+    const size_t o = ((size_t)(ks * NM + mt) * 64 + lane);
+    wH[ks] = __builtin_bit_cast(half8_t, w_hi[o]);
+    wL[ks] = __builtin_bit_cast(half8_t, w_lo[o]);
+  }
+  float bl[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int co = MODE == 0 ? 16 * mt + 4 * grp + i : i;
+    bl[i] = (MODE == 0 || co < C) ? bias[co] : 0.f;
+  }
+
+  // DMA: piece q = 8 j + wave (j < 6) covers plane c = q / 3 (hi for c < 8), pixels 64 (q % 3) ..
+  // +63 of the halo (pixels past 179 re-read pixel 179 into the plane's padding).
+  unsigned doff[kS3Pieces];
+#pragma unroll
+  for (int j = 0; j < kS3Pieces; ++j) {
+    const int q = 8 * j + wave, c = q / 3, k = q - 3 * c;
+    const int p = min(64 * k + lane, kS3HaloPix - 1);
+    const int pr = p / kS3HaloW, pc = p - pr * kS3HaloW;
+    doff[j] = (unsigned)(((pr * s.Wp + pc) * kWidth + 8 * (c & 7)) * 2);
+  }
+  auto issue = [&](int tt, int bi) {                    // clamped: always kS3Pieces instructions
+    int b, ty0, tx0;
+    s3_decode(tt < g.tiles ? tt : g.tiles - 1, g, b, ty0, tx0);
+    const size_t base = (((size_t)b * s.Hp + ty0 + s.pad - 1) * s.Wp + tx0 + s.pad - 1) * kWidth;
+    const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc((void*)(in_hi + base), (short)0, 0x7fffffff,
+                                                                        0x00020000);
+    const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc((void*)(in_lo + base), (short)0, 0x7fffffff,
+                                                                        0x00020000);
+    unsigned char* dst = smem + bi * kS3Buf;
+#pragma unroll
+    for (int j = 0; j < kS3Pieces; ++j) {
+      const int q = 8 * j + wave, c = q / 3, k = q - 3 * c;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(c < 8 ? rh : rl,
+                                               (__attribute__((address_space(3))) void*)(dst + c * kS3Plane + k * 1024),
+                                               16, doff[j], 0, 0, 0);
+    }
+  };
+
+  const int G = gridDim.x;
+  int t = xcd_block_s3(blockIdx.x, G);
+  if (t < g.tiles) {
+    issue(t, 0);
+    issue(t + G, 1);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");   // tile t landed
+  }
+  __syncthreads();
+  const unsigned plane = (unsigned)(s.H * s.W);
+  int cur = 0;
+  for (; t < g.tiles; t += G) {
+    int b, ty0, tx0;
+    s3_decode(t, g, b, ty0, tx0);
+    // tail: the residual input, loaded before this tile's DMA issue (so waiting for it never
+    // waits on the DMA); always kMaxC loads (c >= C: zero-size descriptor)
+    float xi[MODE == 1 ? kMaxC : 1];
+    unsigned toff = 0;
+    if constexpr (MODE == 1) {
+      const int y = ty0 + row0, x = tx0 + px;
+      toff = (lane < 16 && y < s.H && x < s.W) ? (unsigned)(y * s.W + x) * 4u : 0x80000000u;
+#pragma unroll
+      for (int c = 0; c < kMaxC; ++c) {
+        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(xin + ((size_t)b * C + (c < C ? c : 0)) * plane), (short)0, c < C ? (int)(plane * 4u) : 0,
+            0x00020000);
+        xi[c] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, toff, 0, 0));
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    issue(t + 2 * G, cur >= 1 ? cur - 1 : 2);
+    const unsigned char* fb = smem + cur * kS3Buf + grp * kS3Plane + (row0 * kS3HaloW + px) * 16;
+    auto ldB = [&](int ks, int n, int lo) {
+      const int tap = ks >> 1, dy = tap / 3, dx = tap - 3 * dy;
+      return *reinterpret_cast<const half8_t*>(fb + (8 * lo + 4 * (ks & 1)) * kS3Plane +
+                                               ((n + dy) * kS3HaloW + dx) * 16);
+    };
+    floatx4 acc[NT];
+    half8_t bh[2][NT], bo[2][NT];
+#pragma unroll
+    for (int n = 0; n < NT; ++n) {
+      bh[0][n] = ldB(0, n, 0);
+      bo[0][n] = ldB(0, n, 1);
+    }
+#pragma unroll
+    for (int ks = 0; ks < kS3KSteps; ++ks) {
+      const int r = ks & 1;
+      if (ks + 1 < kS3KSteps) {
+#pragma unroll
+        for (int n = 0; n < NT; ++n) {
+          bh[r ^ 1][n] = ldB(ks + 1, n, 0);
+          bo[r ^ 1][n] = ldB(ks + 1, n, 1);
+        }
+      }
+#pragma unroll
+      for (int n = 0; n < NT; ++n)
+        acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wH[ks], bh[r][n], ks == 0 ? floatx4{} : acc[n], 0, 0, 0);
+#pragma unroll
+      for (int n = 0; n < NT; ++n) acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wL[ks], bh[r][n], acc[n], 0, 0, 0);
+#pragma unroll
+      for (int n = 0; n < NT; ++n) acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wH[ks], bo[r][n], acc[n], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if constexpr (MODE == 0) {
+#pragma unroll
+      for (int n = 0; n < NT; ++n) {
+        const int y = ty0 + row0 + n;
+        h4_t hi, lo;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float v = acc[n][i] + bl[i];
+          v = ACT == 0 ? fmaxf(v, v * 0.01f) : fmaxf(v, 0.f);
+          hi[i] = (half_t)v;
+          lo[i] = (half_t)(v - (float)hi[i]);
+        }
+        const size_t rowb = (((size_t)b * s.Hp + y + s.pad) * s.Wp + tx0 + s.pad) * kWidth;
+        const int nrec = y < s.H ? min(kS3TileW, s.W - tx0) * 128 : 0;
+        const unsigned off = (unsigned)(px * 128 + (16 * mt + 4 * grp) * 2);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2i_t, hi),
+                                              __builtin_amdgcn_make_buffer_rsrc(out_hi + rowb, (short)0, nrec, 0x00020000),
+                                              off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2i_t, lo),
+                                              __builtin_amdgcn_make_buffer_rsrc(out_lo + rowb, (short)0, nrec, 0x00020000),
+                                              off, 0, 0);
+      }
+      // tile t+1 landed: younger than its DMA are the DMA of t+2 (6) and this tile's 8 stores
+      asm volatile("s_waitcnt vmcnt(14) lgkmcnt(0)" ::: "memory");
+    } else {
+      // lanes 0..15 hold channels 0..3 of pixel (row0, px): D rows 4 (l >> 4) + i
+#pragma unroll
+      for (int c = 0; c < kMaxC; ++c) {
+        const float nc = acc[0][c] + bl[c];
+        float o = residual_sign > 0 ? nc + xi[c] : xi[c] - nc;
+        if (clamp_out) o = fminf(fmaxf(o, 0.f), 1.f);
+        __builtin_amdgcn_raw_buffer_store_b32(
+            __builtin_bit_cast(int, o),
+            __builtin_amdgcn_make_buffer_rsrc((void*)(xout + ((size_t)b * C + (c < C ? c : 0)) * plane), (short)0,
+                                              c < C ? (int)(plane * 4u) : 0, 0x00020000),
+            toff, 0, 0);
+      }
+      // tile t+1 landed: younger than its DMA are this tile's 4 loads, the DMA of t+2 and 4 stores
+      asm volatile("s_waitcnt vmcnt(14) lgkmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    cur = cur == 2 ? 0 : cur + 1;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA may land after the workgroup ends
+}
+
+#define PNP_S3_INST(M, A)                                                                                      \
+  template __global__ void conv_s3_kernel<M, A>(const half_t* __restrict__, const half_t* __restrict__,       \
+                                                half_t* __restrict__, half_t* __restrict__,                    \
+                                                const uint4* __restrict__, const uint4* __restrict__,          \
+                                                const float* __restrict__, const float* __restrict__,          \
+                                                float* __restrict__, ConvShape, S3Geom, int, int, int);
+PNP_S3_INST(0, 0)
+PNP_S3_INST(0, 1)
+PNP_S3_INST(1, 0)
+#undef PNP_S3_INST
+
+S3Geom s3_geom(const ConvShape& s) {
+  S3Geom g;
+  g.tiles_x = (s.W + kS3TileW - 1) / kS3TileW;
+  g.tiles_y = (s.H + kS3TileH - 1) / kS3TileH;
+  g.tiles = s.B * g.tiles_x * g.tiles_y;
+  return g;
+}
+
+inline uint16_t f16_bits(float f) {
+  _Float16 h = (_Float16)f;
+  uint16_t u;
+  memcpy(&u, &h, 2);
+  return u;
+}
+
+}  // namespace
+
+hipError_t conv_s3_kernels_init() {
+  for (const void* k : {(const void*)conv_s3_kernel<0, 0>, (const void*)conv_s3_kernel<0, 1>,
+                        (const void*)conv_s3_kernel<1, 0>}) {
+    hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kS3Lds);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+// W: [64][64][3][3] fp32 -> hi / lo fragments [18 ks][4 M-tiles][64 lanes][8] fp16: lane l holds
+// A[row l & 15][k = 8 (l >> 4) .. +7], row r of M-tile mt = output channel 16 mt + r, k-step ks =
+// tap ks >> 1, input channels 32 (ks & 1) + k.  hi = fp16(w), lo = fp16(w - hi).
+void pack_body_weights_s3(const float* W, uint16_t* hi, uint16_t* lo) {
+  for (int ks = 0; ks < kS3KSteps; ++ks) {
+    const int tap = ks >> 1, ky = tap / 3, kx = tap % 3;
+    for (int mt = 0; mt < 4; ++mt)
+      for (int l = 0; l < 64; ++l)
+        for (int j = 0; j < 8; ++j) {
+          const int co = 16 * mt + (l & 15), ci = 32 * (ks & 1) + 8 * (l >> 4) + j;
+          const float w = W[((co * 64 + ci) * 3 + ky) * 3 + kx];
+          const float h = (float)(_Float16)w;
+          const size_t o = (((size_t)ks * 4 + mt) * 64 + l) * 8 + j;
+          hi[o] = f16_bits(w);
+          lo[o] = f16_bits(w - h);
+        }
+  }
+}
+
+void launch_conv_s3_body(const half_t* in_hi, const half_t* in_lo, half_t* out_hi, half_t* out_lo, const void* w_hi,
+                         const void* w_lo, const float* bias, const ConvShape& s, int act, int num_cus,
+                         hipStream_t st) {
+  const S3Geom g = s3_geom(s);
+  const int grid = g.tiles < num_cus ? g.tiles : num_cus;
+  if (act == 0)
+    hipLaunchKernelGGL((conv_s3_kernel<0, 0>), dim3(grid), dim3(512), kS3Lds, st, in_hi, in_lo, out_hi, out_lo,
+                       (const uint4*)w_hi, (const uint4*)w_lo, bias, nullptr, nullptr, s, g, kWidth, 1, 0);
+  else
+    hipLaunchKernelGGL((conv_s3_kernel<0, 1>), dim3(grid), dim3(512), kS3Lds, st, in_hi, in_lo, out_hi, out_lo,
+                       (const uint4*)w_hi, (const uint4*)w_lo, bias, nullptr, nullptr, s, g, kWidth, 1, 0);
+}
+
+void launch_conv_s3_tail(const half_t* in_hi, const half_t* in_lo, const float* xin, float* xout, const void* w_hi,
+                         const void* w_lo, const float* bias, const ConvShape& s, int C, int residual_sign,
+                         int clamp_out, int num_cus, hipStream_t st) {
+  const S3Geom g = s3_geom(s);
+  const int grid = g.tiles < num_cus ? g.tiles : num_cus;
+  hipLaunchKernelGGL((conv_s3_kernel<1, 0>), dim3(grid), dim3(512), kS3Lds, st, in_hi, in_lo, nullptr, nullptr,
+                     (const uint4*)w_hi, (const uint4*)w_lo, bias, xin, xout, s, g, C, residual_sign, clamp_out);
+}
+
+}  // namespace pnp

@@ -19,9 +19,12 @@ void pack_body_weights(const float* W, uint16_t* out);
 void pack_body_weights16(const float* W, uint16_t* out);   // v_mfma_f32_16x16x32_f16 fragments (conv_body_x8)
 void pack_head_weights(const float* W, int C, uint16_t* out);
 void pack_tail_weights(const float* W, int C, uint16_t* out);
-// w_lo (nullable): the split weights' low halves (PNP_PREC_FP16W2), packed like w
+// w_lo (nullable): the split weights' low halves (PNP_PREC_FP16W2 / FP16X3), packed like w.
+// out_lo (nullable, FP16X3): the input is split too (three MFMAs per product) and the output is
+// written as hi (out) + lo (out_lo) fp16 images.
 void launch_conv_head(const float* in32, int C, half_t* out, const void* w, const void* w_lo, const float* bias,
-                      const ConvShape& s, int act, int num_cus, int blocks_per_cu, hipStream_t st);
+                      const ConvShape& s, int act, int num_cus, int blocks_per_cu, hipStream_t st,
+                      half_t* out_lo = nullptr);
 // one 64 -> 64 layer; ablate != 0 only in the PNP_PROFILING build (profiling, results wrong)
 void launch_conv_body(const half_t* in, half_t* out, const void* w, const float* bias, const ConvShape& s,
                       int act, int num_cus, int ablate, hipStream_t st);
@@ -38,6 +41,19 @@ void launch_conv_body_f2(const half_t* in, half_t* out, const void* w16_1, const
 // one 64 -> 64 layer with split weights W_hi + W_lo (PNP_PREC_FP16W2)
 void launch_conv_body_w2(const half_t* in, half_t* out, const void* w, const void* w_lo, const float* bias,
                          const ConvShape& s, int act, int num_cus, hipStream_t st);
+// split-fp16 denoiser (conv_s3.hip, PNP_PREC_FP16X3): activations as fp16 hi + lo images (two
+// padded NHWC64 buffers), weights hi + lo, three fp16 MFMAs per product; 8 x 16 output tiles.
+constexpr int kS3TileH = 8, kS3TileW = 16;
+hipError_t conv_s3_kernels_init();
+// W [64][64][3][3] -> hi / lo fragments, kBodyWBytes each
+void pack_body_weights_s3(const float* W, uint16_t* hi, uint16_t* lo);
+void launch_conv_s3_body(const half_t* in_hi, const half_t* in_lo, half_t* out_hi, half_t* out_lo, const void* w_hi,
+                         const void* w_lo, const float* bias, const ConvShape& s, int act, int num_cus,
+                         hipStream_t st);
+// 64 -> C + residual (x_in fp32 NCHW) + clamp -> fp32 NCHW; weights: pack_tail_weights of hi and lo
+void launch_conv_s3_tail(const half_t* in_hi, const half_t* in_lo, const float* xin, float* xout, const void* w_hi,
+                         const void* w_lo, const float* bias, const ConvShape& s, int C, int residual_sign,
+                         int clamp_out, int num_cus, hipStream_t st);
 // fp32-operand denoiser (conv32.hip, PNP_PREC_FP32): mode 0 = head (NCHW fp32 in), 1 = body,
 // 2 = tail (NCHW fp32 out + residual + clamp); activations fp32 padded NHWC64, pad 1.
 hipError_t conv32_kernels_init();

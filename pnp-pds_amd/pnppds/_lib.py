@@ -23,8 +23,8 @@ METHOD_A, METHOD_B, METHOD_C, METHOD_ADMM_B2 = 0, 1, 2, 3
  METHOD_C_PNPADMM, METHOD_C_RED) = range(4, 13)
 TV_METHODS = (METHOD_A_PDS_TV, METHOD_A_FBS_TV, METHOD_B_HTV)   # no denoiser
 OP_ID, OP_BLUR, OP_RANDOM_SAMPLING = 0, 1, 2
-PREC_FP16, PREC_FP32, PREC_FP16W2 = 0, 1, 2
-PRECISIONS = {"fp16": PREC_FP16, "fp32": PREC_FP32, "fp16w2": PREC_FP16W2}
+PREC_FP16, PREC_FP32, PREC_FP16W2, PREC_FP16X3 = 0, 1, 2, 3
+PRECISIONS = {"fp16": PREC_FP16, "fp32": PREC_FP32, "fp16w2": PREC_FP16W2, "fp16x3": PREC_FP16X3}
 TUNE_DENOISE_CHUNK = 1
 TUNE_BODY_LAYERS = 2
 TUNE_GRAPH = 3
@@ -45,7 +45,7 @@ class pnp_params(C.Structure):
                 ("record_ssim", C.c_int32)]
 
 
-ABI_VERSION = 3   # include/pnppds.h PNP_ABI_VERSION
+ABI_VERSION = 4   # include/pnppds.h PNP_ABI_VERSION
 class pnp_degrade_params(C.Structure):
     _fields_ = [("gaussian_nl", C.c_double), ("sp_nl", C.c_double), ("poisson_alpha", C.c_double),
                 ("poisson_noise", C.c_int32), ("seed", C.c_uint32)]

@@ -56,7 +56,7 @@ def test_exports_are_plain_c(lib):
 
 def test_abi_version_and_errors_without_gpu(lib):
     from pnppds import _lib
-    assert lib.pnp_abi_version() == _lib.ABI_VERSION == 3
+    assert lib.pnp_abi_version() == _lib.ABI_VERSION == 4
     lib.pnp_last_error.restype = ctypes.c_char_p
     h = ctypes.c_void_p()
     rc = lib.pnp_create(0, ctypes.byref(h))

@@ -108,6 +108,54 @@ def test_denoiser_fp16w2(gpu_ctx, name, B, C, H, W):
     assert np.abs(out - ref).mean() < e16          # on average nearer fp32 than fp16 weights
 
 
+# split fp16 (PNP_PREC_FP16X3, conv_s3.hip): activations and weights as fp16 hi + lo pairs,
+# three MFMAs per product.  ~21 significant bits on both operands (the lo halves of small
+# values are fp16 subnormals), so it sits between the fp32 path and fp16w2.
+TOL_X3 = 5e-5
+
+
+@pytest.mark.parametrize("name", ["DnCNN_nobn_nch_3_nlev_0.01", "DnCNN_nobn_nch_1_nlev_0.01",
+                                  "dncnn_color_blind", "dncnn_15"])
+def test_denoiser_fp16x3_golden(gpu_ctx, golden_denoiser, name):
+    """The split-fp16 path against the reference's own denoiser outputs and the fp32 oracle."""
+    w = DenoiserWeights.load_npz(os.path.join(WEIGHTS_DIR, name + ".npz"))
+    xin = golden_denoiser[f"in_{name}"]
+    x4 = xin.reshape((1, 1) + xin.shape) if xin.ndim == 2 else xin[None]
+    gpu_ctx.set_precision("fp16x3")
+    try:
+        out = run_denoise(gpu_ctx, w, x4).reshape(xin.shape)
+    finally:
+        gpu_ctx.set_precision("fp16")
+    ref = golden_denoiser[f"out_{name}"]
+    scale = max(1.0, float(np.abs(ref).max()))
+    err = float(np.abs(out - ref).max())
+    e16 = float(np.abs(O.OracleDenoiser(w, emulate_fp16=True).forward_batch(x4).reshape(xin.shape) - ref).max())
+    print(f"{name}: fp16x3 path max|d| vs reference = {err:.2e} (fp16 operands: {e16:.2e})")
+    assert err <= TOL_X3 * scale
+    o32 = O.OracleDenoiser(w).forward_batch(x4).reshape(xin.shape)
+    assert np.abs(out - o32).max() <= TOL_X3 * scale
+
+
+@pytest.mark.parametrize("B,C,H,W", [(3, 3, 50, 70), (2, 1, 33, 31), (1, 3, 8, 16), (1, 1, 5, 7), (2, 3, 256, 256),
+                                     (4, 3, 41, 100)])
+def test_denoiser_fp16x3_ragged_batched(gpu_ctx, B, C, H, W):
+    """Split fp16: partial 8 x 16 tiles, tiny images, several images per launch, against the
+    fp32 oracle; each image alone gives the batch's bits."""
+    rng = np.random.default_rng(B * 100 + H + 9)
+    w = random_weights(C, depth=6, seed=H + 1, scale=0.9)
+    x = rng.uniform(-0.1, 1.1, (B, C, H, W)).astype(np.float32)
+    gpu_ctx.set_precision("fp16x3")
+    try:
+        out = run_denoise(gpu_ctx, w, x)
+        one = run_denoise(gpu_ctx, w, x[B - 1:B])
+    finally:
+        gpu_ctx.set_precision("fp16")
+    ref = O.OracleDenoiser(w).forward_batch(x)
+    print(f"fp16x3 {B}x{C}x{H}x{W}: max|d| vs fp32 oracle = {np.abs(out - ref).max():.2e}")
+    np.testing.assert_allclose(out, ref, atol=TOL_X3)
+    np.testing.assert_array_equal(one[0], out[B - 1])
+
+
 @pytest.mark.parametrize("B,C,H,W", [(3, 3, 50, 70), (2, 1, 33, 31), (1, 3, 8, 32), (2, 3, 256, 256)])
 def test_denoiser_fp32_ragged_batched(gpu_ctx, B, C, H, W):
     """fp32 path: partial tiles, tiny images, several images per launch; batch vs single bits."""

@@ -24,7 +24,7 @@ PSNR_TOL_DB = 0.01          # north_star: PSNR within 0.01 dB of the reference
 # still differ by about one fp16 rounding (2^-11 relative): c_n stalls near 3e-4 while the
 # reference's fp32 iteration keeps contracting (to 7e-8 after 1200 iterations).  So c_n is
 # compared down to that floor for fp16, and down to 2e-6 for the fp32-operand path.
-C_FLOOR = {"fp16": 1e-3, "fp16w2": 1e-3, "fp32": 2e-6}
+C_FLOOR = {"fp16": 1e-3, "fp16w2": 1e-3, "fp16x3": 2e-5, "fp32": 2e-6}
 
 
 def run_long(g, precision=None):
@@ -40,7 +40,16 @@ def run_long(g, precision=None):
 @pytest.mark.parametrize("case,precision", [("A_blur_1200", "fp16"), ("A_blur_1200", "fp32"),
                                             ("B_blur_300", "fp16"), ("B_blur_300", "fp32"),
                                             ("A_blur_1200", "fp16w2"),
-                                            ("C_rs_300", "auto"), ("C_rs_3000", "auto")])
+                                            ("C_rs_300", "auto"), ("C_rs_3000", "auto"),
+                                            # split fp16 (three MFMAs per product)
+                                            ("A_blur_1200", "fp16x3"), ("C_rs_3000", "fp16x3"),
+                                            ("B_blur_300", "fp16x3"),
+                                            # the reference's other regimes (main.py:130-139, BASELINE
+                                            # config 1): gray 256^2 Id, random sampling x 3000, sigma 0.0025
+                                            ("A_gray_id_1200", "auto"), ("A_rs_3000", "auto"),
+                                            ("A_blur_s0025_1200", "auto"), ("A_rs_s0025_3000", "auto"),
+                                            ("A_gray_id_1200", "fp16x3"), ("A_rs_3000", "fp16x3"),
+                                            ("A_blur_s0025_1200", "fp16x3"), ("A_rs_s0025_3000", "fp16x3")])
 def test_long_trajectory_psnr(case, precision):
     """Every iteration's PSNR within 0.01 dB of the reference's trajectory.  'auto' is the
     default precision policy (fp32 operands for the Poisson methods: with fp16 ones ours-C
