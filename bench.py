@@ -250,8 +250,8 @@ def main():
     ap.add_argument("--op", default="", choices=["", "blur", "Id", "random_sampling"],
                     help="override the config's degradation operator (profiling the elementwise K1/K2)")
     ap.add_argument("--precision", default="auto", choices=["auto", "fp16", "fp16w2", "fp16x3", "fp32"],
-                    help="denoiser operands: auto = the solver's policy (fp32 for the Poisson methods, "
-                         "fp16 otherwise; pnppds.iteration.FP32_METHODS)")
+                    help="denoiser operands: auto = the library's per-solve policy (PNP_PREC_AUTO: fp16 for "
+                         "ours-A/B on blur, split fp16 'fp16x3' otherwise)")
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU-baseline work")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile", type=int, default=1, help="HIP-event per-kernel timing in the timed region")
@@ -296,8 +296,7 @@ def main():
     arch = f"DnCNN_nobn_nch_{C}_nlev_0.01"
     ctx = _lib.Context(local)
     ctx.set_denoiser(resolve_weights(arch, C))
-    args.precision = resolve_precision(args.precision, resolve_method(cfg["method"]))
-    ctx.set_precision(args.precision)
+    ctx.set_precision(resolve_precision(args.precision))
     if args.body_layers:
         ctx.set_body_layers(args.body_layers)
     if args.graph:
@@ -326,6 +325,7 @@ def main():
                       cfg["sigma"], cfg["sp"], POISSON_ALPHA, cfg["r"], True)
     ctx.set_denoise_chunk(args.chunk)
     ctx.solver_setup(resolve_method(cfg["method"]), prm, B, C, H, W, cap)
+    prec_req, args.precision = ctx.get_precision()      # what 'auto' resolves to for this solve
     ctx.solver_load_device(d_x0.data_ptr(), d_obs.data_ptr(), d_true.data_ptr())   # x_0 (main.py:62-64)
     if args.ablate:
         ctx.set_ablate(args.ablate)
@@ -367,7 +367,7 @@ def main():
                     f"np.random.seed(1234) streams); real {arch} weights",
             "config": {"workload": cfg["desc"].format(B=B, S=H), "config": args.config, "global_batch": B * world,
                        "image": f"{C}x{H}x{W}", "deg_op": "blur_1" if cfg["op"] == "blur" else cfg["op"],
-                       "method": cfg["method"], "precision": args.precision,
+                       "method": cfg["method"], "precision": args.precision, "precision_requested": prec_req,
                        "parallelism": f"dp{world} (independent image shards, no collective)"},
             "batch_iters_per_s": round(K / t_el, 3),
             "build_id": _lib.build_id(),

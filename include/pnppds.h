@@ -86,10 +86,14 @@ enum pnp_precision {
                         parity fallback; about 1/10 of the fp16 path's throughput     */
   PNP_PREC_FP16W2 = 2,/* fp16 activations, weights split into fp16 hi + lo halves (two
                         MFMAs per product, ~22-bit weights), fp32 accumulation         */
-  PNP_PREC_FP16X3 = 3 /* activations and weights both split into fp16 hi + lo halves,
+  PNP_PREC_FP16X3 = 3,/* activations and weights both split into fp16 hi + lo halves,
                         three fp16 MFMAs per product (hi*hi + hi*lo + lo*hi), fp32
                         accumulation: near-fp32 results at 1/3 of the fp16 MFMA rate
                         (ABI 4)                                                      */
+  PNP_PREC_AUTO = 4   /* default (ABI 4): per solve, FP16 for A/B-Proposed on the blur
+                        operator (measured within 0.01 dB of the reference over its
+                        experiments' lengths), FP16X3 otherwise; single denoiser calls
+                        (pnp_op_denoise) run FP16X3                                  */
 };
 
 /* Scalar parameters of iteration.test_iter (iteration.py:10), same names/meaning. */
@@ -125,8 +129,10 @@ int pnp_synchronize(pnp_ctx* ctx);
  * clamp_io: 1 => clamp input and output to [0,1] (denoiser.py:40,42).            */
 int pnp_set_denoiser(pnp_ctx* ctx, int channels, int depth, int width, const float* params,
                      size_t n_params, int activation, int residual_sign, int clamp_io);
-/* Denoiser operand precision (pnp_precision); applies to every later denoiser call. */
+/* Denoiser operand precision (pnp_precision); applies to every later denoiser call.
+ * pnp_get_precision: the requested value and the one the next solver step will use.   */
 int pnp_set_precision(pnp_ctx* ctx, int precision);
+int pnp_get_precision(pnp_ctx* ctx, int* requested, int* effective);
 
 /* Performance knobs (no effect on results).
  * PNP_TUNE_DENOISE_CHUNK: images per denoiser pass (0 = auto: the whole batch, unless its

@@ -18,13 +18,16 @@
 // Layout.  Hidden activations are two fp16 NHWC64 images (hi, lo) with the same zero border
 // (kActPad) as the fp16 path, 128 B per pixel each.  A workgroup (8 waves, 2 per SIMD, one per
 // CU: the LDS holds three halo buffers) is persistent over 8 x 16 output tiles.  A tile's
-// 10 x 18 input halo sits in LDS as 16 chunk planes (hi chunks 0-7, lo chunks 0-7: plane c
-// holds channels 8(c & 7) .. +7 of every halo pixel, 16 B per pixel), so a B fragment of
-// v_mfma_f32_16x16x32_f16 (16 pixels x 32 channels: lane l reads chunk 4 hs + (l >> 4) of
-// pixel l & 15) is four 256-B runs in planes 256-B apart: conflict-free.  Planes are 192
-// pixels (3072 B): a halo plane is exactly 3 LDS-DMA pieces of 64 pixels (buffer_load ... lds,
-// 16 B per lane), 48 pieces per tile = 6 per wave, all with the same instruction count.  The
-// DMA runs two tiles ahead (3-deep ring).
+// 10 x 18 input halo sits in LDS pixel-major, hi then lo (128 B per pixel, 192 pixel slots per
+// half), its eight 16-B channel chunks XOR-swizzled per halo column: slot s of pixel (pr, pc)
+// holds chunk s ^ f(pc), f(pc) = kS3Swz[pc >> 1].  An LDS-DMA piece (buffer_load ... lds, 16 B
+// per lane) then fetches 8 whole 128-B pixel lines (lane l: pixel l >> 3, source chunk
+// (l & 7) ^ f), 48 pieces per tile = 6 per wave with the same instruction count, and a B
+// fragment of v_mfma_f32_16x16x32_f16 (16 pixels x 32 channels: lane l reads chunk
+// 4 hs + (l >> 4) of pixel l & 15) hits 16 distinct bank quads in each of the four lane groups
+// of a ds_read_b128 for every tap offset (f was found by exhaustive search; an earlier
+// chunk-planar form, 16 B per lane from 64 different lines per piece, ran the tail 1.9x
+// slower).  The DMA runs two tiles ahead (3-deep ring).
 //
 // Body (64 -> 64): wave w owns output channels 16 (w & 3) .. +15 of tile rows 4 (w >> 2) .. +3
 // (four N-subtiles of 16 pixels).  Its A fragments, hi and lo, for all 18 K-steps stay in
@@ -41,8 +44,8 @@ namespace {
 
 constexpr int kS3HaloW = kS3TileW + 2;                  // 18
 constexpr int kS3HaloPix = (kS3TileH + 2) * kS3HaloW;   // 180
-constexpr int kS3Plane = 192 * 16;                      // 3072 B: 3 DMA pieces, a multiple of 256 B
-constexpr int kS3Buf = 16 * kS3Plane;                   // 49152 B: 8 hi + 8 lo chunk planes
+constexpr int kS3Half = 192 * 128;                      // 24576 B: hi (or lo) pixels of a halo, 24 DMA pieces
+constexpr int kS3Buf = 2 * kS3Half;                     // 49152 B
 constexpr int kS3Lds = 3 * kS3Buf;                      // 147456 B
 constexpr int kS3KSteps = 18;                           // 9 taps x 2 channel halves of 32
 constexpr int kS3Pieces = 6;                            // DMA pieces per wave per tile (48 / 8)
@@ -62,6 +65,9 @@ __device__ __forceinline__ void s3_decode(int t, const S3Geom& g, int& b, int& t
   ty0 = ty * kS3TileH;
   tx0 = (r - ty * g.tiles_x) * kS3TileW;
 }
+
+// chunk swizzle of halo column pc: f = {0,1,2,4,5,6,2,6,0}[pc >> 1], 3 bits each
+__device__ __forceinline__ int s3_swz(int pc) { return (0x00CB5888u >> (3 * (pc >> 1))) & 7; }
 
 __device__ __forceinline__ int xcd_block_s3(int b, int G) {   // as conv.hip xcd_block
   return (G & 7) ? b : (b & 7) * (G >> 3) + (b >> 3);
@@ -101,15 +107,15 @@ __global__ __launch_bounds__(512, 1) void conv_s3_kernel(const half_t* __restric
     bl[i] = (MODE == 0 || co < C) ? bias[co] : 0.f;
   }
 
-  // DMA: piece q = 8 j + wave (j < 6) covers plane c = q / 3 (hi for c < 8), pixels 64 (q % 3) ..
-  // +63 of the halo (pixels past 179 re-read pixel 179 into the plane's padding).
+  // DMA: piece q = 8 j + wave (j < 6) covers half q / 24 (hi, lo), pixels 8 (q % 24) .. +7 (pixels
+  // past 179 re-read pixel 179 into the padding slots)
   unsigned doff[kS3Pieces];
 #pragma unroll
   for (int j = 0; j < kS3Pieces; ++j) {
-    const int q = 8 * j + wave, c = q / 3, k = q - 3 * c;
-    const int p = min(64 * k + lane, kS3HaloPix - 1);
+    const int k = (8 * j + wave) % 24;
+    const int p = min(8 * k + (lane >> 3), kS3HaloPix - 1);
     const int pr = p / kS3HaloW, pc = p - pr * kS3HaloW;
-    doff[j] = (unsigned)(((pr * s.Wp + pc) * kWidth + 8 * (c & 7)) * 2);
+    doff[j] = (unsigned)(((pr * s.Wp + pc) * kWidth + 8 * ((lane & 7) ^ s3_swz(pc))) * 2);
   }
   auto issue = [&](int tt, int bi) {                    // clamped: always kS3Pieces instructions
     int b, ty0, tx0;
@@ -122,13 +128,20 @@ __global__ __launch_bounds__(512, 1) void conv_s3_kernel(const half_t* __restric
     unsigned char* dst = smem + bi * kS3Buf;
 #pragma unroll
     for (int j = 0; j < kS3Pieces; ++j) {
-      const int q = 8 * j + wave, c = q / 3, k = q - 3 * c;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(c < 8 ? rh : rl,
-                                               (__attribute__((address_space(3))) void*)(dst + c * kS3Plane + k * 1024),
+      const int q = 8 * j + wave, h = q / 24, k = q - 24 * h;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(h ? rl : rh,
+                                               (__attribute__((address_space(3))) void*)(dst + h * kS3Half + k * 1024),
                                                16, doff[j], 0, 0, 0);
     }
   };
 
+  // per-lane part of the B-fragment addresses: tap column dx, channel half hs
+  unsigned lofs[3][2];
+#pragma unroll
+  for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+    for (int hs = 0; hs < 2; ++hs)
+      lofs[dx][hs] = (unsigned)((px + dx) * 128 + 16 * ((4 * hs + grp) ^ s3_swz(px + dx)));
   const int G = gridDim.x;
   int t = xcd_block_s3(blockIdx.x, G);
   if (t < g.tiles) {
@@ -159,27 +172,32 @@ __global__ __launch_bounds__(512, 1) void conv_s3_kernel(const half_t* __restric
       __builtin_amdgcn_sched_barrier(0);
     }
     issue(t + 2 * G, cur >= 1 ? cur - 1 : 2);
-    const unsigned char* fb = smem + cur * kS3Buf + grp * kS3Plane + (row0 * kS3HaloW + px) * 16;
+    const unsigned char* fb = smem + cur * kS3Buf + row0 * kS3HaloW * 128;
     auto ldB = [&](int ks, int n, int lo) {
       const int tap = ks >> 1, dy = tap / 3, dx = tap - 3 * dy;
-      return *reinterpret_cast<const half8_t*>(fb + (8 * lo + 4 * (ks & 1)) * kS3Plane +
-                                               ((n + dy) * kS3HaloW + dx) * 16);
+      return *reinterpret_cast<const half8_t*>(fb + lofs[dx][ks & 1] + lo * kS3Half + (n + dy) * kS3HaloW * 128);
     };
+    // B fragments are read PD K-steps ahead (the body's 12 MFMAs per K-step cover one step of LDS
+    // latency; the tail's 3 do not); per K-step the next reads are interleaved one per MFMA.
+    constexpr int PD = MODE == 0 ? 1 : 3;
     floatx4 acc[NT];
-    half8_t bh[2][NT], bo[2][NT];
+    half8_t bh[PD + 1][NT], bo[PD + 1][NT];
 #pragma unroll
-    for (int n = 0; n < NT; ++n) {
-      bh[0][n] = ldB(0, n, 0);
-      bo[0][n] = ldB(0, n, 1);
-    }
+    for (int d = 0; d < PD; ++d)
+#pragma unroll
+      for (int n = 0; n < NT; ++n) {
+        bh[d][n] = ldB(d, n, 0);
+        bo[d][n] = ldB(d, n, 1);
+      }
 #pragma unroll
     for (int ks = 0; ks < kS3KSteps; ++ks) {
-      const int r = ks & 1;
-      if (ks + 1 < kS3KSteps) {
+      const int r = ks % (PD + 1);
+      if (ks + PD < kS3KSteps) {
+        const int w = (ks + PD) % (PD + 1);
 #pragma unroll
         for (int n = 0; n < NT; ++n) {
-          bh[r ^ 1][n] = ldB(ks + 1, n, 0);
-          bo[r ^ 1][n] = ldB(ks + 1, n, 1);
+          bh[w][n] = ldB(ks + PD, n, 0);
+          bo[w][n] = ldB(ks + PD, n, 1);
         }
       }
 #pragma unroll
@@ -189,6 +207,14 @@ __global__ __launch_bounds__(512, 1) void conv_s3_kernel(const half_t* __restric
       for (int n = 0; n < NT; ++n) acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wL[ks], bh[r][n], acc[n], 0, 0, 0);
 #pragma unroll
       for (int n = 0; n < NT; ++n) acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wH[ks], bo[r][n], acc[n], 0, 0, 0);
+      if (ks + PD < kS3KSteps) {
+#pragma unroll
+        for (int i = 0; i < 2 * NT; ++i) {         // one LDS read, one MFMA
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, NT, 0);
+      }
       __builtin_amdgcn_sched_barrier(0);
     }
     if constexpr (MODE == 0) {

@@ -23,8 +23,9 @@ METHOD_A, METHOD_B, METHOD_C, METHOD_ADMM_B2 = 0, 1, 2, 3
  METHOD_C_PNPADMM, METHOD_C_RED) = range(4, 13)
 TV_METHODS = (METHOD_A_PDS_TV, METHOD_A_FBS_TV, METHOD_B_HTV)   # no denoiser
 OP_ID, OP_BLUR, OP_RANDOM_SAMPLING = 0, 1, 2
-PREC_FP16, PREC_FP32, PREC_FP16W2, PREC_FP16X3 = 0, 1, 2, 3
-PRECISIONS = {"fp16": PREC_FP16, "fp32": PREC_FP32, "fp16w2": PREC_FP16W2, "fp16x3": PREC_FP16X3}
+PREC_FP16, PREC_FP32, PREC_FP16W2, PREC_FP16X3, PREC_AUTO = 0, 1, 2, 3, 4
+PRECISIONS = {"fp16": PREC_FP16, "fp32": PREC_FP32, "fp16w2": PREC_FP16W2, "fp16x3": PREC_FP16X3, "auto": PREC_AUTO}
+PRECISION_NAMES = {v: k for k, v in PRECISIONS.items()}
 TUNE_DENOISE_CHUNK = 1
 TUNE_BODY_LAYERS = 2
 TUNE_GRAPH = 3
@@ -67,6 +68,7 @@ _SIGS = {
     "pnp_synchronize": ([_P], C.c_int),
     "pnp_set_denoiser": ([_P, C.c_int, C.c_int, C.c_int, _F, C.c_size_t, C.c_int, C.c_int, C.c_int], C.c_int),
     "pnp_set_precision": ([_P, C.c_int], C.c_int),
+    "pnp_get_precision": ([_P, C.POINTER(C.c_int), C.POINTER(C.c_int)], C.c_int),
     "pnp_set_tuning": ([_P, C.c_int, C.c_int], C.c_int),
     "pnp_set_operator": ([_P, C.c_int, _D, C.c_int, C.c_int, C.POINTER(C.c_uint8), C.c_int, C.c_int], C.c_int),
     "pnp_run": ([_P, C.c_int, C.POINTER(pnp_params), C.c_int, C.c_int, C.c_int, C.c_int, _F, _F, _F, C.c_int,
@@ -190,7 +192,7 @@ class Context:
         self.h = h
         self._denoiser_key = None
         self._operator_key = None
-        self.precision = PRECISIONS["fp16"]   # the library's default (pnp_set_precision)
+        self.precision = PREC_AUTO            # the library's default (pnp_set_precision)
 
     # -- plumbing --
     def _check(self, rc):
@@ -223,12 +225,21 @@ class Context:
         self._denoiser_key = key
 
     def set_precision(self, precision):
-        """Denoiser operands: 'fp16' (default; fp32 accumulation), 'fp16w2' (fp16 activations,
-        weights as fp16 hi + lo pairs: two MFMAs per product) or 'fp32' (the reference's own
-        precision, models/denoiser.py:37; about a tenth of the throughput)."""
+        """Denoiser operands: 'auto' (default: the library's per-solve policy, fp16 for ours-A/B
+        on blur and fp16x3 otherwise; include/pnppds.h PNP_PREC_AUTO), 'fp16' (fp32
+        accumulation), 'fp16w2' (fp16 activations, weights as fp16 hi + lo pairs: two MFMAs per
+        product), 'fp16x3' (activations and weights as hi + lo pairs: three MFMAs per product,
+        near-fp32) or 'fp32' (the reference's own precision, models/denoiser.py:37; about a
+        tenth of the fp16 throughput)."""
         code = PRECISIONS[precision] if isinstance(precision, str) else int(precision)
         self._check(self.lib.pnp_set_precision(self.h, code))
         self.precision = code
+
+    def get_precision(self):
+        """(requested, effective) precision names; effective = what the next solver step uses."""
+        r, e = C.c_int(), C.c_int()
+        self._check(self.lib.pnp_get_precision(self.h, C.byref(r), C.byref(e)))
+        return PRECISION_NAMES[r.value], PRECISION_NAMES[e.value]
 
     def set_denoise_chunk(self, images: int):
         """Images per denoiser pass (0 = auto).  Performance only."""

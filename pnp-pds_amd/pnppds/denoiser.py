@@ -15,10 +15,12 @@ from .weights import DenoiserWeights, resolve_weights
 
 
 class Denoiser:
-    def __init__(self, file_name, ch=3, weights: DenoiserWeights | None = None, precision="fp16"):
+    def __init__(self, file_name, ch=3, weights: DenoiserWeights | None = None, precision="auto"):
         self.weights = weights if weights is not None else resolve_weights(file_name, ch)
         self.ch = ch
-        self.precision = precision   # 'fp16' MFMA operands (default) or 'fp32' (the reference's)
+        # 'auto' (default): split fp16 for a single denoiser call (the reference's fp32 to ~2e-7);
+        # 'fp16', 'fp16w2', 'fp16x3' or 'fp32' (Context.set_precision)
+        self.precision = precision
         self.key = ("den", self.weights.name, file_name, id(weights) if weights is not None else 0)
         self.cost = 0
 

@@ -12,9 +12,10 @@ Differences from the reference, by design:
     README names at :183-185); unknown methods raise ValueError.
   * ``phi``/``adj_phi`` must come from pnppds.operators.get_observation_operators (opaque
     Python closures cannot run on the device; there is no host fallback).
-  * state is fp32 on the device (the reference mixes fp32 x and fp64 y); denoiser
-    operands are fp16 with fp32 accumulation, except for the Poisson methods, which run fp32
-    operands (``precision='auto'``; FP32_METHODS below).  Tolerances: DESIGN.md §Parity.
+  * state is fp32 on the device (the reference mixes fp32 x and fp64 y); the denoiser's
+    operands follow ``precision='auto'`` (the library's per-solve policy, PNP_PREC_AUTO in
+    include/pnppds.h): fp16 with fp32 accumulation for ours-A / ours-B on the blur operator,
+    split fp16 (fp16x3, near-fp32) for everything else.  Tolerances: DESIGN.md §Parity.
   * ``ssim`` is computed on the device every iteration (utils_eval.eval_ssim restated;
     skimage is absent here, so its parity is unpinned).
   * comparisonB-4 / comparisonB-5 run with the DnCNN denoiser their text uses; the
@@ -60,24 +61,17 @@ def make_params(gamma1, gamma2, alpha_s, alpha_n, myLambda, m1, m2, gammaInADMMS
 
 BM3D_METHODS = ("A-PnPPDS-BM3D", "A-PnPFBS-BM3D", "comparisonB-1", "C-PnPPDS-BM3D")
 
-# Denoiser operand precision per method when precision="auto" (the default).  Measured against
-# the reference's own trajectories (tests/test_gpu_long.py): with fp16 operands
-# ours-A stays within 0.0043 dB over the 1200 iterations of a blur experiment and ours-B within
-# 0.0006 dB over 300, but the Poisson method drifts (ours-C, random sampling, gamma1 = 0.00035:
-# 0.008 dB at 300 iterations, 0.19 dB at the 3000 that main.py:136-139 runs), because its tiny
-# primal steps integrate the fp16 denoiser's deterministic error through the dual.  Splitting
-# the weights into fp16 hi + lo halves ('fp16w2') removes the weight rounding that drives the
-# early drift (0.0008 dB at 1500 iterations) but not the fp16 activations' noise floor, which
-# still costs 0.10 dB by iteration 2200 while the reference converges.  fp32 operands hold
-# every case to <= 0.00013 dB, so the Poisson-family methods default to them.
-FP32_METHODS = (_lib.METHOD_C, _lib.METHOD_C_PNPADMM, _lib.METHOD_C_RED)
-
-
-def resolve_precision(precision, method_code: int) -> str:
-    if precision == "auto":
-        return "fp32" if method_code in FP32_METHODS else "fp16"
+# Denoiser operand precision.  'auto' (the default) leaves the choice to the library, per solve
+# (include/pnppds.h PNP_PREC_AUTO, capi.hip auto_precision), from the reference's own long
+# trajectories (tests/test_gpu_long.py): fp16 operands hold every iteration
+# within 0.01 dB only for ours-A / ours-B on the blur operator (0.0043 dB over 1200 blur
+# iterations at sigma 0.01, 0.0023 at 0.0025); on Id and random sampling (42-50 dB
+# restorations: gray Id 0.067 dB, A random sampling 0.05-0.11 dB over 3000) and for the Poisson
+# method (0.19 dB) they do not, and those run split fp16 (fp16x3: activations and weights as
+# fp16 hi + lo pairs, three MFMAs per product; <= 0.002 dB on every long golden).
+def resolve_precision(precision, method_code: int | None = None) -> str:
     if precision not in _lib.PRECISIONS:
-        raise ValueError(f"precision must be 'auto', 'fp16', 'fp16w2' or 'fp32', not {precision!r}")
+        raise ValueError(f"precision must be one of {sorted(_lib.PRECISIONS)}, not {precision!r}")
     return precision
 
 
@@ -114,8 +108,9 @@ def test_iter_batch(x_0, x_obsrv, x_true, phi, adj_phi, gamma1, gamma2, alpha_s,
     avg_time).  ssim is computed on the device each iteration (iteration.py:189) when record_ssim;
     C == 1 batches are scored as the reference's (H, W) grayscale arrays.  precision: the
     denoiser's MFMA operands, 'fp16', 'fp16w2' (split weights, two MFMAs per product), 'fp32'
-    (the reference's, about 10x slower) or 'auto' (default: fp32 for the Poisson methods, fp16
-    otherwise; FP32_METHODS)."""
+    (the reference's, about 10x slower), 'fp16x3' (split fp16: hi + lo activations and weights,
+    three MFMAs per product, near-fp32) or 'auto' (default: the library's per-solve policy,
+    fp16 for ours-A/B on blur and fp16x3 otherwise)."""
     m = resolve_method(method)
     _check_ops(phi, adj_phi)
     x0 = np.asarray(x_0)
@@ -142,7 +137,7 @@ def test_iter(x_0, x_obsrv, x_true, phi, adj_phi, gamma1, gamma2, alpha_s, alpha
               gammaInADMMStep1, gaussian_nl, sp_nl, poisson_alpha, path_prox, max_iter, method="A-Proposed",
               ch=3, r=1, *, precision="auto"):
     """iteration.py:10 signature; x_0 etc. are (C,H,W) (RGB) or (H,W) (gray).  Keyword-only
-    extension: precision ('auto' default, 'fp16', 'fp32'; see test_iter_batch)."""
+    extension: precision ('auto' default, 'fp16', 'fp16w2', 'fp16x3', 'fp32'; see test_iter_batch)."""
     x0 = np.asarray(x_0)
     shp = x0.shape
     to4 = (lambda a: np.asarray(a).reshape((1, 1) + shp)) if x0.ndim == 2 else \

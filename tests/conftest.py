@@ -37,5 +37,6 @@ def gpu_ctx():
     """One device context for the whole GPU session (tests run in one process)."""
     from pnppds import _lib
     ctx = _lib.Context(0)
+    ctx.set_precision("fp16")   # the denoiser tests on this context target the fp16 path unless they set another
     yield ctx
     ctx.close()

@@ -281,7 +281,10 @@ LONG_CASES = [
     # the lowest noise level of the grid (main.py:130), blur and random sampling
     ("A_blur_s0025_1200", "A-Proposed", "blur",       3, 128, 0.0025, 0.0, False, 0.99,  0.99,        0.95, 1.0,  1.0, 0.8, 1200),
     ("A_rs_s0025_3000", "A-Proposed", "random_sampling", 3, 128, 0.0025, 0.0, False, 0.99, 0.99,      0.95, 1.0,  1.0, 0.8, 3000),
+    # comparisonB-2 (BASELINE config 5's method) at its config's inner counts m1 = 35, m2 = 5
+    ("ADMM_B2_30",   "comparisonB-2", "blur",         3, 128, 0.01, 0.1, False, 0.99,    0.99,        0.95, 0.95, 1.0, 0.8, 30),
 ]
+LONG_INNER = {"ADMM_B2_30": (35, 5)}     # (m1, m2) where not the default 15, 15
 
 
 def make_long_golden(ref_root="/root/reference", only=None):
@@ -305,14 +308,15 @@ def make_long_golden(ref_root="/root/reference", only=None):
             xt = xt[0]                      # the reference's grayscale images are (H, W)
         obs, x0 = degrade(xt, phi, Id, deg, sig, sp, pois, 300)
         arch = f"DnCNN_nobn_nch_{ch}_nlev_0.01"
+        m1, m2 = LONG_INNER.get(name, (15, 15))
         t = time.perf_counter()
-        res = iteration.test_iter(x0, obs, xt, phi, adj, g1, g2, as_, an, lam, 15, 15, 0.1, sig, sp, 300,
+        res = iteration.test_iter(x0, obs, xt, phi, adj, g1, g2, as_, an, lam, m1, m2, 0.1, sig, sp, 300,
                                   os.path.join(nn_dir, arch + ".pth"), iters, method, ch, r)
         xs, ss, c, ps, _ssim, _t = res
         small = (lambda a: np.asarray(a, np.float32)) if n >= 256 else np.asarray   # fixture size
         np.savez_compressed(os.path.join(HERE, f"long_{name}.npz"), x_true=xt, x_obs=small(obs),
                             x_0=small(x0), x_out=np.asarray(xs).astype(np.float16), c=c, psnr=ps,
-                            params=np.array([g1, g2, as_, an, lam, 15, 15, 0.1, sig, sp, 300, iters, ch, r]),
+                            params=np.array([g1, g2, as_, an, lam, m1, m2, 0.1, sig, sp, 300, iters, ch, r]),
                             method=np.array(method), deg_op=np.array(deg), arch=np.array(arch))
         print(f"long_{name}.npz psnr {ps[0]:.3f} -> {ps[-1]:.3f} ({time.perf_counter()-t:.1f}s)", flush=True)
 

@@ -13,13 +13,13 @@ pytestmark = pytest.mark.gpu
 def _setup(case, B):
     from pnppds import _lib
     from pnppds import operators as ops
-    from pnppds.iteration import make_params, resolve_method, resolve_precision
+    from pnppds.iteration import make_params, resolve_method
     from pnppds.weights import resolve_weights
     g = load_golden(f"iter_{case}.npz")
     g1, g2, as_, an, lam, m1, m2, gadmm, sig, sp, palpha, iters, ch, r = g["params"]
     ctx = _lib.Context(0)
     m = resolve_method(str(g["method"]))
-    ctx.set_precision(resolve_precision("auto", m))
+    ctx.set_precision("auto")
     ctx.set_denoiser(resolve_weights(str(g["arch"]), int(ch)))
     phi, _ = ops.get_observation_operators(str(g["deg_op"]), "blur_1", r)
     phi.configure(ctx, g["x_0"].shape[-2], g["x_0"].shape[-1])
