@@ -779,14 +779,16 @@ void graph_build(pnp_ctx* ctx) {
 // n iterations: plain steps until the state is warm (no allocation pending) and x sits in
 // buffer 0, then graph replays of two iterations, then a plain step for an odd remainder.
 // PNP_PREC_AUTO: fp16 operands where the reference's long trajectories show
-// them within 0.01 dB — ours-A / ours-B on the blur operator (A blur 1200 iterations at
-// sigma 0.01 and 0.0025: 0.0043 / 0.0023 dB; B blur: 0.0005) — and split fp16 (fp16x3, three
-// MFMAs per product, near-fp32) everywhere else: the Id and random-sampling operators, whose
-// restorations reach 42-50 dB (fp16: gray Id 0.067 dB at 23 iterations, A random sampling
+// them within 0.01 dB — ours-A / ours-B / comparisonB-2 on the blur operator (A blur 1200
+// iterations at sigma 0.01 and 0.0025: 0.0043 / 0.0023 dB; B blur 300: 0.0005; comparisonB-2
+// at m1 = 35, m2 = 5, 30 outer iterations: 0.0039) — and split fp16 (fp16x3, three MFMAs per
+// product, near-fp32) everywhere else: the Id and random-sampling operators, whose
+// restorations reach 42-50 dB (fp16: gray Id 256^2 0.037 dB over 1200, A random sampling
 // 0.051 dB at sigma 0.01 and 0.113 at 0.0025 over 3000), the Poisson methods (ours-C: 0.19 dB
-// over 3000) and every comparison method (no long-trajectory evidence for fp16).
+// over 3000) and the other comparison methods (no long-trajectory evidence for fp16).
 int auto_precision(int method, int op_kind) {
-  if ((method == PNP_METHOD_A || method == PNP_METHOD_B) && op_kind == PNP_OP_BLUR) return PNP_PREC_FP16;
+  if ((method == PNP_METHOD_A || method == PNP_METHOD_B || method == PNP_METHOD_ADMM_B2) && op_kind == PNP_OP_BLUR)
+    return PNP_PREC_FP16;
   return PNP_PREC_FP16X3;
 }
 

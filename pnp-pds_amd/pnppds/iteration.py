@@ -14,7 +14,7 @@ Differences from the reference, by design:
     Python closures cannot run on the device; there is no host fallback).
   * state is fp32 on the device (the reference mixes fp32 x and fp64 y); the denoiser's
     operands follow ``precision='auto'`` (the library's per-solve policy, PNP_PREC_AUTO in
-    include/pnppds.h): fp16 with fp32 accumulation for ours-A / ours-B on the blur operator,
+    include/pnppds.h): fp16 with fp32 accumulation for ours-A / ours-B / comparisonB-2 on the blur operator,
     split fp16 (fp16x3, near-fp32) for everything else.  Tolerances: DESIGN.md §Parity.
   * ``ssim`` is computed on the device every iteration (utils_eval.eval_ssim restated;
     skimage is absent here, so its parity is unpinned).
@@ -64,8 +64,8 @@ BM3D_METHODS = ("A-PnPPDS-BM3D", "A-PnPFBS-BM3D", "comparisonB-1", "C-PnPPDS-BM3
 # Denoiser operand precision.  'auto' (the default) leaves the choice to the library, per solve
 # (include/pnppds.h PNP_PREC_AUTO, capi.hip auto_precision), from the reference's own long
 # trajectories (tests/test_gpu_long.py): fp16 operands hold every iteration
-# within 0.01 dB only for ours-A / ours-B on the blur operator (0.0043 dB over 1200 blur
-# iterations at sigma 0.01, 0.0023 at 0.0025); on Id and random sampling (42-50 dB
+# within 0.01 dB only for ours-A / ours-B / comparisonB-2 on the blur operator (0.0043 dB over
+# 1200 blur iterations at sigma 0.01, 0.0023 at 0.0025; comparisonB-2 0.0039 over 30 outer); on Id and random sampling (42-50 dB
 # restorations: gray Id 0.067 dB, A random sampling 0.05-0.11 dB over 3000) and for the Poisson
 # method (0.19 dB) they do not, and those run split fp16 (fp16x3: activations and weights as
 # fp16 hi + lo pairs, three MFMAs per product; <= 0.002 dB on every long golden).
@@ -110,7 +110,7 @@ def test_iter_batch(x_0, x_obsrv, x_true, phi, adj_phi, gamma1, gamma2, alpha_s,
     denoiser's MFMA operands, 'fp16', 'fp16w2' (split weights, two MFMAs per product), 'fp32'
     (the reference's, about 10x slower), 'fp16x3' (split fp16: hi + lo activations and weights,
     three MFMAs per product, near-fp32) or 'auto' (default: the library's per-solve policy,
-    fp16 for ours-A/B on blur and fp16x3 otherwise)."""
+    fp16 for ours-A/B and comparisonB-2 on blur, fp16x3 otherwise)."""
     m = resolve_method(method)
     _check_ops(phi, adj_phi)
     x0 = np.asarray(x_0)

@@ -49,10 +49,12 @@ def run_long(g, precision=None):
                                             ("A_gray_id_1200", "auto"), ("A_rs_3000", "auto"),
                                             ("A_blur_s0025_1200", "auto"), ("A_rs_s0025_3000", "auto"),
                                             ("A_gray_id_1200", "fp16x3"), ("A_rs_3000", "fp16x3"),
-                                            ("A_blur_s0025_1200", "fp16x3"), ("A_rs_s0025_3000", "fp16x3")])
+                                            ("A_blur_s0025_1200", "fp16x3"), ("A_rs_s0025_3000", "fp16x3"),
+                                            # comparisonB-2 at config 5's inner counts (m1 = 35, m2 = 5)
+                                            ("ADMM_B2_30", "auto")])
 def test_long_trajectory_psnr(case, precision):
     """Every iteration's PSNR within 0.01 dB of the reference's trajectory.  'auto' is the
-    default precision policy (PNP_PREC_AUTO: fp16 operands for ours-A/B on blur, split fp16
+    default precision policy (PNP_PREC_AUTO: fp16 operands for ours-A/B and comparisonB-2 on blur, split fp16
     elsewhere; with fp16 ones ours-C drifts 0.19 dB over 3000 iterations and ours-A on random
     sampling 0.05-0.11 dB)."""
     g = load_golden(f"long_{case}.npz")
