@@ -197,6 +197,9 @@ int pnp_op_proj_l1_ball(pnp_ctx* ctx, const float* x, float* out, int B, int64_t
 int pnp_op_prox_gkl(pnp_ctx* ctx, const float* x, const float* x0, float* out, int64_t count,
                     double gamma, double alpha, void* stream);
 int pnp_op_denoise(pnp_ctx* ctx, const float* x, float* out, int B, int C, int H, int W, void* stream);
+/* dst = src on the device (float4 streaming copy; 16-B aligned, bytes % 16 == 0).  The
+ * measured copy ceiling bench.py reports the prox passes' HBM fraction against.        */
+int pnp_device_copy(pnp_ctx* ctx, void* dst, const void* src, size_t bytes, void* stream);
 /* psnr_out: host array of B doubles (synchronous). */
 int pnp_op_psnr(pnp_ctx* ctx, const float* x_true, const float* x, int B, int64_t n, double* psnr_out,
                 void* stream);

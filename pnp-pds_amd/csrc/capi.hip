@@ -1461,6 +1461,16 @@ int pnp_op_denoise(pnp_ctx* ctx, const float* x, float* out, int B, int C, int H
   });
 }
 
+int pnp_device_copy(pnp_ctx* ctx, void* dst, const void* src, size_t bytes, void* stream) {
+  if (!ctx) return PNP_E_ARG;
+  return guarded(ctx, [&] {
+    if (!dst || !src || bytes % 16 || ((uintptr_t)dst | (uintptr_t)src) % 16)
+      fail(ctx, PNP_E_ARG, "copy needs 16-B aligned pointers and a multiple of 16 bytes");
+    launch_copy_f4(src, dst, bytes, ctx->num_cus, pick_stream(ctx, stream));
+    check_launch(ctx, "copy_f4");
+  });
+}
+
 int pnp_op_psnr(pnp_ctx* ctx, const float* x_true, const float* x, int B, int64_t n, double* psnr_out,
                 void* stream) {
   if (!ctx) return PNP_E_ARG;

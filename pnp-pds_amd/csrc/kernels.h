@@ -171,5 +171,7 @@ void launch_metrics(const float* xn, const float* xo, const float* xt, double* p
 void launch_it_advance(int* itp, hipStream_t st);
 void launch_pack_input(const float* x, float* u32, int B, int C, int H, int W, int clamp_in,
                        hipStream_t st);
+// dst = src, bytes a multiple of 16 (16-B aligned pointers): float4 streaming copy
+void launch_copy_f4(const void* src, void* dst, size_t bytes, int num_cus, hipStream_t st);
 
 }  // namespace pnp

@@ -1813,6 +1813,31 @@ void launch_gkl(const float* x, const float* x0, float* out, size_t count, doubl
   hipLaunchKernelGGL(gkl_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, x0, out, count, gamma, alpha);
 }
 
+// Streaming copy (bench.py's measured copy ceiling for the prox passes' HBM fraction): every
+// thread moves 4 x 16 B per step, all four loads in flight before the stores, grid-strided.
+__global__ __launch_bounds__(256) void copy_f4_kernel(const floatx4* __restrict__ src, floatx4* __restrict__ dst,
+                                                      size_t n4) {
+  const size_t stride = (size_t)gridDim.x * 256 * 4;
+  for (size_t i = (size_t)blockIdx.x * 1024 + threadIdx.x; i < n4; i += stride) {
+    floatx4 v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (i + 256 * k < n4) v[k] = src[i + 256 * k];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (i + 256 * k < n4) dst[i + 256 * k] = v[k];
+  }
+}
+
+void launch_copy_f4(const void* src, void* dst, size_t bytes, int num_cus, hipStream_t st) {
+  const size_t n4 = bytes / 16;
+  size_t blocks = (n4 + 1023) / 1024;
+  const size_t cap = (size_t)num_cus * 8;
+  if (blocks > cap) blocks = cap;
+  if (blocks == 0) return;
+  hipLaunchKernelGGL(copy_f4_kernel, dim3((unsigned)blocks), dim3(256), 0, st, (const floatx4*)src, (floatx4*)dst, n4);
+}
+
 void launch_pack_input(const float* x, float* u32, int B, int C, int H, int W, int clamp_in, hipStream_t st) {
   const size_t total = (size_t)B * C * H * W;
   size_t blocks = (total + 255) / 256;

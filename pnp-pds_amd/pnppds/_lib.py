@@ -69,6 +69,7 @@ _SIGS = {
     "pnp_set_denoiser": ([_P, C.c_int, C.c_int, C.c_int, _F, C.c_size_t, C.c_int, C.c_int, C.c_int], C.c_int),
     "pnp_set_precision": ([_P, C.c_int], C.c_int),
     "pnp_get_precision": ([_P, C.POINTER(C.c_int), C.POINTER(C.c_int)], C.c_int),
+    "pnp_device_copy": ([_P, _P, _P, C.c_size_t, _P], C.c_int),
     "pnp_set_tuning": ([_P, C.c_int, C.c_int], C.c_int),
     "pnp_set_operator": ([_P, C.c_int, _D, C.c_int, C.c_int, C.POINTER(C.c_uint8), C.c_int, C.c_int], C.c_int),
     "pnp_run": ([_P, C.c_int, C.POINTER(pnp_params), C.c_int, C.c_int, C.c_int, C.c_int, _F, _F, _F, C.c_int,
@@ -347,6 +348,10 @@ class Context:
 
     def op_denoise(self, x, out, B, Cc, H, W, stream=None):
         self._check(self.lib.pnp_op_denoise(self.h, _P(x), _P(out), B, Cc, H, W, _P(stream) if stream else None))
+
+    def device_copy(self, dst, src, nbytes, stream=None):
+        """dst = src (device pointers): the float4 streaming copy bench.py measures."""
+        self._check(self.lib.pnp_device_copy(self.h, _P(dst), _P(src), nbytes, _P(stream) if stream else None))
 
     def op_psnr(self, xt, x, B, n, stream=None):
         out = np.empty(B, np.float64)

@@ -50,8 +50,9 @@ def _run(xt, xobs64, x0, phi, adj, prm, iters, method, r, sl=slice(None)):
 
 
 def test_cfg3_ours_b_blur_sparse_batch64():
-    """cfg3: batch 64, RGB 256x256, blur + Gaussian 0.01 + salt-and-pepper 0.1, ours-B."""
-    B, H, iters, r = 64, 256, 4, 0.8
+    """cfg3: batch 64, RGB 256x256, blur + Gaussian 0.01 + salt-and-pepper 0.1, ours-B; image 0
+    against the oracle every iteration for 60 iterations."""
+    B, H, iters, r = 64, 256, 60, 0.8
     prm = (1.0, 0.49, 0.95, 0.95, 1.0, 15, 15, 0.1, 0.01, 0.1, 300.0)   # param_memo.py:44
     xt = _synthetic(B, H, H, seed=3)
     phi, adj, xobs, x0 = _observe(xt, "blur", r, 0.01, 0.1, False, 300.0)
@@ -75,8 +76,8 @@ def test_cfg3_ours_b_blur_sparse_batch64():
 
 def test_cfg4_ours_c_random_sampling_poisson_512():
     """cfg4: RGB 512x512, random_sampling r=0.8 + Poisson alpha=300, ours-C; one GPU's shard
-    of the 8-GPU batch of 256 (32 images)."""
-    B, H, iters, r = 32, 512, 3, 0.8
+    of the 8-GPU batch of 256 (32 images); image 0 against the oracle for 50 iterations."""
+    B, H, iters, r = 32, 512, 50, 0.8
     prm = (0.00035, 1 / 0.00035, 1.0, 1.0, 1.0, 15, 15, 0.1, 0.0, 0.0, 300.0)   # param_memo.py:92
     xt = _synthetic(B, H, H, seed=4)
     phi, adj, xobs, x0 = _observe(xt, "random_sampling", r, 0.0, 0.0, True, 300.0)
@@ -114,3 +115,18 @@ def test_cfg5_admm_blur_sparse_1024():
     np.testing.assert_allclose(pb[0], po, atol=0.01)
     np.testing.assert_allclose(xb[0], xo, atol=5e-3)
     np.testing.assert_allclose(sb[0], so, atol=5e-3)
+
+
+def test_cfg5_admm_full_inner_counts_256_crop():
+    """cfg5's method at its own inner counts (m1 = 35 denoiser x-steps, m2 = 5 l1 s-steps,
+    admm.py:30-44) for one outer iteration on a 256^2 crop, against the oracle."""
+    H, r = 256, 0.8
+    prm = (0.99, 0.99, 0.95, 0.95, 1.0, 35, 5, 0.1, 0.01, 0.1, 300.0)
+    xt = np.ascontiguousarray(_synthetic(1, 1024, 1024, seed=5)[:, :, :H, :H])
+    phi, adj, xobs, x0 = _observe(xt, "blur", r, 0.01, 0.1, False, 300.0)
+    x, s, c, psnr, _, _ = _run(xt, xobs, x0, phi, adj, prm, 1, "comparisonB-2", r)
+    xo, so, co, po, _, _ = _oracle_image0(xt, xobs, "blur", r, prm, 1, "comparisonB-2")
+    print(f"cfg5 crop m1=35 m2=5: |dPSNR| {abs(psnr[0, 0] - po[0]):.5f} dB, max|dx| {np.abs(x[0] - xo).max():.2e}")
+    np.testing.assert_allclose(psnr[0], po, atol=0.01)
+    np.testing.assert_allclose(x[0], xo, atol=5e-3)
+    np.testing.assert_allclose(s[0], so, atol=5e-3)
