@@ -139,9 +139,11 @@ int pnp_get_precision(pnp_ctx* ctx, int* requested, int* effective);
  * activation ping-pong pair would exceed an eighth of the device's memory; then equal passes). */
 enum pnp_tuning_key {
   PNP_TUNE_DENOISE_CHUNK = 1,
-  PNP_TUNE_BODY_LAYERS = 2,  /* 64->64 layers per launch: 0 = auto (default: 2 when the batch has
-                                at least one 32-column strip per CU, else 1), 1 (conv_body_v3)
-                                or 2 (conv_body_f2, the intermediate stays in LDS).
+  PNP_TUNE_BODY_LAYERS = 2,  /* 64->64 layers per launch: 0 = auto (default: all of them in one
+                                persistent launch when the batch has at most 2 tiles per CU,
+                                e.g. one 256^2 image; else 2 when it has at least one 32-column
+                                strip per CU, else 1), 1 (conv_body_v3), 2 (conv_body_f2, the
+                                intermediate stays in LDS) or 3 (all: conv_stack16).
                                 Bit-identical results.                                         */
   PNP_TUNE_GRAPH = 3          /* 1: iteration launches replayed from a hipGraph (two iterations
                                 per replay, methods A/B/C); 0: direct launches (default).

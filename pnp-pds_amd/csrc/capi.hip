@@ -50,7 +50,7 @@ struct pnp_ctx {
   int den_C = 0, den_depth = 0, den_act = 0, den_residual = 1, den_clamp = 1;
   int den_chunk = 0;   // images per denoiser pass; 0 = auto
   int ablate = 0;         // PNP_PROFILING build only: parts of conv_body_v3 skipped, results wrong
-  int body_layers = 0;    // PNP_TUNE_BODY_LAYERS: 0 auto (use_pair), 1 conv_body_v3, 2 conv_body_f2
+  int body_layers = 0;    // PNP_TUNE_BODY_LAYERS: 0 auto, 1 conv_body_v3, 2 conv_body_f2, 3 conv_stack16
   bool den_ready = false;
   int prec_req = PNP_PREC_AUTO;   // pnp_set_precision (default: the per-solve policy, auto_precision)
   int prec = PNP_PREC_FP16X3;     // the operands the denoiser runs with now (resolved from prec_req)
@@ -100,6 +100,11 @@ struct pnp_ctx {
   bool capturing = false;      // solver_step is being captured: record unconditionally, itp set
   const int* itp = nullptr;    // device iteration counter the metric kernels read while captured
   DevBuf it_dev;
+
+  // persistent small-batch denoiser (conv_stack16): per-tile progress words, one array for the
+  // solver's stream and one for the single ops (concurrent launches must not share them)
+  DevBuf stack_done, scr_stack_done, stack_err;
+  int stack_epoch = 0, scr_stack_epoch = 0;
 
   // profiling
   bool prof = false;
@@ -276,6 +281,39 @@ bool use_pair(pnp_ctx* ctx, int mb, int W) {
   return strips >= cus && strips * 5 >= rounds * cus * 4;
 }
 
+// All body layers in one persistent launch (conv_stack16) for small batches: at most 2 tiles
+// of 8 x 32 per CU (B = 1 at 256^2: 256 tiles), where per-layer launches are fixed-cost-bound
+// (~11 us each for ~2 us of MFMA work).  Not while a graph is captured: the launch's epoch tag
+// is a kernel argument, which a replay would repeat.
+bool use_stack(pnp_ctx* ctx, int tiles) {
+  if (ctx->capturing) return false;
+  if (ctx->body_layers) return ctx->body_layers == 3;
+  return tiles <= 2 * ctx->num_cus;
+}
+
+// The progress words and this launch's epoch (advanced by nbody + 1 per launch; the words are
+// reset before the tag could wrap).
+int* stack_flags(pnp_ctx* ctx, bool solver, int tiles, int nbody, hipStream_t st, int& epoch) {
+  DevBuf& d = solver ? ctx->stack_done : ctx->scr_stack_done;
+  int& e = solver ? ctx->stack_epoch : ctx->scr_stack_epoch;
+  if (!d.p || d.bytes < (size_t)tiles * sizeof(int)) {
+    ensure(ctx, d, (size_t)std::max(tiles, 4096) * sizeof(int));
+    HIPCHK(ctx, hipMemsetAsync(d.p, 0, d.bytes, st));
+    e = 0;
+  }
+  if (!ctx->stack_err.p) {
+    ensure(ctx, ctx->stack_err, sizeof(int));
+    HIPCHK(ctx, hipMemsetAsync(ctx->stack_err.p, 0, sizeof(int), st));
+  }
+  if (e > (1 << 30)) {
+    HIPCHK(ctx, hipMemsetAsync(d.p, 0, d.bytes, st));
+    e = 0;
+  }
+  epoch = e + 1;
+  e += nbody + 1;
+  return P<int>(d);
+}
+
 // Images per denoiser pass.  The two ping-pong activation buffers may take an eighth of the
 // card's HBM (36 GB of the MI355X's 288 GB: cfg5's 64 x 1024^2 shard, 17.3 GB, is one pass),
 // and a batch that needs several passes is split into equal ones: a small remainder pass
@@ -364,7 +402,18 @@ void run_denoiser(pnp_ctx* ctx, const float* u32, float* xout, DevBuf (&act)[2],
         check_launch(ctx, "conv_head");
       }
       int cur = 0;
-      for (int l = 0; l < ctx->den_depth - 2; ++l, cur ^= 1) {
+      const int nbody = ctx->den_depth - 2;
+      if (nbody > 0 && use_stack(ctx, s3_tiles(s))) {   // every body layer in one launch
+        ProfScope ps(ctx, "conv_stack_s3", st);
+        int epoch = 0;
+        int* done = stack_flags(ctx, &act[0] == &ctx->act[0], s3_tiles(s), nbody, st, epoch);
+        launch_conv_stack_s3(P<half_t>(act[0]), P<half_t>(alo[0]), P<half_t>(act[1]), P<half_t>(alo[1]),
+                             ctx->body_s3h.p, ctx->body_s3l.p, P<float>(ctx->body_b), nbody, s, ctx->den_act,
+                             ctx->num_cus, done, epoch, P<int>(ctx->stack_err), st);
+        check_launch(ctx, "conv_stack_s3");
+        cur = nbody & 1;
+      }
+      for (int l = (nbody > 0 && use_stack(ctx, s3_tiles(s))) ? nbody : 0; l < nbody; ++l, cur ^= 1) {
         ProfScope ps(ctx, "conv_body_s3", st);
         launch_conv_s3_body(P<half_t>(act[cur]), P<half_t>(alo[cur]), P<half_t>(act[cur ^ 1]), P<half_t>(alo[cur ^ 1]),
                             (const char*)ctx->body_s3h.p + (size_t)l * kBodyWBytes,
@@ -396,7 +445,17 @@ void run_denoiser(pnp_ctx* ctx, const float* u32, float* xout, DevBuf (&act)[2],
     int cur = 0;
     const int nbody = ctx->den_depth - 2;
     const bool pair = use_pair(ctx, mb, W);
-    for (int l = 0; l < nbody;) {
+    const bool stack = !w2 && !ctx->ablate && nbody > 0 && use_stack(ctx, s.tiles);
+    if (stack) {                                 // every body layer in one launch
+      ProfScope ps(ctx, "conv_stack16", st);
+      int epoch = 0;
+      int* done = stack_flags(ctx, &act[0] == &ctx->act[0], s.tiles, nbody, st, epoch);
+      launch_conv_stack16(P<half_t>(act[0]), P<half_t>(act[1]), ctx->body_w.p, P<float>(ctx->body_b), nbody, s,
+                          ctx->den_act, ctx->num_cus, done, epoch, P<int>(ctx->stack_err), st);
+      check_launch(ctx, "conv_stack16");
+      cur = nbody & 1;
+    }
+    for (int l = stack ? nbody : 0; l < nbody;) {
       const char* wl = (const char*)ctx->body_w.p + (size_t)l * kBodyWBytes;
       const float* bl = P<float>(ctx->body_b) + l * kWidth;
       if (!w2 && pair && !ctx->ablate && l + 1 < nbody) {   // layers l, l+1 in one launch
@@ -911,10 +970,23 @@ void solver_reset_state(pnp_ctx* ctx) {
   ctx->loaded = true;
 }
 
+// A persistent denoiser whose neighbour wait hit its spin bound (a workgroup never became
+// resident): the results are wrong, so the fetch fails loudly instead of returning them.
+void check_stack_err(pnp_ctx* ctx) {
+  if (!ctx->stack_err.p) return;
+  int e = 0;
+  HIPCHK(ctx, hipMemcpy(&e, ctx->stack_err.p, sizeof(int), hipMemcpyDeviceToHost));
+  if (e) {
+    HIPCHK(ctx, hipMemset(ctx->stack_err.p, 0, sizeof(int)));
+    fail(ctx, PNP_E_INTERNAL, "persistent denoiser: a tile's neighbour wait timed out (results invalid)");
+  }
+}
+
 void solver_fetch(pnp_ctx* ctx, float* x_out, float* s_out, double* c_out, double* psnr_out, double* ssim_out) {
   if (!ctx->loaded) fail(ctx, PNP_E_STATE, "solver not loaded");
   const size_t N = (size_t)ctx->B * ctx->C * ctx->H * ctx->W;
   HIPCHK(ctx, hipStreamSynchronize(ctx->stream));
+  check_stack_err(ctx);
   if (x_out) HIPCHK(ctx, hipMemcpy(x_out, ctx->x[ctx->cur].p, N * sizeof(float), hipMemcpyDeviceToHost));
   if (s_out) {
     HIPCHK(ctx, hipMemcpy(s_out, ctx->s.p, N * sizeof(float), hipMemcpyDeviceToHost));
@@ -998,6 +1070,7 @@ int pnp_destroy(pnp_ctx* ctx) {
                     &ctx->partials, &ctx->metrics, &ctx->theta, &ctx->scr_u32,
                     &ctx->scr_act[0], &ctx->scr_act[1], &ctx->scr_part, &ctx->scr_theta,
                     &ctx->act_lo[0], &ctx->act_lo[1], &ctx->scr_act_lo[0], &ctx->scr_act_lo[1], &ctx->body_s3h, &ctx->body_s3l,
+                    &ctx->stack_done, &ctx->scr_stack_done, &ctx->stack_err,
                     &ctx->z, &ctx->p, &ctx->t, &ctx->dense_fwd, &ctx->dense_adj, &ctx->ssim_scr,
                     &ctx->taps64, &ctx->y1, &ctx->d, &ctx->c1, &ctx->dg_words, &ctx->dg_flag, &ctx->dg_rank, &ctx->dg_scan, &ctx->dg_noise,
                     &ctx->dg_img, &ctx->dg_draws, &ctx->dg_first, &ctx->dg_status,
@@ -1033,7 +1106,7 @@ int pnp_set_tuning(pnp_ctx* ctx, int key, int value) {
       return;
     }
     if (key == PNP_TUNE_BODY_LAYERS) {
-      if (value < 0 || value > 2) fail(ctx, PNP_E_ARG, "body layers per launch must be 0 (auto), 1 or 2");
+      if (value < 0 || value > 3) fail(ctx, PNP_E_ARG, "body layers per launch must be 0 (auto), 1, 2 or 3 (all)");
       ctx->body_layers = value;
       return;
     }

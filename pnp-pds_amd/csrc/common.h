@@ -60,6 +60,33 @@ __device__ __forceinline__ float act_fn(float v, int act) {
   return act == 0 ? (v > 0.f ? v : 0.01f * v) : (v > 0.f ? v : 0.f);
 }
 
+// ---- tile hand-off between workgroups (persistent small-batch denoiser) ------------------
+// A layer's output tile is published with a per-tile progress word: the producer stores the
+// tile with device-scope (sc1) stores, its storing waves drain (s_waitcnt vmcnt(0)), the
+// workgroup barriers, then one lane stores done[t] = value (device scope).  A consumer polls
+// with device-scope loads and then reads the tile with device-scope loads (the per-XCD L2s
+// and per-CU L1s are not coherent with each other: MI355X_MICROARCH.md, inter-workgroup
+// visibility).  Every spin is bounded: a stuck wait sets *err and proceeds (results wrong,
+// no hang).
+constexpr int kTileSpinMax = 1 << 20;   // polls of ~0.1-1 us each: ~0.1-1 s before giving up
+
+__device__ __forceinline__ void tile_publish(int* flag, int value) {
+  __hip_atomic_store(flag, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Wave-level: lanes with want set poll flags[idx] until >= target (wrap-safe); every lane
+// returns after all of them saw it (or the spin bound hit: *err = 1).  Call from one wave,
+// then the workgroup barrier.
+__device__ __forceinline__ void tile_wait(const int* flags, int idx, bool want, int target, int* err) {
+  for (int it = 0; it < kTileSpinMax; ++it) {
+    bool ok = true;
+    if (want) ok = (__hip_atomic_load(flags + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) >= 0;
+    if (__builtin_amdgcn_ballot_w64(!ok) == 0) return;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  if ((threadIdx.x & 63) == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // ---- block reductions ------------------------------------------------------------------
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {

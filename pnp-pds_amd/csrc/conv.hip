@@ -126,6 +126,7 @@ struct RingDma {                                               // one wave's sha
       off[j] = (unsigned)(((pr * s.Wp + pc) * kWidth + c * 8) * 2);
     }
   }
+  template <int CPOL = 0>
   __device__ __forceinline__ void issue(unsigned char* hl, const half_t* __restrict__ in, const ConvShape& s, int t,
                                         int wave) const {
     int b, ty0, tx0;
@@ -140,7 +141,7 @@ struct RingDma {                                               // one wave's sha
       const int g = NW * j + wave;
       if (UNIFORM || g < kDmaSlots - 1 || (g == kDmaSlots - 1 && lane < 32))   // slot 42: pixels 336..339
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(hl + g * 1024), 16,
-                                                 off[j], 0, 0, 0);
+                                                 off[j], 0, 0, CPOL);
     }
   }
 };
@@ -743,6 +744,125 @@ template __global__ void conv_body_w2_kernel<1>(const half_t* __restrict__, half
                                                 const float* __restrict__, ConvShape);
 
 // ------------------------------------------------------------------------------------
+// conv_stack16: every 64 -> 64 body layer of a small batch in ONE launch (fp16 operands).
+// The reference denoises one image per call (main.py:36,69), where each per-layer launch of
+// conv_body_v3 (one 8 x 32 tile per CU at 256^2) spends ~11 us for ~2 us of MFMA work: wave
+// launch, weights into registers, halo DMA, drain.  Here a workgroup keeps its tiles for all
+// layers; layer l + 1 of a tile starts once the 3 x 3 neighbourhood of tiles has published
+// layer l (tile_wait / tile_publish, common.h: agent-scope release / acquire on a per-tile
+// progress word, epoch-tagged per launch so the words are never reset), and the next layer's
+// weights load into the registers right after a layer's last tile is published, in flight
+// while the neighbourhood catches up.  The handed-off activations never sit stale in a cache:
+// the epilogue stores and the halo's LDS-DMA loads are device-scope (sc1), so neither side
+// needs an L2 write-back or invalidate fence (MI355X_MICROARCH.md, inter-workgroup
+// visibility: the sc1 form).  Measured at B = 1 RGB 256^2 (cfg2 iteration, ms): agent-scope
+// release / acquire fences with plain DMA 0.29 (per-layer launches: 0.24); sc1 loads through
+// registers 0.235; sc1 LDS-DMA 0.207.  One wave per SIMD (4 waves): wave w
+// owns channels 32 (w & 1) .. +31 of tile rows 4 (w >> 1) .. +3, i.e. conv_body_w2's tiling
+// on conv_body_v3's fragments (pack_body_weights), so every output is the same MFMA chain and
+// the same fp16 rounding as the per-layer launches: bit-identical (test_gpu_graph.py).  Two
+// 44 KiB halo buffers alternate over a workgroup's tiles.  The grid is at most one workgroup
+// per CU (all resident: the waits only ever point at lower layers, so no cycle) and the host
+// uses it only when the batch has at most 2 tiles per CU.
+// ------------------------------------------------------------------------------------
+constexpr int kStkLds = 2 * kW2Halo;                           // 90112 B
+constexpr int kCpolDevice = 16;                                // sc1: device-scope load / store
+
+template <int ACT>
+__global__ __launch_bounds__(256, 1) void conv_stack16_kernel(half_t* __restrict__ actA, half_t* __restrict__ actB,
+                                                               const uint4* __restrict__ wpk,
+                                                               const float* __restrict__ bias, int nbody,
+                                                               ConvShape s, int* __restrict__ done, int epoch,
+                                                               int* __restrict__ err) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int m = wave & 1, rq = wave >> 1;
+  const int h = lane >> 5, col = lane & 31;
+  auto buf = [&](int i) { return smem + i * kW2Halo; };
+  RingDma<4, true> dma;
+  dma.init(s, wave);
+  const int G = gridDim.x;
+  const int K = (s.tiles - (int)blockIdx.x + G - 1) / G;      // this workgroup's tiles (grid <= tiles)
+
+  half8_t w[kBodyKSteps];
+  float bl[16];
+  auto load_w = [&](int l) {
+    const unsigned char* src = reinterpret_cast<const unsigned char*>(wpk) + (size_t)l * kBodyWBytes;
+#pragma unroll
+    for (int ks = 0; ks < kBodyKSteps; ++ks)
+      w[ks] = *reinterpret_cast<const half8_t*>(src + ((ks * 2 + m) * 64 + lane) * 16);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) bl[r] = bias[l * kWidth + 32 * m + 16 * h + r];
+  };
+  load_w(0);
+  for (int l = 0; l < nbody; ++l) {
+    const half_t* in = (l & 1) ? actB : actA;
+    half_t* out = (l & 1) ? actA : actB;
+    for (int k = 0; k < K; ++k) {
+      const int t = (int)blockIdx.x + k * G;
+      int b, ty0, tx0;
+      decode_tile(t, s, b, ty0, tx0);
+      if (l > 0) {                            // the 3 x 3 neighbourhood has published layer l - 1
+        if (wave == 0) {
+          const int ny = ty0 / kTileH + lane / 3 - 1, nx = tx0 / kTileW + lane % 3 - 1;
+          const bool want = lane < 9 && ny >= 0 && ny < s.tiles_y && nx >= 0 && nx < s.tiles_x;
+          tile_wait(done, want ? (b * s.tiles_y + ny) * s.tiles_x + nx : 0, want, epoch + l, err);
+        }
+        __syncthreads();
+      }
+      dma.template issue<kCpolDevice>(buf(k & 1), in, s, t, wave);   // device scope: never a stale line
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      const unsigned char* hl = buf(k & 1);
+      auto ldB = [&](int ks, int n) {
+        const int tap = ks >> 2, sub = ks & 3;
+        return *reinterpret_cast<const half8_t*>(hl + halo_off(4 * rq + n + tap / 3, col + tap % 3, 2 * sub + h));
+      };
+      floatx16 acc[4];
+      half8_t fb[2][4];
+#pragma unroll
+      for (int n = 0; n < 4; ++n) fb[0][n] = ldB(0, n);
+#pragma unroll
+      for (int ks = 0; ks < kBodyKSteps; ++ks) {
+        const int r = ks & 1;
+        if (ks + 1 < kBodyKSteps) {
+#pragma unroll
+          for (int n = 0; n < 4; ++n) fb[r ^ 1][n] = ldB(ks + 1, n);
+        }
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+          acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(w[ks], fb[r][n], ks == 0 ? floatx16{} : acc[n], 0, 0, 0);
+      }
+      // lane (col, h) holds channels 32m + 16h .. +15 of pixel (row 4rq + n, column col)
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        const int y = ty0 + 4 * rq + n;
+        const half8_t v0 = bias_act8<ACT>(acc[n], 0, bl), v1 = bias_act8<ACT>(acc[n], 8, bl + 8);
+        half_t* row = out + (((size_t)b * s.Hp + y + s.pad) * s.Wp + tx0 + s.pad) * kWidth;
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc(row, (short)0, y < s.H ? min(kTileW, s.W - tx0) * 128 : 0, 0x00020000);
+        const unsigned off = (unsigned)(col * 128 + 64 * m + 32 * h);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i_t, v0), rs, off, 0, kCpolDevice);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i_t, v1), rs, off + 16, 0, kCpolDevice);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's stores done (device scope)
+      __syncthreads();
+      if (tid == 0) tile_publish(done + t, epoch + l + 1);
+    }
+    // the next layer's weights: in flight while the neighbourhood catches up
+    if (l + 1 < nbody) load_w(l + 1);
+  }
+}
+
+template __global__ void conv_stack16_kernel<0>(half_t* __restrict__, half_t* __restrict__, const uint4* __restrict__,
+                                                const float* __restrict__, int, ConvShape, int* __restrict__, int,
+                                                int* __restrict__);
+template __global__ void conv_stack16_kernel<1>(half_t* __restrict__, half_t* __restrict__, const uint4* __restrict__,
+                                                const float* __restrict__, int, ConvShape, int* __restrict__, int,
+                                                int* __restrict__);
+
+// ------------------------------------------------------------------------------------
 // Head layer C -> 64 (basic_models.py:16,27-28).  Input: the fp32 NCHW denoiser input u32
 // (the same buffer the tail's residual reads), converted to fp16 (round to nearest even, as
 // every fp16 cast here) while the halo is written to LDS as one 8-B quad per pixel (channels
@@ -1172,6 +1292,10 @@ hipError_t conv_kernels_init() {
     e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kW2Lds);
     if (e != hipSuccess) return e;
   }
+  for (const void* k : {(const void*)conv_stack16_kernel<0>, (const void*)conv_stack16_kernel<1>}) {
+    e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kStkLds);
+    if (e != hipSuccess) return e;
+  }
   for (const void* k : {(const void*)conv_tail_kernel<false>, (const void*)conv_tail_kernel<true>}) {
     e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kTailLds);
     if (e != hipSuccess) return e;
@@ -1244,6 +1368,17 @@ void launch_conv_body(const half_t* in, half_t* out, const void* w, const float*
   if (act != 0) V3(0, 1);
   else V3(0, 0);
 #undef V3
+}
+
+void launch_conv_stack16(half_t* a, half_t* b, const void* w, const float* bias, int nbody, const ConvShape& s,
+                         int act, int num_cus, int* done, int epoch, int* err, hipStream_t st) {
+  const int grid = s.tiles < num_cus ? s.tiles : num_cus;
+  if (act == 0)
+    hipLaunchKernelGGL((conv_stack16_kernel<0>), dim3(grid), dim3(256), kStkLds, st, a, b, (const uint4*)w, bias, nbody,
+                       s, done, epoch, err);
+  else
+    hipLaunchKernelGGL((conv_stack16_kernel<1>), dim3(grid), dim3(256), kStkLds, st, a, b, (const uint4*)w, bias, nbody,
+                       s, done, epoch, err);
 }
 
 void launch_conv_tail(const half_t* in, const float* xin, float* xout, const void* w, const void* w_lo,

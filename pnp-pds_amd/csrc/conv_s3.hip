@@ -51,6 +51,7 @@ constexpr int kS3KSteps = 18;                           // 9 taps x 2 channel ha
 constexpr int kS3Pieces = 6;                            // DMA pieces per wave per tile (48 / 8)
 
 typedef int v2i_t __attribute__((ext_vector_type(2)));
+typedef int v4i_t __attribute__((ext_vector_type(4)));
 typedef _Float16 h4_t __attribute__((ext_vector_type(4)));
 
 struct S3Geom {
@@ -274,6 +275,167 @@ PNP_S3_INST(0, 1)
 PNP_S3_INST(1, 0)
 #undef PNP_S3_INST
 
+// ------------------------------------------------------------------------------------
+// conv_stack_s3: every body layer of a small batch in ONE launch on split fp16 (the
+// conv_stack16 protocol of conv.hip for conv_s3's tiles and fragments): a workgroup keeps its
+// 8 x 16 tiles for all layers, layer l + 1 of a tile starts once its 3 x 3 neighbourhood has
+// published layer l (common.h tile_wait / tile_publish), and the handed-off hi / lo images are
+// written and read at device scope (sc1 stores and sc1 LDS-DMA into the same swizzled
+// pixel-major image as conv_s3_kernel's).  4 waves, one per SIMD: wave w owns channels 16 w .. +15 of all 8 tile rows
+// (two groups of 4 N-subtiles), the same MFMA chain per output as conv_s3_kernel: bit-identical.
+// ------------------------------------------------------------------------------------
+constexpr int kS3StkLds = 2 * kS3Buf;                   // 98304 B
+constexpr int kS3StkPieces = 12;                        // LDS-DMA pieces per wave per tile (48 / 4)
+constexpr int kCpolDev = 16;                            // sc1: device-scope load / store
+
+template <int ACT>
+__global__ __launch_bounds__(256, 1) void conv_stack_s3_kernel(half_t* __restrict__ aH, half_t* __restrict__ aL,
+                                                                half_t* __restrict__ bH, half_t* __restrict__ bL,
+                                                                const uint4* __restrict__ w_hi,
+                                                                const uint4* __restrict__ w_lo,
+                                                                const float* __restrict__ bias, int nbody, ConvShape s,
+                                                                S3Geom g, int* __restrict__ done, int epoch,
+                                                                int* __restrict__ err) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int mt = wave, px = lane & 15, grp = lane >> 4;
+  const int G = gridDim.x;
+  const int K = (g.tiles - (int)blockIdx.x + G - 1) / G;
+  unsigned lofs[3][2];
+#pragma unroll
+  for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+    for (int hs = 0; hs < 2; ++hs)
+      lofs[dx][hs] = (unsigned)((px + dx) * 128 + 16 * ((4 * hs + grp) ^ s3_swz(px + dx)));
+
+  // DMA: piece q = 4 j + wave (j < 12) covers half q / 24, pixels 8 (q % 24) .. +7 (as conv_s3_kernel)
+  unsigned doff[kS3StkPieces];
+#pragma unroll
+  for (int j = 0; j < kS3StkPieces; ++j) {
+    const int kk = (4 * j + wave) % 24;
+    const int p = min(8 * kk + (lane >> 3), kS3HaloPix - 1);
+    const int pr = p / kS3HaloW, pc = p - pr * kS3HaloW;
+    doff[j] = (unsigned)(((pr * s.Wp + pc) * kWidth + 8 * ((lane & 7) ^ s3_swz(pc))) * 2);
+  }
+  half8_t wH[kS3KSteps], wL[kS3KSteps];
+  float bl[4];
+  auto load_w = [&](int l) {
+#pragma unroll
+    for (int ks = 0; ks < kS3KSteps; ++ks) {
+      const size_t o = (size_t)l * (kBodyWBytes / 16) + (size_t)(ks * 4 + mt) * 64 + lane;
+      wH[ks] = __builtin_bit_cast(half8_t, w_hi[o]);
+      wL[ks] = __builtin_bit_cast(half8_t, w_lo[o]);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bl[i] = bias[l * kWidth + 16 * mt + 4 * grp + i];
+  };
+  load_w(0);
+  for (int l = 0; l < nbody; ++l) {
+    const half_t* inH = (l & 1) ? bH : aH;
+    const half_t* inL = (l & 1) ? bL : aL;
+    half_t* outH = (l & 1) ? aH : bH;
+    half_t* outL = (l & 1) ? aL : bL;
+    for (int k = 0; k < K; ++k) {
+      const int t = (int)blockIdx.x + k * G;
+      int b, ty0, tx0;
+      s3_decode(t, g, b, ty0, tx0);
+      if (l > 0) {
+        if (wave == 0) {
+          const int ny = ty0 / kS3TileH + lane / 3 - 1, nx = tx0 / kS3TileW + lane % 3 - 1;
+          const bool want = lane < 9 && ny >= 0 && ny < g.tiles_y && nx >= 0 && nx < g.tiles_x;
+          tile_wait(done, want ? (b * g.tiles_y + ny) * g.tiles_x + nx : 0, want, epoch + l, err);
+        }
+        __syncthreads();
+      }
+      unsigned char* hb = smem + (k & 1) * kS3Buf;
+      {                                       // halo (hi, lo): device-scope (sc1) LDS-DMA, 12 pieces per wave
+        const size_t base = (((size_t)b * s.Hp + ty0 + s.pad - 1) * s.Wp + tx0 + s.pad - 1) * kWidth;
+        const __amdgpu_buffer_rsrc_t rh =
+            __builtin_amdgcn_make_buffer_rsrc((void*)(inH + base), (short)0, 0x7fffffff, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rl =
+            __builtin_amdgcn_make_buffer_rsrc((void*)(inL + base), (short)0, 0x7fffffff, 0x00020000);
+#pragma unroll
+        for (int j = 0; j < kS3StkPieces; ++j) {
+          const int q = 4 * j + wave, h = q / 24, kk = q - 24 * h;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(h ? rl : rh,
+                                                   (__attribute__((address_space(3))) void*)(hb + h * kS3Half + kk * 1024),
+                                                   16, doff[j], 0, 0, kCpolDev);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __syncthreads();
+#pragma unroll
+      for (int gq = 0; gq < 2; ++gq) {        // tile rows 4 gq .. +3
+        const unsigned char* fb = hb + 4 * gq * kS3HaloW * 128;
+        auto ldB = [&](int ks, int n, int lo) {
+          const int tap = ks >> 1, dy = tap / 3, dx = tap - 3 * dy;
+          return *reinterpret_cast<const half8_t*>(fb + lofs[dx][ks & 1] + lo * kS3Half + (n + dy) * kS3HaloW * 128);
+        };
+        floatx4 acc[4];
+        half8_t bh[2][4], bo[2][4];
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+          bh[0][n] = ldB(0, n, 0);
+          bo[0][n] = ldB(0, n, 1);
+        }
+#pragma unroll
+        for (int ks = 0; ks < kS3KSteps; ++ks) {
+          const int r = ks & 1;
+          if (ks + 1 < kS3KSteps) {
+#pragma unroll
+            for (int n = 0; n < 4; ++n) {
+              bh[r ^ 1][n] = ldB(ks + 1, n, 0);
+              bo[r ^ 1][n] = ldB(ks + 1, n, 1);
+            }
+          }
+#pragma unroll
+          for (int n = 0; n < 4; ++n)
+            acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wH[ks], bh[r][n], ks == 0 ? floatx4{} : acc[n], 0, 0, 0);
+#pragma unroll
+          for (int n = 0; n < 4; ++n) acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wL[ks], bh[r][n], acc[n], 0, 0, 0);
+#pragma unroll
+          for (int n = 0; n < 4; ++n) acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wH[ks], bo[r][n], acc[n], 0, 0, 0);
+        }
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+          const int y = ty0 + 4 * gq + n;
+          h4_t hi, lo;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            float v = acc[n][i] + bl[i];
+            v = ACT == 0 ? fmaxf(v, v * 0.01f) : fmaxf(v, 0.f);
+            hi[i] = (half_t)v;
+            lo[i] = (half_t)(v - (float)hi[i]);
+          }
+          const size_t rowb = (((size_t)b * s.Hp + y + s.pad) * s.Wp + tx0 + s.pad) * kWidth;
+          const int nrec = y < s.H ? min(kS3TileW, s.W - tx0) * 128 : 0;
+          const unsigned off = (unsigned)(px * 128 + (16 * mt + 4 * grp) * 2);
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2i_t, hi),
+                                                __builtin_amdgcn_make_buffer_rsrc(outH + rowb, (short)0, nrec, 0x00020000),
+                                                off, 0, kCpolDev);
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2i_t, lo),
+                                                __builtin_amdgcn_make_buffer_rsrc(outL + rowb, (short)0, nrec, 0x00020000),
+                                                off, 0, kCpolDev);
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) tile_publish(done + t, epoch + l + 1);
+    }
+    if (l + 1 < nbody) load_w(l + 1);
+  }
+}
+
+template __global__ void conv_stack_s3_kernel<0>(half_t* __restrict__, half_t* __restrict__, half_t* __restrict__,
+                                                 half_t* __restrict__, const uint4* __restrict__,
+                                                 const uint4* __restrict__, const float* __restrict__, int, ConvShape,
+                                                 S3Geom, int* __restrict__, int, int* __restrict__);
+template __global__ void conv_stack_s3_kernel<1>(half_t* __restrict__, half_t* __restrict__, half_t* __restrict__,
+                                                 half_t* __restrict__, const uint4* __restrict__,
+                                                 const uint4* __restrict__, const float* __restrict__, int, ConvShape,
+                                                 S3Geom, int* __restrict__, int, int* __restrict__);
+
 S3Geom s3_geom(const ConvShape& s) {
   S3Geom g;
   g.tiles_x = (s.W + kS3TileW - 1) / kS3TileW;
@@ -295,6 +457,10 @@ hipError_t conv_s3_kernels_init() {
   for (const void* k : {(const void*)conv_s3_kernel<0, 0>, (const void*)conv_s3_kernel<0, 1>,
                         (const void*)conv_s3_kernel<1, 0>}) {
     hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kS3Lds);
+    if (e != hipSuccess) return e;
+  }
+  for (const void* k : {(const void*)conv_stack_s3_kernel<0>, (const void*)conv_stack_s3_kernel<1>}) {
+    hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kS3StkLds);
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
@@ -339,6 +505,21 @@ void launch_conv_s3_tail(const half_t* in_hi, const half_t* in_lo, const float* 
   const int grid = g.tiles < num_cus ? g.tiles : num_cus;
   hipLaunchKernelGGL((conv_s3_kernel<1, 0>), dim3(grid), dim3(512), kS3Lds, st, in_hi, in_lo, nullptr, nullptr,
                      (const uint4*)w_hi, (const uint4*)w_lo, bias, xin, xout, s, g, C, residual_sign, clamp_out);
+}
+
+int s3_tiles(const ConvShape& s) { return s3_geom(s).tiles; }
+
+void launch_conv_stack_s3(half_t* aH, half_t* aL, half_t* bH, half_t* bL, const void* w_hi, const void* w_lo,
+                          const float* bias, int nbody, const ConvShape& s, int act, int num_cus, int* done, int epoch,
+                          int* err, hipStream_t st) {
+  const S3Geom g = s3_geom(s);
+  const int grid = g.tiles < num_cus ? g.tiles : num_cus;
+  if (act == 0)
+    hipLaunchKernelGGL((conv_stack_s3_kernel<0>), dim3(grid), dim3(256), kS3StkLds, st, aH, aL, bH, bL,
+                       (const uint4*)w_hi, (const uint4*)w_lo, bias, nbody, s, g, done, epoch, err);
+  else
+    hipLaunchKernelGGL((conv_stack_s3_kernel<1>), dim3(grid), dim3(256), kS3StkLds, st, aH, aL, bH, bL,
+                       (const uint4*)w_hi, (const uint4*)w_lo, bias, nbody, s, g, done, epoch, err);
 }
 
 }  // namespace pnp

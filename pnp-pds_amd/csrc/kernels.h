@@ -38,6 +38,11 @@ void launch_conv_tail(const half_t* in, const float* xin, float* xout, const voi
 void launch_conv_body_f2(const half_t* in, half_t* out, const void* w16_1, const void* w16_2, const void* w32_1,
                          const void* w32_2, const float* b1, const float* b2, const ConvShape& s, int act,
                          int num_cus, hipStream_t st);
+// all nbody 64 -> 64 layers in one launch for small batches (grid = min(tiles, CUs)); the
+// result ends in a if nbody is even, else in b.  done: s.tiles progress words (zeroed once),
+// epoch: this launch's tag (advance by >= nbody + 1 per launch); err: set on a stuck wait.
+void launch_conv_stack16(half_t* a, half_t* b, const void* w, const float* bias, int nbody, const ConvShape& s,
+                         int act, int num_cus, int* done, int epoch, int* err, hipStream_t st);
 // one 64 -> 64 layer with split weights W_hi + W_lo (PNP_PREC_FP16W2)
 void launch_conv_body_w2(const half_t* in, half_t* out, const void* w, const void* w_lo, const float* bias,
                          const ConvShape& s, int act, int num_cus, hipStream_t st);
@@ -54,6 +59,12 @@ void launch_conv_s3_body(const half_t* in_hi, const half_t* in_lo, half_t* out_h
 void launch_conv_s3_tail(const half_t* in_hi, const half_t* in_lo, const float* xin, float* xout, const void* w_hi,
                          const void* w_lo, const float* bias, const ConvShape& s, int C, int residual_sign,
                          int clamp_out, int num_cus, hipStream_t st);
+// all nbody body layers in one launch for small batches (as launch_conv_stack16; result in a* if
+// nbody is even); s3_tiles: the 8 x 16 tile count of a batch
+int s3_tiles(const ConvShape& s);
+void launch_conv_stack_s3(half_t* aH, half_t* aL, half_t* bH, half_t* bL, const void* w_hi, const void* w_lo,
+                          const float* bias, int nbody, const ConvShape& s, int act, int num_cus, int* done, int epoch,
+                          int* err, hipStream_t st);
 // fp32-operand denoiser (conv32.hip, PNP_PREC_FP32): mode 0 = head (NCHW fp32 in), 1 = body,
 // 2 = tail (NCHW fp32 out + residual + clamp); activations fp32 padded NHWC64, pad 1.
 hipError_t conv32_kernels_init();

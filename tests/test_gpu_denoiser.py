@@ -192,10 +192,35 @@ def test_body_two_layers_per_launch_bit_identical(gpu_ctx, name, B, C, H, W):
     gpu_ctx.set_body_layers(1)
     try:
         single = run_denoise(gpu_ctx, w, x)
-    finally:
         gpu_ctx.set_body_layers(2)
-    fused = run_denoise(gpu_ctx, w, x)
+        fused = run_denoise(gpu_ctx, w, x)
+    finally:
+        gpu_ctx.set_body_layers(0)
     np.testing.assert_array_equal(fused, single)
+
+
+@pytest.mark.parametrize("name,B,C,H,W", [("DnCNN_nobn_nch_3_nlev_0.01", 1, 3, 256, 256),     # 256 tiles: 1 per CU
+                                          ("DnCNN_nobn_nch_1_nlev_0.01", 2, 1, 256, 256),     # 512: 2 per workgroup
+                                          ("DnCNN_nobn_nch_3_nlev_0.01", 3, 3, 256, 256),     # 768: 3 per workgroup
+                                          ("dncnn_15", 2, 1, 37, 45),                         # odd layer count
+                                          ("dncnn_color_blind", 1, 3, 9, 33),                 # ReLU, tiny image
+                                          ("DnCNN_nobn_nch_3_nlev_0.01", 3, 3, 50, 70)])      # ragged tiles
+def test_body_all_layers_one_launch_bit_identical(gpu_ctx, name, B, C, H, W):
+    """conv_stack16 (every body layer in one persistent launch, tiles handed between
+    workgroups through per-tile progress words) gives the one-layer launches' bits."""
+    rng = np.random.default_rng(12)
+    w = DenoiserWeights.load_npz(os.path.join(WEIGHTS_DIR, name + ".npz"))
+    x = rng.uniform(0, 1, (B, C, H, W)).astype(np.float32)
+    try:
+        gpu_ctx.set_body_layers(1)
+        single = run_denoise(gpu_ctx, w, x)
+        gpu_ctx.set_body_layers(3)
+        stack = run_denoise(gpu_ctx, w, x)
+        stack2 = run_denoise(gpu_ctx, w, x)          # a second launch: the next epoch of the progress words
+    finally:
+        gpu_ctx.set_body_layers(0)
+    np.testing.assert_array_equal(stack, single)
+    np.testing.assert_array_equal(stack2, single)
 
 
 def test_denoiser_full_size_rgb(gpu_ctx):
@@ -210,3 +235,28 @@ def test_denoiser_full_size_rgb(gpu_ctx):
     assert np.abs(out - ref).max() < TOL_VS_FP32
     # the denoiser denoises: closer to the clean image than its input
     assert np.mean((out[0] - clean) ** 2) < np.mean((x[0] - clean) ** 2)
+
+
+@pytest.mark.parametrize("name,B,C,H,W", [("DnCNN_nobn_nch_1_nlev_0.01", 1, 1, 256, 256),     # 512 tiles: 2 per WG
+                                          ("DnCNN_nobn_nch_3_nlev_0.01", 1, 3, 64, 96),
+                                          ("dncnn_15", 2, 1, 37, 45),                         # odd layer count
+                                          ("dncnn_color_blind", 1, 3, 9, 33),                 # ReLU, tiny image
+                                          ("DnCNN_nobn_nch_3_nlev_0.01", 3, 3, 256, 256)])    # 1536 tiles: 6 per WG
+def test_fp16x3_all_layers_one_launch_bit_identical(gpu_ctx, name, B, C, H, W):
+    """conv_stack_s3 (every split-fp16 body layer in one persistent launch) gives the bits of
+    one conv_s3 launch per layer."""
+    rng = np.random.default_rng(13)
+    w = DenoiserWeights.load_npz(os.path.join(WEIGHTS_DIR, name + ".npz"))
+    x = rng.uniform(0, 1, (B, C, H, W)).astype(np.float32)
+    gpu_ctx.set_precision("fp16x3")
+    try:
+        gpu_ctx.set_body_layers(1)
+        single = run_denoise(gpu_ctx, w, x)
+        gpu_ctx.set_body_layers(3)
+        stack = run_denoise(gpu_ctx, w, x)
+        stack2 = run_denoise(gpu_ctx, w, x)
+    finally:
+        gpu_ctx.set_body_layers(0)
+        gpu_ctx.set_precision("fp16")
+    np.testing.assert_array_equal(stack, single)
+    np.testing.assert_array_equal(stack2, single)

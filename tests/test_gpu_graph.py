@@ -25,9 +25,10 @@ def _setup(case, B):
     phi.configure(ctx, g["x_0"].shape[-2], g["x_0"].shape[-1])
     prm = make_params(g1, g2, as_, an, lam, int(m1), int(m2), gadmm, sig, sp, palpha, r, True, True)
     rng = np.random.default_rng(1)
-    x0 = np.stack([g["x_0"]] * B) + 0.01 * rng.standard_normal((B,) + g["x_0"].shape)
-    xo = np.stack([g["x_obs"]] * B).astype(np.float32)
-    xt = np.stack([g["x_true"]] * B).astype(np.float32)
+    chw = (lambda a: a[None]) if g["x_0"].ndim == 2 else (lambda a: a)   # gray: the reference's (H, W)
+    x0 = np.stack([chw(g["x_0"])] * B) + 0.01 * rng.standard_normal((B,) + chw(g["x_0"]).shape)
+    xo = np.stack([chw(g["x_obs"])] * B).astype(np.float32)
+    xt = np.stack([chw(g["x_true"])] * B).astype(np.float32)
     return ctx, m, prm, x0.astype(np.float32), xo, xt
 
 
@@ -123,3 +124,21 @@ def test_op_l1_ball_side_stream_fresh_context():
         s.synchronize()
         np.testing.assert_allclose(do.cpu().numpy(), want, atol=2e-6)
         ctx.close()
+
+
+@pytest.mark.parametrize("case", ["A_blur", "A_gray", "B_blur"])
+def test_single_image_stack_equals_per_layer(case):
+    """B = 1 (the reference's call pattern): the auto choice for a single image, all body
+    layers in one persistent launch (conv_stack16), against one launch per layer, through the
+    solver: x, s and every metric, same bits; and with graph replay on (captured steps fall
+    back to per-layer launches, the plain ones keep the persistent launch)."""
+    ctx, m, prm, x0, xo, xt = _setup(case, 1)
+    ctx.set_precision("fp16")
+    ctx.set_body_layers(1)
+    ref = ctx.run(m, prm, x0, xo, xt, 7)
+    for mode, graph in ((0, 0), (3, 0), (0, 1)):
+        ctx.set_body_layers(mode)
+        ctx.set_graph(graph)
+        got = ctx.run(m, prm, x0, xo, xt, 7)
+        for a, b in zip(ref[:5], got[:5]):
+            np.testing.assert_array_equal(a, b)
