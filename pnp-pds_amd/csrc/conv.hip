@@ -766,6 +766,21 @@ template __global__ void conv_body_w2_kernel<1>(const half_t* __restrict__, half
 // uses it only when the batch has at most 2 tiles per CU.
 // ------------------------------------------------------------------------------------
 constexpr int kStkLds = 2 * kW2Halo;                           // 90112 B
+#ifdef STACK_STAMPS   // diagnostic build (tools/stack_stamps.py): s_memrealtime per phase, first tile of WG < 512
+__device__ unsigned long long stack_stamps[512][24][6];
+#define STK_STAMP(L, I)                                                                                     \
+  do {                                                                                                      \
+    if (k == 0 && blockIdx.x < 512 && (L) < 24) {                                                           \
+      unsigned long long t_;                                                                                \
+      __builtin_amdgcn_sched_barrier(0);                                                                    \
+      asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                        \
+      __builtin_amdgcn_sched_barrier(0);                                                                    \
+      if (tid == 0) stack_stamps[blockIdx.x][(L)][(I)] = t_;                                                \
+    }                                                                                                       \
+  } while (0)
+#else
+#define STK_STAMP(L, I) do {} while (0)
+#endif
 constexpr int kCpolDevice = 16;                                // sc1: device-scope load / store
 
 template <int ACT>
@@ -803,6 +818,7 @@ __global__ __launch_bounds__(256, 1) void conv_stack16_kernel(half_t* __restrict
       const int t = (int)blockIdx.x + k * G;
       int b, ty0, tx0;
       decode_tile(t, s, b, ty0, tx0);
+      STK_STAMP(l, 0);
       if (l > 0) {                            // the 3 x 3 neighbourhood has published layer l - 1
         if (wave == 0) {
           const int ny = ty0 / kTileH + lane / 3 - 1, nx = tx0 / kTileW + lane % 3 - 1;
@@ -811,9 +827,11 @@ __global__ __launch_bounds__(256, 1) void conv_stack16_kernel(half_t* __restrict
         }
         __syncthreads();
       }
+      STK_STAMP(l, 1);
       dma.template issue<kCpolDevice>(buf(k & 1), in, s, t, wave);   // device scope: never a stale line
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
+      STK_STAMP(l, 2);
       const unsigned char* hl = buf(k & 1);
       auto ldB = [&](int ks, int n) {
         const int tap = ks >> 2, sub = ks & 3;
@@ -834,6 +852,7 @@ __global__ __launch_bounds__(256, 1) void conv_stack16_kernel(half_t* __restrict
         for (int n = 0; n < 4; ++n)
           acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(w[ks], fb[r][n], ks == 0 ? floatx16{} : acc[n], 0, 0, 0);
       }
+      STK_STAMP(l, 3);
       // lane (col, h) holds channels 32m + 16h .. +15 of pixel (row 4rq + n, column col)
 #pragma unroll
       for (int n = 0; n < 4; ++n) {
@@ -848,7 +867,9 @@ __global__ __launch_bounds__(256, 1) void conv_stack16_kernel(half_t* __restrict
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's stores done (device scope)
       __syncthreads();
+      STK_STAMP(l, 4);
       if (tid == 0) tile_publish(done + t, epoch + l + 1);
+      STK_STAMP(l, 5);
     }
     // the next layer's weights: in flight while the neighbourhood catches up
     if (l + 1 < nbody) load_w(l + 1);
@@ -1394,3 +1415,10 @@ void launch_conv_tail(const half_t* in, const float* xin, float* xout, const voi
 }
 
 }  // namespace pnp
+
+#ifdef STACK_STAMPS
+extern "C" int pnp_diag_stack_stamps(unsigned long long* host, size_t n) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(pnp::stack_stamps), n * sizeof(unsigned long long), 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
