@@ -17,13 +17,18 @@ import csv
 import json
 import re
 
-WIDE_READ = ("conv_body_f2", "conv_body", "conv_tail")   # conv_head reads fp32 u32 4 B per lane (r02)
+WIDE_READ = ("conv_body_f2", "conv_body", "conv_tail", "conv_body_s3", "conv_tail_s3", "conv_stack")   # 16 B/lane
+# (conv_head reads fp32 u32 4 B per lane, r02)
 
 
 def short(name):
     n = re.sub(r"\(.*", "", name)
     if any(k in n for k in ("conv_body_x8", "conv_body_f8", "conv_body_f2")):   # the two-layer launch (bench scope "conv_body_f2")
         return "conv_body_f2"
+    if "conv_s3_kernel" in n:                                               # split fp16: body (MODE 0) / tail
+        return "conv_tail_s3" if "ILi1E" in n else "conv_body_s3"
+    if "conv_stack" in n:
+        return "conv_stack"
     for k in ("conv_body_f2", "conv_body", "conv_head", "conv_tail", "k1", "k2", "k3_l2_dual", "l1_", "ssim"):
         if k in n:
             return k
