@@ -81,7 +81,7 @@ def stream_copy_gbs(torch, ctx, device, nbytes=1 << 30, reps=10):
     b = torch.empty_like(a)
     a.fill_(1.0)
     torch.cuda.synchronize()
-    st = torch.cuda.current_stream(device)
+    st = torch.cuda.Stream(device)     # not the legacy default stream (handle 0 = the library's own stream)
     best = float("inf")
     for _ in range(reps):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -90,6 +90,7 @@ def stream_copy_gbs(torch, ctx, device, nbytes=1 << 30, reps=10):
         e1.record(st)
         e1.synchronize()
         best = min(best, e0.elapsed_time(e1) * 1e-3)
+    st.synchronize()
     assert torch.equal(a[:1024], b[:1024]) and torch.equal(a[-1024:], b[-1024:])
     del a, b
     return 2 * nbytes / best / 1e9
@@ -140,13 +141,13 @@ def conv_bytes_per_launch(m, H, W, elem=2):
     return 2 * m * H * W * 64 * elem
 
 
-TRAFFIC_JSON = "profiles/r02/bench/traffic.json"
+TRAFFIC_JSON = "profiles/r03/bench/traffic.json"
 
 
 def measured_traffic(kernel, cfg_name, B):
     """HBM bytes per launch from this round's committed PMC passes of this bench command
     (tools/profile_bench.sh + tools/traffic_from_pmc.py), or None."""
-    for path in (TRAFFIC_JSON, "profiles/r01/bench/traffic.json"):
+    for path in (TRAFFIC_JSON, "profiles/r02/bench/traffic.json"):
         try:
             with open(os.path.join(REPO, path)) as f:
                 t = json.load(f)

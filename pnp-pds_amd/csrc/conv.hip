@@ -358,6 +358,9 @@ __device__ __forceinline__ int f2_slot(int row) { return (row + 1 + 18 * 64) % k
 // Weights: pack_body_weights16, [18 ks][2 M-tiles][2 subtiles][64 lanes][8 x f16].
 // ------------------------------------------------------------------------------------
 constexpr int kX8KSteps = 18;
+#ifdef X8_CLOCK
+__device__ unsigned long long x8_clock[1024][2];   // per workgroup: shader-clock cycles, 100 MHz ticks
+#endif
 
 template <int NT, int PLANE, class Side>
 __device__ __forceinline__ void x8_kloop(const half8_t (&wA)[kX8KSteps][2], const unsigned char* ring,
@@ -434,6 +437,10 @@ __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __re
   float bl[8];
 #pragma unroll
   for (int r = 0; r < 8; ++r) bl[r] = (layer ? b2 : b1)[32 * m + 8 * g + r];
+#ifdef X8_CLOCK   // diagnostic build (tools/x8_clock.py): shader clock vs the 100 MHz real-time clock
+  unsigned long long c0_, r0_;
+  asm volatile("s_memtime %0\n\ts_memrealtime %1\n\ts_waitcnt lgkmcnt(0)" : "=s"(c0_), "=s"(r0_)::"memory");
+#endif
   const unsigned img_bytes = (unsigned)(s.Hp * s.Wp) * 128u;
 
   const int S = 8 * sb;
@@ -622,6 +629,14 @@ __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __re
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#ifdef X8_CLOCK
+  unsigned long long c1_, r1_;
+  asm volatile("s_memtime %0\n\ts_memrealtime %1\n\ts_waitcnt lgkmcnt(0)" : "=s"(c1_), "=s"(r1_)::"memory");
+  if (tid == 0 && blockIdx.x < 1024) {
+    x8_clock[blockIdx.x][0] = c1_ - c0_;
+    x8_clock[blockIdx.x][1] = r1_ - r0_;
+  }
+#endif
 }
 
 template __global__ void conv_body_x8_kernel<0>(const half_t* __restrict__, half_t* __restrict__,
@@ -1419,6 +1434,13 @@ void launch_conv_tail(const half_t* in, const float* xin, float* xout, const voi
 #ifdef STACK_STAMPS
 extern "C" int pnp_diag_stack_stamps(unsigned long long* host, size_t n) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(pnp::stack_stamps), n * sizeof(unsigned long long), 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
+
+#ifdef X8_CLOCK
+extern "C" int pnp_diag_x8_clock(unsigned long long* host, size_t n) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(pnp::x8_clock), n * sizeof(unsigned long long), 0,
                              hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
 }
 #endif
