@@ -481,7 +481,7 @@ __global__ __launch_bounds__(256) void k3_l2_dual(float* __restrict__ y, const f
   const size_t chunk = 2048;
   const size_t beg = (size_t)blockIdx.x * chunk;
   for (size_t k = beg + threadIdx.x; k < beg + chunk && k < n; k += 256)
-    yb[k] = (float)(omf * ((double)yb[k] - gamma2 * (double)ob[k]));
+    yb[k] = (float)(omf * ((double)yb[k] - gamma2 * (double)ob[k]));   // (non-temporal: 0.119 vs 0.099 ms)
 }
 
 __global__ __launch_bounds__(256) void k3_metrics(const double* __restrict__ partials, int tiles, size_t n,
@@ -956,8 +956,10 @@ __device__ __forceinline__ void rb_tile_origin(int tile, int tiles_x, int& i0, i
 
 // Column-pair loads / stores of the blur kernels' epilogues: nv valid columns (0..2);
 // vec = both valid and 8-B aligned (one dwordx2), else guarded scalar accesses.
+// The epilogue streams (read once / written once per pass: x, y, s, x_obs, w in, u32, y, s, w
+// out) are non-temporal: K1 0.162 -> 0.159 ms, K2 0.276 -> 0.272 at the metric (A/B, r03).
 __device__ __forceinline__ f2_t ld2g(const float* __restrict__ p, size_t idx, int nv, bool vec) {
-  if (vec) return *reinterpret_cast<const f2_t*>(p + idx);
+  if (vec) return __builtin_nontemporal_load(reinterpret_cast<const f2_t*>(p + idx));
   f2_t v = {0.f, 0.f};
   if (nv > 0) v.x = p[idx];
   if (nv > 1) v.y = p[idx + 1];
@@ -965,7 +967,7 @@ __device__ __forceinline__ f2_t ld2g(const float* __restrict__ p, size_t idx, in
 }
 __device__ __forceinline__ void st2g(float* __restrict__ p, size_t idx, const f2_t& v, int nv, bool vec) {
   if (vec) {
-    *reinterpret_cast<f2_t*>(p + idx) = v;
+    __builtin_nontemporal_store(v, reinterpret_cast<f2_t*>(p + idx));
     return;
   }
   if (nv > 0) p[idx] = v.x;
@@ -1814,7 +1816,9 @@ void launch_gkl(const float* x, const float* x0, float* out, size_t count, doubl
 }
 
 // Streaming copy (bench.py's measured copy ceiling for the prox passes' HBM fraction): every
-// thread moves 4 x 16 B per step, all four loads in flight before the stores, grid-strided.
+// thread moves 4 x 16 B per step, all four loads in flight before the stores, non-temporal
+// (tools/probes/copy_bw.hip, 1 GiB: plain 5.5-5.8 TB/s, non-temporal 5.9-6.3 TB/s, best with
+// 64 blocks per CU), grid-strided.
 __global__ __launch_bounds__(256) void copy_f4_kernel(const floatx4* __restrict__ src, floatx4* __restrict__ dst,
                                                       size_t n4) {
   const size_t stride = (size_t)gridDim.x * 256 * 4;
@@ -1822,17 +1826,17 @@ __global__ __launch_bounds__(256) void copy_f4_kernel(const floatx4* __restrict_
     floatx4 v[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k)
-      if (i + 256 * k < n4) v[k] = src[i + 256 * k];
+      if (i + 256 * k < n4) v[k] = __builtin_nontemporal_load(src + i + 256 * k);
 #pragma unroll
     for (int k = 0; k < 4; ++k)
-      if (i + 256 * k < n4) dst[i + 256 * k] = v[k];
+      if (i + 256 * k < n4) __builtin_nontemporal_store(v[k], dst + i + 256 * k);
   }
 }
 
 void launch_copy_f4(const void* src, void* dst, size_t bytes, int num_cus, hipStream_t st) {
   const size_t n4 = bytes / 16;
   size_t blocks = (n4 + 1023) / 1024;
-  const size_t cap = (size_t)num_cus * 8;
+  const size_t cap = (size_t)num_cus * 64;
   if (blocks > cap) blocks = cap;
   if (blocks == 0) return;
   hipLaunchKernelGGL(copy_f4_kernel, dim3((unsigned)blocks), dim3(256), 0, st, (const floatx4*)src, (floatx4*)dst, n4);
