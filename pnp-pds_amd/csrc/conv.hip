@@ -358,6 +358,10 @@ __device__ __forceinline__ int f2_slot(int row) { return (row + 1 + 18 * 64) % k
 // Weights: pack_body_weights16, [18 ks][2 M-tiles][2 subtiles][64 lanes][8 x f16].
 // ------------------------------------------------------------------------------------
 constexpr int kX8KSteps = 18;
+// Non-temporal output stores (A/B at the metric, r03, ms per launch): the head's 0.446 -> 0.439
+// (kept); conv_body_x8 2.248 -> 2.267 and the tail unchanged (not kept).
+constexpr int kNtX8 = 0, kNtTail = 0;                          // buffer-store cache policy (2 = nt)
+constexpr bool kNtHead = true;
 #ifdef X8_CLOCK
 __device__ unsigned long long x8_clock[1024][2];   // per workgroup: shader-clock cycles, 100 MHz ticks
 #endif
@@ -601,7 +605,7 @@ __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __re
           for (int n = 0; n < 2; ++n) {
             const half8_t v = x8_bias_act<ACT>(acc[n], bl);
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i_t, v), rs,
-                                                   (unsigned)((16 * n + px) * 128 + 64 * m + 16 * g), 0, 0);
+                                                   (unsigned)((16 * n + px) * 128 + 64 * m + 16 * g), 0, kNtX8);
           }
         };
         group(0, true);
@@ -1071,7 +1075,14 @@ __global__ __launch_bounds__(256) void conv_head_kernel(const float* __restrict_
         const uint4 q = *reinterpret_cast<const uint4*>(stg + (n * 32 + p) * 128 + 16 * (c ^ (p & 7)));
         const int y = ty0 + 2 * wave + n, x = tx0 + p;
         if (y < s.H && x < s.W)
-          *reinterpret_cast<uint4*>(dst + (((size_t)b * s.Hp + y + s.pad) * s.Wp + x + s.pad) * kWidth + 8 * c) = q;
+        {
+          if (kNtHead)
+            __builtin_nontemporal_store(__builtin_bit_cast(v4i_t, q),
+                                        reinterpret_cast<v4i_t*>(dst + (((size_t)b * s.Hp + y + s.pad) * s.Wp + x + s.pad) *
+                                                                           kWidth + 8 * c));
+          else
+            *reinterpret_cast<uint4*>(dst + (((size_t)b * s.Hp + y + s.pad) * s.Wp + x + s.pad) * kWidth + 8 * c) = q;
+        }
       }
     }
   }
@@ -1201,7 +1212,7 @@ __global__ __launch_bounds__(256, 1) void conv_tail_kernel(const half_t* __restr
                                             __builtin_amdgcn_make_buffer_rsrc(
                                                 (void*)(xout + ((size_t)b * C + (c < C ? c : 0)) * plane), (short)0,
                                                 c < C ? (int)(plane * 4u) : 0, 0x00020000),
-                                            off, 0, 0);
+                                            off, 0, kNtTail);
     }
     // tile t+1 landed: younger than its DMA are this tile's 4 loads, DMA of t+2 and 4 stores
     asm volatile("s_waitcnt vmcnt(19) lgkmcnt(0)" ::: "memory");
