@@ -366,9 +366,13 @@ constexpr bool kNtHead = true;
 __device__ unsigned long long x8_clock[1024][2];   // per workgroup: shader-clock cycles, 100 MHz ticks
 #endif
 
+#ifndef X8_EPI
+#define X8_EPI 0      // A/B builds: 1 = bias as the first MFMA's C, 2 = LeakyReLU in packed fp16, 4 = uniform pad skip
+#endif
 template <int NT, int PLANE, class Side>
 __device__ __forceinline__ void x8_kloop(const half8_t (&wA)[kX8KSteps][2], const unsigned char* ring,
-                                         const int (&ad)[NT][3], floatx4 (&acc)[NT][2], Side&& side) {
+                                         const int (&ad)[NT][3], floatx4 (&acc)[NT][2], Side&& side,
+                                         const floatx4 (&c0)[2]) {
   auto ldB = [&](int ks, int n) {
     const int tap = ks >> 1, hs = ks & 1, dy = tap / 3, dx = tap - 3 * dy;
     return *reinterpret_cast<const half8_t*>(ring + ad[n][dy] + (4 * hs * PLANE + 16 * dx));
@@ -390,19 +394,30 @@ __device__ __forceinline__ void x8_kloop(const half8_t (&wA)[kX8KSteps][2], cons
 #pragma unroll
       for (int q = 0; q < 2; ++q)
         acc[n][q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wA[ks][q], fb[ks % (D + 1)][n],
-                                                           ks == 0 ? floatx4{} : acc[n][q], 0, 0, 0);
+                                                           ks == 0 ? ((X8_EPI & 1) ? c0[q] : floatx4{}) : acc[n][q],
+                                                           0, 0, 0);
     side(ks);
     __builtin_amdgcn_sched_barrier(0);
   }
 }
 
 // bias + activation of a lane's chunk (acc[0] = channels +0..3, acc[1] = +4..7) -> 8 x fp16
+typedef _Float16 h2v_t __attribute__((ext_vector_type(2)));
 template <int ACT>
 __device__ __forceinline__ half8_t x8_bias_act(const floatx4 (&a)[2], const float* bl) {
   half8_t o;
 #pragma unroll
   for (int r = 0; r < 8; r += 2) {
-    f2v_t v = f2v_t{a[r >> 2][r & 3], a[r >> 2][(r & 3) + 1]} + f2v_t{bl[r], bl[r + 1]};
+    f2v_t v = f2v_t{a[r >> 2][r & 3], a[r >> 2][(r & 3) + 1]};
+    if (!(X8_EPI & 1)) v += f2v_t{bl[r], bl[r + 1]};
+    if (X8_EPI & 2) {
+      h2v_t hv = __builtin_convertvector(v, h2v_t);
+      hv = ACT == 0 ? __builtin_elementwise_max(hv, hv * (h2v_t){(_Float16)0.01f, (_Float16)0.01f})
+                    : __builtin_elementwise_max(hv, (h2v_t){(_Float16)0.f, (_Float16)0.f});
+      o[r] = hv.x;
+      o[r + 1] = hv.y;
+      continue;
+    }
     if (ACT == 0) {
       const f2v_t t = v * 0.01f;
       v = f2v_t{fmaxf(v.x, t.x), fmaxf(v.y, t.y)};
@@ -441,6 +456,7 @@ __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __re
   float bl[8];
 #pragma unroll
   for (int r = 0; r < 8; ++r) bl[r] = (layer ? b2 : b1)[32 * m + 8 * g + r];
+  const floatx4 c0[2] = {floatx4{bl[0], bl[1], bl[2], bl[3]}, floatx4{bl[4], bl[5], bl[6], bl[7]}};
 #ifdef X8_CLOCK   // diagnostic build (tools/x8_clock.py): shader clock vs the 100 MHz real-time clock
   unsigned long long c0_, r0_;
   asm volatile("s_memtime %0\n\ts_memrealtime %1\n\ts_waitcnt lgkmcnt(0)" : "=s"(c0_), "=s"(r0_)::"memory");
@@ -518,6 +534,7 @@ __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __re
           rowoff[q] = sl * (kF2InW * 16);
           sl = sl == kF2Ring - 1 ? 0 : sl + 1;
         }
+        const bool all_in = 8 * jb + 8 <= s.H && x0 + kTileW <= s.W;   // rows and columns of u < 16 inside
         // N-subtile u < 16: row u >> 1, columns 1 + 16 (u & 1) .. +15; u == 16: the strip halo
         // (columns 0 and 33 of the 8 rows: pixel px -> row px >> 1, column px & 1 ? 33 : 0)
         auto group = [&](auto ntc, int u0, int u1, bool first) {
@@ -537,14 +554,15 @@ __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __re
             }
           }
           floatx4 acc[NT][2];
-          if (first) x8_kloop<NT, kF2InPlane>(wA, ring, ad, acc, side);
-          else x8_kloop<NT, kF2InPlane>(wA, ring, ad, acc, noside);
+          if (first) x8_kloop<NT, kF2InPlane>(wA, ring, ad, acc, side, c0);
+          else x8_kloop<NT, kF2InPlane>(wA, ring, ad, acc, noside, c0);
 #pragma unroll
           for (int n = 0; n < NT; ++n) {
             const int x = x0 - 1 + pcol[n];
             const bool inside = 8 * jb + prow[n] < s.H && x >= 0 && x < s.W;
             half8_t v = x8_bias_act<ACT>(acc[n], bl);
-            if (!inside) v = half8_t{};                   // the next layer's zero padding
+            if (!((X8_EPI & 4) && (n == 0 ? u0 : u1) < 16 && all_in) && !inside)
+              v = half8_t{};                              // the next layer's zero padding
             *reinterpret_cast<half8_t*>(mid + (4 * m + g) * kF2MidPlane +
                                         (f2_slot(8 * J + prow[n]) * kF2MidW + pcol[n]) * 16) = v;
           }
@@ -591,8 +609,8 @@ __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __re
 #pragma unroll
             for (int dy = 0; dy < 3; ++dy) ad[n][dy] = lb + rowoff[t + dy] + 16 * 16 * n;
           floatx4 acc[2][2];
-          if (first) x8_kloop<2, kF2MidPlane>(wA, mid, ad, acc, side);
-          else x8_kloop<2, kF2MidPlane>(wA, mid, ad, acc, noside);
+          if (first) x8_kloop<2, kF2MidPlane>(wA, mid, ad, acc, side, c0);
+          else x8_kloop<2, kF2MidPlane>(wA, mid, ad, acc, noside, c0);
           const int R = 8 * J - 9 + 4 * half + t;
           int k, r;
           locate(R, kJ, k, r);
