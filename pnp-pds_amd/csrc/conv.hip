@@ -93,6 +93,42 @@ __device__ __forceinline__ void bias_act_s(half8_t& o, int q, const floatx16& a,
 typedef int v4i_t __attribute__((ext_vector_type(4)));
 typedef int v2i_t __attribute__((ext_vector_type(2)));
 
+// Epilogue of the fp16 body layers (conv_body_x8 / conv_body_v3 / conv_stack16; round 3).  The
+// bias is the C operand of a tile's first MFMA, so the accumulator already holds conv + bias;
+// the activation runs on the fp16-rounded pair in packed fp16: LeakyReLU(h) = max(h, h * 0.01h),
+// ReLU(h) = max(h, 0).  Three single-pass VALU ops per pair (v_cvt_pk_f16_f32, v_pk_mul_f16,
+// v_pk_max_f16) instead of five with fp32 packed ops (bias add, 0.01x, two maxes, cvt).  The
+// kernels run at the chip's power limit, where fewer VALU instructions per MFMA return as clock:
+// conv_body_x8 2.316 -> 2.215 ms per launch at the metric (A/B, r03).  ReLU is bit-identical to
+// rounding after the fp32 activation; LeakyReLU's negative branch multiplies by fp16(0.01) =
+// 0.0100021 in fp16 (≤ 1 fp16 ulp from fp16(0.01 v)), the same in all three kernels, so they
+// stay bit-identical to each other (tests/test_gpu_graph.py, test_gpu_denoiser.py).
+typedef _Float16 h2v_t __attribute__((ext_vector_type(2)));
+template <int ACT>
+__device__ __forceinline__ h2v_t act_h2(f2v_t v) {
+  const h2v_t h = __builtin_convertvector(v, h2v_t);
+  return ACT == 0 ? __builtin_elementwise_max(h, h * (h2v_t){(_Float16)0.01f, (_Float16)0.01f})
+                  : __builtin_elementwise_max(h, (h2v_t){(_Float16)0.f, (_Float16)0.f});
+}
+// 8 accumulator rows a[off .. off + 7] (bias included) -> 8 x fp16
+template <int ACT>
+__device__ __forceinline__ half8_t act8_h(const floatx16& a, int off) {
+  half8_t o;
+#pragma unroll
+  for (int r = 0; r < 8; r += 2) {
+    const h2v_t hv = act_h2<ACT>(f2v_t{a[off + r], a[off + r + 1]});
+    o[r] = hv.x;
+    o[r + 1] = hv.y;
+  }
+  return o;
+}
+__device__ __forceinline__ floatx16 bias16(const float* bl) {     // C operand: rows = bl[0 .. 15]
+  floatx16 c;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) c[r] = bl[r];
+  return c;
+}
+
 // ------------------------------------------------------------------------------------
 // LDS-DMA halo staging (buffer_load_dword... lds).  The 10 x 34 halo of an 8 x 32 tile
 // is 340 pixels = 43 slots of 8 pixels (1 KiB); lane l of a slot loads 16-B chunk
@@ -220,15 +256,14 @@ __global__ __launch_bounds__(512, 2) void conv_body_v3_kernel(const half_t* __re
     if constexpr ((ABL & 2) == 0) __builtin_amdgcn_raw_buffer_store_b128(v, rs[j >> 1], (pix & 31) * 128 + 64 * m + 16 * c, 0, 0);
   };
   floatx16 acc0 = {}, acc1 = {};
-  auto epilogue = [&](int eb, int ety0, int etx0) {   // bias + activation -> fp16 -> staging (wave-private)
-    const float* bl = bias_l + 32 * m + 16 * h;
+  auto epilogue = [&](int eb, int ety0, int etx0) {   // activation -> fp16 -> staging (wave-private)
     const int sw = (col >> 1) & 3;    // ds_write_b128 banks repeat every 128 B: 8 lanes distinct
 #pragma unroll
     for (int n = 0; n < 2; ++n) {
       const int pix = n * 32 + col;
       const floatx16& a = n == 0 ? acc0 : acc1;
-      *reinterpret_cast<half8_t*>(stg + pix * 64 + 16 * ((2 * h) ^ sw)) = bias_act8<ACT>(a, 0, bl);
-      *reinterpret_cast<half8_t*>(stg + pix * 64 + 16 * ((2 * h + 1) ^ sw)) = bias_act8<ACT>(a, 8, bl + 8);
+      *reinterpret_cast<half8_t*>(stg + pix * 64 + 16 * ((2 * h) ^ sw)) = act8_h<ACT>(a, 0);
+      *reinterpret_cast<half8_t*>(stg + pix * 64 + 16 * ((2 * h + 1) ^ sw)) = act8_h<ACT>(a, 8);
     }
     const int ncols = min(kTileW, s.W - etx0);
 #pragma unroll
@@ -250,8 +285,7 @@ __global__ __launch_bounds__(512, 2) void conv_body_v3_kernel(const half_t* __re
       return *reinterpret_cast<const half8_t*>(
           hl + halo_off(2 * rp + n + tap / 3, col + tap % 3, 2 * sub + h));
     };
-    acc0 = floatx16{};
-    acc1 = floatx16{};
+    const floatx16 cb = *reinterpret_cast<const floatx16*>(bias_l + 32 * m + 16 * h);   // first MFMA's C
     half8_t fb[2][2];
     v4i_t sv;
 #pragma unroll
@@ -272,8 +306,8 @@ __global__ __launch_bounds__(512, 2) void conv_body_v3_kernel(const half_t* __re
         fb[r ^ 1][0] = ldB(ks + 1, 0);
         fb[r ^ 1][1] = ldB(ks + 1, 1);
       }
-      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(wA[ks], fb[r][0], acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(wA[ks], fb[r][1], acc1, 0, 0, 0);
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(wA[ks], fb[r][0], ks == 0 ? cb : acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(wA[ks], fb[r][1], ks == 0 ? cb : acc1, 0, 0, 0);
       if ((ks & 7) == 4) {
         __builtin_amdgcn_sched_barrier(0);
         stage_store(ks >> 3, sv);
@@ -366,8 +400,8 @@ constexpr bool kNtHead = true;
 __device__ unsigned long long x8_clock[1024][2];   // per workgroup: shader-clock cycles, 100 MHz ticks
 #endif
 
-#ifndef X8_EPI
-#define X8_EPI 0      // A/B builds: 1 = bias as the first MFMA's C, 2 = LeakyReLU in packed fp16, 4 = uniform pad skip
+#ifndef X8_PADBR
+#define X8_PADBR 1    // layer l's zero-padding select skipped on interior steps by a uniform branch (A/B builds: 0)
 #endif
 template <int NT, int PLANE, class Side>
 __device__ __forceinline__ void x8_kloop(const half8_t (&wA)[kX8KSteps][2], const unsigned char* ring,
@@ -394,38 +428,21 @@ __device__ __forceinline__ void x8_kloop(const half8_t (&wA)[kX8KSteps][2], cons
 #pragma unroll
       for (int q = 0; q < 2; ++q)
         acc[n][q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wA[ks][q], fb[ks % (D + 1)][n],
-                                                           ks == 0 ? ((X8_EPI & 1) ? c0[q] : floatx4{}) : acc[n][q],
-                                                           0, 0, 0);
+                                                           ks == 0 ? c0[q] : acc[n][q], 0, 0, 0);
     side(ks);
     __builtin_amdgcn_sched_barrier(0);
   }
 }
 
-// bias + activation of a lane's chunk (acc[0] = channels +0..3, acc[1] = +4..7) -> 8 x fp16
-typedef _Float16 h2v_t __attribute__((ext_vector_type(2)));
+// activation of a lane's chunk (acc[0] = channels +0..3, acc[1] = +4..7; bias included) -> 8 x fp16
 template <int ACT>
-__device__ __forceinline__ half8_t x8_bias_act(const floatx4 (&a)[2], const float* bl) {
+__device__ __forceinline__ half8_t x8_act(const floatx4 (&a)[2]) {
   half8_t o;
 #pragma unroll
   for (int r = 0; r < 8; r += 2) {
-    f2v_t v = f2v_t{a[r >> 2][r & 3], a[r >> 2][(r & 3) + 1]};
-    if (!(X8_EPI & 1)) v += f2v_t{bl[r], bl[r + 1]};
-    if (X8_EPI & 2) {
-      h2v_t hv = __builtin_convertvector(v, h2v_t);
-      hv = ACT == 0 ? __builtin_elementwise_max(hv, hv * (h2v_t){(_Float16)0.01f, (_Float16)0.01f})
-                    : __builtin_elementwise_max(hv, (h2v_t){(_Float16)0.f, (_Float16)0.f});
-      o[r] = hv.x;
-      o[r + 1] = hv.y;
-      continue;
-    }
-    if (ACT == 0) {
-      const f2v_t t = v * 0.01f;
-      v = f2v_t{fmaxf(v.x, t.x), fmaxf(v.y, t.y)};
-    } else {
-      v = f2v_t{fmaxf(v.x, 0.f), fmaxf(v.y, 0.f)};
-    }
-    o[r] = (half_t)v.x;
-    o[r + 1] = (half_t)v.y;
+    const h2v_t hv = act_h2<ACT>(f2v_t{a[r >> 2][r & 3], a[r >> 2][(r & 3) + 1]});
+    o[r] = hv.x;
+    o[r + 1] = hv.y;
   }
   return o;
 }
@@ -456,7 +473,7 @@ __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __re
   float bl[8];
 #pragma unroll
   for (int r = 0; r < 8; ++r) bl[r] = (layer ? b2 : b1)[32 * m + 8 * g + r];
-  const floatx4 c0[2] = {floatx4{bl[0], bl[1], bl[2], bl[3]}, floatx4{bl[4], bl[5], bl[6], bl[7]}};
+  const floatx4 c0[2] = {floatx4{bl[0], bl[1], bl[2], bl[3]}, floatx4{bl[4], bl[5], bl[6], bl[7]}};   // first MFMA's C
 #ifdef X8_CLOCK   // diagnostic build (tools/x8_clock.py): shader clock vs the 100 MHz real-time clock
   unsigned long long c0_, r0_;
   asm volatile("s_memtime %0\n\ts_memrealtime %1\n\ts_waitcnt lgkmcnt(0)" : "=s"(c0_), "=s"(r0_)::"memory");
@@ -556,16 +573,20 @@ __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __re
           floatx4 acc[NT][2];
           if (first) x8_kloop<NT, kF2InPlane>(wA, ring, ad, acc, side, c0);
           else x8_kloop<NT, kF2InPlane>(wA, ring, ad, acc, noside, c0);
+          auto epi = [&](bool masked) {
 #pragma unroll
-          for (int n = 0; n < NT; ++n) {
-            const int x = x0 - 1 + pcol[n];
-            const bool inside = 8 * jb + prow[n] < s.H && x >= 0 && x < s.W;
-            half8_t v = x8_bias_act<ACT>(acc[n], bl);
-            if (!((X8_EPI & 4) && (n == 0 ? u0 : u1) < 16 && all_in) && !inside)
-              v = half8_t{};                              // the next layer's zero padding
-            *reinterpret_cast<half8_t*>(mid + (4 * m + g) * kF2MidPlane +
-                                        (f2_slot(8 * J + prow[n]) * kF2MidW + pcol[n]) * 16) = v;
-          }
+            for (int n = 0; n < NT; ++n) {
+              const int x = x0 - 1 + pcol[n];
+              const bool inside = 8 * jb + prow[n] < s.H && x >= 0 && x < s.W;
+              half8_t v = x8_act<ACT>(acc[n]);
+              if ((masked || (n == 0 ? u0 : u1) == 16) && !inside) v = half8_t{};   // the next layer's zero padding
+              *reinterpret_cast<half8_t*>(mid + (4 * m + g) * kF2MidPlane +
+                                          (f2_slot(8 * J + prow[n]) * kF2MidW + pcol[n]) * 16) = v;
+            }
+          };
+          if (!X8_PADBR) epi(true);
+          else if (__builtin_amdgcn_readfirstlane((int)all_in)) epi(false);
+          else epi(true);
         };
         using I1 = std::integral_constant<int, 1>;
         using I2 = std::integral_constant<int, 2>;
@@ -621,7 +642,7 @@ __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __re
               ok ? (void*)row : (void*)out, (short)0, ok ? min(kTileW, s.W - G.x0) * 128 : 0, 0x00020000);
 #pragma unroll
           for (int n = 0; n < 2; ++n) {
-            const half8_t v = x8_bias_act<ACT>(acc[n], bl);
+            const half8_t v = x8_act<ACT>(acc[n]);
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i_t, v), rs,
                                                    (unsigned)((16 * n + px) * 128 + 64 * m + 16 * g), 0, kNtX8);
           }
@@ -887,14 +908,14 @@ __global__ __launch_bounds__(256, 1) void conv_stack16_kernel(half_t* __restrict
         }
 #pragma unroll
         for (int n = 0; n < 4; ++n)
-          acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(w[ks], fb[r][n], ks == 0 ? floatx16{} : acc[n], 0, 0, 0);
+          acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(w[ks], fb[r][n], ks == 0 ? bias16(bl) : acc[n], 0, 0, 0);
       }
       STK_STAMP(l, 3);
       // lane (col, h) holds channels 32m + 16h .. +15 of pixel (row 4rq + n, column col)
 #pragma unroll
       for (int n = 0; n < 4; ++n) {
         const int y = ty0 + 4 * rq + n;
-        const half8_t v0 = bias_act8<ACT>(acc[n], 0, bl), v1 = bias_act8<ACT>(acc[n], 8, bl + 8);
+        const half8_t v0 = act8_h<ACT>(acc[n], 0), v1 = act8_h<ACT>(acc[n], 8);
         half_t* row = out + (((size_t)b * s.Hp + y + s.pad) * s.Wp + tx0 + s.pad) * kWidth;
         const __amdgpu_buffer_rsrc_t rs =
             __builtin_amdgcn_make_buffer_rsrc(row, (short)0, y < s.H ? min(kTileW, s.W - tx0) * 128 : 0, 0x00020000);
