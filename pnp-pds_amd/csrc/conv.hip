@@ -400,6 +400,9 @@ constexpr bool kNtHead = true;
 __device__ unsigned long long x8_clock[1024][2];   // per workgroup: shader-clock cycles, 100 MHz ticks
 #endif
 
+#ifndef X8_OPQ
+#define X8_OPQ 1      // fragment addresses as opaque VGPRs (A/B builds: 0)
+#endif
 #ifndef X8_PADBR
 #define X8_PADBR 1    // layer l's zero-padding select skipped on interior steps by a uniform branch (A/B builds: 0)
 #endif
@@ -407,9 +410,21 @@ template <int NT, int PLANE, class Side>
 __device__ __forceinline__ void x8_kloop(const half8_t (&wA)[kX8KSteps][2], const unsigned char* ring,
                                          const int (&ad)[NT][3], floatx4 (&acc)[NT][2], Side&& side,
                                          const floatx4 (&c0)[2]) {
+  // One VGPR per (N-subtile, tap row), opaque to the compiler: otherwise it splits ad into the
+  // lane part and the wave-uniform ring-row part and re-adds them (v_add_u32 SGPR + VGPR) for
+  // every fragment read instead of folding the K-step's constant into the ds_read offset.
+  int av[NT][3];
+#pragma unroll
+  for (int n = 0; n < NT; ++n)
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy) {
+      av[n][dy] = (int)(size_t)ring + ad[n][dy];          // LDS byte address
+      if (X8_OPQ) asm volatile("" : "+v"(av[n][dy]));
+    }
+  typedef const __attribute__((address_space(3))) half8_t* lds_h8p;
   auto ldB = [&](int ks, int n) {
     const int tap = ks >> 1, hs = ks & 1, dy = tap / 3, dx = tap - 3 * dy;
-    return *reinterpret_cast<const half8_t*>(ring + ad[n][dy] + (4 * hs * PLANE + 16 * dx));
+    return *(lds_h8p)(size_t)(unsigned)(av[n][dy] + (4 * hs * PLANE + 16 * dx));
   };
   constexpr int D = 2;
   half8_t fb[D + 1][NT];
