@@ -496,9 +496,12 @@ __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __re
   const unsigned img_bytes = (unsigned)(s.Hp * s.Wp) * 128u;
 
   const int S = 8 * sb;
-  const int K = (nstrips - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
+  // (An XCD-aware strip order, an image's neighbouring strips on CUs sharing one L2, measured
+  // the same: 2.109 vs 2.108 ms, r03.)
+  const int bx = (int)blockIdx.x;
+  const int K = (nstrips - bx + (int)gridDim.x - 1) / (int)gridDim.x;
   auto geom = [&](int k) {
-    const int st = min(blockIdx.x + k * gridDim.x, (unsigned)nstrips - 1);
+    const int st = min(bx + k * (int)gridDim.x, nstrips - 1);
     const int b = st / strips_x;
     return SGeom{b, (st - b * strips_x) * kTileW};
   };
