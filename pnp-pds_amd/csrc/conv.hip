@@ -1193,7 +1193,7 @@ __global__ __launch_bounds__(256, 1) void conv_tail_kernel(const half_t* __restr
     dma.issue(buf(bi), in, s, tt < s.tiles ? tt : s.tiles - 1, wave);
   };
 
-  int t = blockIdx.x;
+  int t = blockIdx.x;      // (an XCD-aware tile order measured the same: 0.5599 vs 0.5545-0.5599 ms, r03)
   if (t < s.tiles) {
     issue_dma(t, 0);
     issue_dma(t + gridDim.x, 1);
