@@ -269,8 +269,6 @@ def main():
                     help="1: iteration launches replayed from a hipGraph (not while --profile)")
     ap.add_argument("--body-layers", type=int, default=0, choices=[0, 1, 2, 3],
                     help="body layers per launch on the fp16 path (0 = the library default)")
-    ap.add_argument("--blur-mfma", type=int, default=1, choices=[0, 1],
-                    help="blur stencils of K1 / K2 on MFMA (1, the library default) or the VALU (0)")
     ap.add_argument("--ablate", type=int, default=0,
                     help="profiling build only (PNP_LIB_PATH=lib_prof/...; results wrong): 1 DMA, 2 stores, 4 MFMA")
     args = ap.parse_args()
@@ -310,8 +308,6 @@ def main():
     ctx.set_precision(resolve_precision(args.precision))
     if args.body_layers:
         ctx.set_body_layers(args.body_layers)
-    if args.blur_mfma != 1:
-        ctx.set_blur_mfma(args.blur_mfma)
     if args.graph:
         ctx.set_graph(args.graph)
     h = load_blur_kernel("blur_1")

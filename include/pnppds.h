@@ -134,7 +134,7 @@ int pnp_set_denoiser(pnp_ctx* ctx, int channels, int depth, int width, const flo
 int pnp_set_precision(pnp_ctx* ctx, int precision);
 int pnp_get_precision(pnp_ctx* ctx, int* requested, int* effective);
 
-/* Performance knobs (no effect on results, except PNP_TUNE_BLUR_MFMA: see there).
+/* Performance knobs (no effect on results).
  * PNP_TUNE_DENOISE_CHUNK: images per denoiser pass (0 = auto: the whole batch, unless its
  * activation ping-pong pair would exceed an eighth of the device's memory; then equal passes). */
 enum pnp_tuning_key {
@@ -145,14 +145,9 @@ enum pnp_tuning_key {
                                 strip per CU, else 1), 1 (conv_body_v3), 2 (conv_body_f2, the
                                 intermediate stays in LDS) or 3 (all: conv_stack16).
                                 Bit-identical results.                                         */
-  PNP_TUNE_GRAPH = 3,         /* 1: iteration launches replayed from a hipGraph (two iterations
+  PNP_TUNE_GRAPH = 3          /* 1: iteration launches replayed from a hipGraph (two iterations
                                 per replay, methods A/B/C); 0: direct launches (default).
                                 Same results either way.                                       */
-  PNP_TUNE_BLUR_MFMA = 4      /* 1 (default): the blur stencils of the fused primal / dual passes
-                                run on the matrix cores in split fp16 (kernels with at most 17
-                                tap rows and a column span of at most 16, e.g. blur_1.mat);
-                                0: packed-fp32 VALU stencils.  The two agree to ~1e-6 absolute
-                                (not bit for bit); both are within the operator tolerance.     */
 };
 int pnp_set_tuning(pnp_ctx* ctx, int key, int value);
 

@@ -51,7 +51,6 @@ struct pnp_ctx {
   int den_chunk = 0;   // images per denoiser pass; 0 = auto
   int ablate = 0;         // PNP_PROFILING build only: parts of conv_body_v3 skipped, results wrong
   int body_layers = 0;    // PNP_TUNE_BODY_LAYERS: 0 auto, 1 conv_body_v3, 2 conv_body_f2, 3 conv_stack16
-  int blur_mf = 1;        // PNP_TUNE_BLUR_MFMA: blur stencils of K1 / K2 on MFMA (blur_mf.hip) where the taps fit
   bool den_ready = false;
   int prec_req = PNP_PREC_AUTO;   // pnp_set_precision (default: the per-solve policy, auto_precision)
   int prec = PNP_PREC_FP16X3;     // the operands the denoiser runs with now (resolved from prec_req)
@@ -65,9 +64,7 @@ struct pnp_ctx {
   int op_kind = PNP_OP_ID;
   int op_H = 0, op_W = 0;
   int op_ntaps = 0, op_R = 0, op_taps_id = 0;
-  DevBuf taps_fwd, taps_adj, mask, dense_fwd, dense_adj, taps64, mf_fwd, mf_adj;
-  MfTapsHost mfh_fwd{}, mfh_adj{};
-  bool mf_ok_fwd = false, mf_ok_adj = false;
+  DevBuf taps_fwd, taps_adj, mask, dense_fwd, dense_adj, taps64;
 
   // solver
   int method = -1, B = 0, C = 0, H = 0, W = 0, cap = 0, it = 0;
@@ -236,12 +233,6 @@ OpDesc op_desc(pnp_ctx* ctx) {
   d.dense_adj = ctx->op_kind == PNP_OP_BLUR ? P<const float>(ctx->dense_adj) : nullptr;
   d.Rd = ctx->op_kind == PNP_OP_BLUR ? dense_radius(ctx->op_R) : 0;
   d.taps_id = ctx->op_kind == PNP_OP_BLUR ? ctx->op_taps_id : TAPS_DENSE;
-  const bool blur = ctx->op_kind == PNP_OP_BLUR;
-  d.mf_fwd = MfTaps{blur && ctx->mf_ok_fwd ? ctx->mf_fwd.p : nullptr, ctx->mfh_fwd.nc, ctx->mfh_fwd.rt,
-                    ctx->mfh_fwd.cl, ctx->mfh_fwd.eh};
-  d.mf_adj = MfTaps{blur && ctx->mf_ok_adj ? ctx->mf_adj.p : nullptr, ctx->mfh_adj.nc, ctx->mfh_adj.rt,
-                    ctx->mfh_adj.cl, ctx->mfh_adj.eh};
-  d.mf_on = ctx->blur_mf;
   return d;
 }
 
@@ -1083,8 +1074,7 @@ int pnp_destroy(pnp_ctx* ctx) {
                     &ctx->z, &ctx->p, &ctx->t, &ctx->dense_fwd, &ctx->dense_adj, &ctx->ssim_scr,
                     &ctx->taps64, &ctx->y1, &ctx->d, &ctx->c1, &ctx->dg_words, &ctx->dg_flag, &ctx->dg_rank, &ctx->dg_scan, &ctx->dg_noise,
                     &ctx->dg_img, &ctx->dg_draws, &ctx->dg_first, &ctx->dg_status,
-                    &ctx->head_w32, &ctx->body_w32, &ctx->tail_w32, &ctx->act32[0], &ctx->act32[1], &ctx->l1_scr, &ctx->scr_act32[0], &ctx->scr_act32[1], &ctx->scr_l1, &ctx->ssim_mm, &ctx->head_wlo, &ctx->body_wlo, &ctx->tail_wlo, &ctx->body_w16,
-                    &ctx->mf_fwd, &ctx->mf_adj};
+                    &ctx->head_w32, &ctx->body_w32, &ctx->tail_w32, &ctx->act32[0], &ctx->act32[1], &ctx->l1_scr, &ctx->scr_act32[0], &ctx->scr_act32[1], &ctx->scr_l1, &ctx->ssim_mm, &ctx->head_wlo, &ctx->body_wlo, &ctx->tail_wlo, &ctx->body_w16};
   for (DevBuf* b : bufs) release(*b);
   graph_release(ctx);
   release(ctx->it_dev);
@@ -1113,11 +1103,6 @@ int pnp_set_tuning(pnp_ctx* ctx, int key, int value) {
     if (key == PNP_TUNE_DENOISE_CHUNK) {
       if (value < 0) fail(ctx, PNP_E_ARG, "chunk must be >= 0");
       ctx->den_chunk = value;
-      return;
-    }
-    if (key == PNP_TUNE_BLUR_MFMA) {
-      if (value < 0 || value > 1) fail(ctx, PNP_E_ARG, "blur MFMA must be 0 (VALU stencils) or 1 (MFMA, default)");
-      ctx->blur_mf = value;
       return;
     }
     if (key == PNP_TUNE_BODY_LAYERS) {
@@ -1312,19 +1297,6 @@ int pnp_set_operator(pnp_ctx* ctx, int kind, const double* h, int kh, int kw, co
         ensure(ctx, ctx->dense_adj, pa.size() * sizeof(float));
         HIPCHK(ctx, hipMemcpy(ctx->dense_fwd.p, pf.data(), pf.size() * sizeof(float), hipMemcpyHostToDevice));
         HIPCHK(ctx, hipMemcpy(ctx->dense_adj.p, pa.data(), pa.size() * sizeof(float), hipMemcpyHostToDevice));
-      }
-      {   // band tables of the MFMA stencils (blur_mf.hip)
-        std::vector<uint16_t> tf, ta;
-        ctx->mf_ok_fwd = build_mf_taps(fwd.data(), (int)fwd.size(), tf, ctx->mfh_fwd);
-        ctx->mf_ok_adj = build_mf_taps(adj.data(), (int)adj.size(), ta, ctx->mfh_adj);
-        if (ctx->mf_ok_fwd) {
-          ensure(ctx, ctx->mf_fwd, tf.size() * 2);
-          HIPCHK(ctx, hipMemcpy(ctx->mf_fwd.p, tf.data(), tf.size() * 2, hipMemcpyHostToDevice));
-        }
-        if (ctx->mf_ok_adj) {
-          ensure(ctx, ctx->mf_adj, ta.size() * 2);
-          HIPCHK(ctx, hipMemcpy(ctx->mf_adj.p, ta.data(), ta.size() * 2, hipMemcpyHostToDevice));
-        }
       }
       if (f64.empty()) f64.push_back(Tap64{0, 0, 0.0});
       ensure(ctx, ctx->taps64, f64.size() * sizeof(Tap64));

@@ -3,8 +3,6 @@
 #pragma once
 #include "common.h"
 
-#include <vector>
-
 namespace pnp {
 
 // ---- denoiser (conv.hip) -----------------------------------------------------------
@@ -81,17 +79,6 @@ void launch_conv32(int mode, const float* in, float* out, const float* xin, cons
 enum { OP_ID = 0, OP_BLUR = 1, OP_MASK = 2 };
 enum { M_A = 0, M_B = 1, M_C = 2 };
 
-// Band tables of the MFMA blur stencils (blur_mf.hip): a == nullptr when the kernel's taps do
-// not fit (a row span over 16 or more than 13 tap columns); then the VALU stencils run.
-constexpr int kMfMaxTapCols = 13;
-struct MfTaps {
-  const void* a;          // [tap column][hi, lo][64 lanes][8 x f16], taps scaled by 2^eh
-  int nc, rt, cl, eh;     // tap columns, rows above / columns left of the output, tap scale exponent
-};
-struct MfTapsHost {
-  int nc, rt, cl, eh;
-};
-
 struct OpDesc {
   int kind;
   const int4* taps_fwd;   // {oy, ox, float bits of w, 0}: Phi:   y[i,j] += w x[i+oy, j+ox] (periodic)
@@ -103,8 +90,6 @@ struct OpDesc {
   const float* dense_adj; //   [p = 0..Rd][oy + Rd][2][2], see pack_tap_pairs
   int Rd;                 // radius of the dense tables: smallest of {2, 4, 8} >= R, 0 if R > 8
   int taps_id;            // compile-time tap pattern (TAPS_*) the stencils are specialised on, 0 = dense
-  MfTaps mf_fwd, mf_adj;  // MFMA stencils of K2 (Phi) and K1 (Phi^T)
-  int mf_on;              // PNP_TUNE_BLUR_MFMA
 };
 inline int dense_radius(int R) { return R <= 2 ? 2 : R <= 4 ? 4 : R <= 8 ? 8 : 0; }
 enum { TAPS_DENSE = 0, TAPS_BLUR_1 = 1, TAPS_SQUARE_MINI = 2 };
@@ -112,16 +97,6 @@ enum { TAPS_DENSE = 0, TAPS_BLUR_1 = 1, TAPS_SQUARE_MINI = 2 };
 int match_taps(int Rd, const uint32_t* fwd_cols, const uint32_t* adj_cols);
 // Column-major dense table W[ox + Rd][oy + Rd] -> the (Rd+1) x (2Rd+1) x 2 float2 pairs rb_stencil reads.
 void pack_tap_pairs(int Rd, const float* W, float* out);
-
-// blur_mf.hip
-bool build_mf_taps(const int4* taps, int ntaps, std::vector<uint16_t>& tab, MfTapsHost& o);
-bool mf_usable(const MfTaps& t, int H, int W);
-void launch_k1_mf(hipStream_t st, const float* x, const float* y, const float* s, float* u32, float* w,
-                  const MfTaps& t, int B, int C, int H, int W, float gamma1, int clamp_in, int method_b);
-void launch_k2_mf(int method, hipStream_t st, const float* xn, const float* xo, float* y, const float* xobs,
-                  const float* xtrue, float* s, const float* w, const float* theta, double* partials,
-                  const MfTaps& t, int B, int C, int H, int W, int cells_x, int cells, double gamma2,
-                  double gkl_gamma, double gkl_alpha, int record, float* mm);
 
 void launch_k1(int kind, const float* x, const float* y, const float* s, float* u32, float* w,
                const OpDesc& op, int B, int C, int H, int W, float gamma1, int clamp_in, int method_b,

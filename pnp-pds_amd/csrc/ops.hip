@@ -1566,10 +1566,6 @@ static void launch_k1_rb(hipStream_t st, const float* x, const float* y, const f
 void launch_k1(int kind, const float* x, const float* y, const float* s, float* u32, float* w,
                const OpDesc& op, int B, int C, int H, int W, float gamma1, int clamp_in, int method_b,
                hipStream_t st) {
-  if (kind == OP_BLUR && op.mf_on && rb_ok(op, C, H, W) && mf_usable(op.mf_adj, H, W)) {
-    launch_k1_mf(st, x, y, s, u32, w, op.mf_adj, B, C, H, W, gamma1, clamp_in, method_b);
-    return;
-  }
   if (kind == OP_BLUR && rb_ok(op, C, H, W)) {
 #define K1RB(TT) launch_k1_rb<TT>(st, x, y, s, u32, w, op, B, C, H, W, gamma1, clamp_in, method_b)
     switch (op.taps_id) {
@@ -1645,11 +1641,6 @@ int launch_k2(int kind, int method, const float* xn, const float* xo, float* y, 
               int record, float* mm, hipStream_t st) {
   const TileGrid g = tile_grid(H, W);
   if (!record) mm = nullptr;
-  if (kind == OP_BLUR && op.mf_on && rb_ok(op, C, H, W) && mf_usable(op.mf_fwd, H, W)) {
-    launch_k2_mf(method, st, xn, xo, y, xobs, xtrue, s, w, theta, partials, op.mf_fwd, B, C, H, W, g.tiles_x,
-                 g.tiles, gamma2, gkl_gamma, gkl_alpha, record, mm);
-    return mm ? C * ((W + kRbW - 1) / kRbW) * ((H + kRbH - 1) / kRbH) : 0;   // 64 x 64 tiles, as the rb kernels
-  }
   if (kind == OP_BLUR && rb_ok(op, C, H, W)) {
 #define K2RB(TT) launch_k2_rb<TT>(method, st, xn, xo, y, xobs, xtrue, s, w, theta, partials, op, B, C, H, W, \
                                   g.tiles_x, g.tiles, gamma2, gkl_gamma, gkl_alpha, record, mm)

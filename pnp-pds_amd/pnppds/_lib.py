@@ -29,7 +29,6 @@ PRECISION_NAMES = {v: k for k, v in PRECISIONS.items()}
 TUNE_DENOISE_CHUNK = 1
 TUNE_BODY_LAYERS = 2
 TUNE_GRAPH = 3
-TUNE_BLUR_MFMA = 4
 TUNE_ABLATE = 99         # profiling build only (make PROFILING=1, lib_prof/): not in include/pnppds.h
 
 
@@ -251,12 +250,6 @@ class Context:
         """Iteration launches replayed from a hipGraph: 1 = on, 0 = off (default).  Same results
         either way (methods A/B/C; the others always launch directly)."""
         self._check(self.lib.pnp_set_tuning(self.h, TUNE_GRAPH, int(mode)))
-
-    def set_blur_mfma(self, on: int):
-        """Blur stencils of the fused K1 / K2 passes: 1 = matrix cores, split fp16 (default, for
-        kernels with <= 17 tap rows and a column span <= 16), 0 = packed-fp32 VALU.  The two agree
-        to ~1e-6 absolute, not bit for bit."""
-        self._check(self.lib.pnp_set_tuning(self.h, TUNE_BLUR_MFMA, int(on)))
 
     def set_body_layers(self, n: int):
         """64->64 denoiser layers per launch: 0 = auto (default: all in one persistent launch for

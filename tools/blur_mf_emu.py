@@ -1,4 +1,5 @@
-"""CPU emulation of the MFMA blur stencil's arithmetic (blur_mf.hip), test infrastructure only.
+"""CPU emulation of the split-fp16 MFMA blur stencil (the round-3 experiment blur_mf.hip, in git
+history at commit "Experiment: blur stencils of K1/K2 as row-Toeplitz MFMAs"), analysis only.
 
 Operands split into fp16 halves after power-of-two scaling (taps: max |w| < 2^15; data: the
 block's max |v| < 2^15), products hi*hi + lo*hi + hi*lo (exact in fp32), fp32 accumulation in tap
