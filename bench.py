@@ -267,7 +267,7 @@ def main():
     ap.add_argument("--chunk", type=int, default=0, help="images per denoiser pass (0 = auto)")
     ap.add_argument("--graph", type=int, default=0, choices=[0, 1],
                     help="1: iteration launches replayed from a hipGraph (not while --profile)")
-    ap.add_argument("--body-layers", type=int, default=0, choices=[0, 1, 2, 3],
+    ap.add_argument("--body-layers", type=int, default=0, choices=[0, 1, 2, 3, 4],
                     help="body layers per launch on the fp16 path (0 = the library default)")
     ap.add_argument("--ablate", type=int, default=0,
                     help="profiling build only (PNP_LIB_PATH=lib_prof/...; results wrong): 1 DMA, 2 stores, 4 MFMA")

@@ -143,8 +143,9 @@ enum pnp_tuning_key {
                                 persistent launch when the batch has at most 2 tiles per CU,
                                 e.g. one 256^2 image; else 2 when it has at least one 32-column
                                 strip per CU, else 1), 1 (conv_body_v3), 2 (conv_body_f2, the
-                                intermediate stays in LDS) or 3 (all: conv_stack16).
-                                Bit-identical results.                                         */
+                                intermediate stays in LDS), 3 (all: conv_stack16x2, two layers
+                                per tile hand-off when their number is even) or 4 (all:
+                                conv_stack16, one layer per hand-off).  Bit-identical results. */
   PNP_TUNE_GRAPH = 3          /* 1: iteration launches replayed from a hipGraph (two iterations
                                 per replay, methods A/B/C); 0: direct launches (default).
                                 Same results either way.                                       */

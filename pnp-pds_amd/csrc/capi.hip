@@ -50,7 +50,7 @@ struct pnp_ctx {
   int den_C = 0, den_depth = 0, den_act = 0, den_residual = 1, den_clamp = 1;
   int den_chunk = 0;   // images per denoiser pass; 0 = auto
   int ablate = 0;         // PNP_PROFILING build only: parts of conv_body_v3 skipped, results wrong
-  int body_layers = 0;    // PNP_TUNE_BODY_LAYERS: 0 auto, 1 conv_body_v3, 2 conv_body_f2, 3 conv_stack16
+  int body_layers = 0;    // PNP_TUNE_BODY_LAYERS: 0 auto, 1 conv_body_v3, 2 conv_body_f2, 3 conv_stack16(x2), 4 conv_stack16
   bool den_ready = false;
   int prec_req = PNP_PREC_AUTO;   // pnp_set_precision (default: the per-solve policy, auto_precision)
   int prec = PNP_PREC_FP16X3;     // the operands the denoiser runs with now (resolved from prec_req)
@@ -287,7 +287,7 @@ bool use_pair(pnp_ctx* ctx, int mb, int W) {
 // is a kernel argument, which a replay would repeat.
 bool use_stack(pnp_ctx* ctx, int tiles) {
   if (ctx->capturing) return false;
-  if (ctx->body_layers) return ctx->body_layers == 3;
+  if (ctx->body_layers) return ctx->body_layers >= 3;
   return tiles <= 2 * ctx->num_cus;
 }
 
@@ -450,10 +450,10 @@ void run_denoiser(pnp_ctx* ctx, const float* u32, float* xout, DevBuf (&act)[2],
       ProfScope ps(ctx, "conv_stack16", st);
       int epoch = 0;
       int* done = stack_flags(ctx, &act[0] == &ctx->act[0], s.tiles, nbody, st, epoch);
-      launch_conv_stack16(P<half_t>(act[0]), P<half_t>(act[1]), ctx->body_w.p, P<float>(ctx->body_b), nbody, s,
-                          ctx->den_act, ctx->num_cus, done, epoch, P<int>(ctx->stack_err), st);
+      cur = launch_conv_stack16(P<half_t>(act[0]), P<half_t>(act[1]), ctx->body_w.p, P<float>(ctx->body_b), nbody,
+                                s, ctx->den_act, ctx->num_cus, done, epoch, P<int>(ctx->stack_err),
+                                ctx->body_layers != 4, st);
       check_launch(ctx, "conv_stack16");
-      cur = nbody & 1;
     }
     for (int l = stack ? nbody : 0; l < nbody;) {
       const char* wl = (const char*)ctx->body_w.p + (size_t)l * kBodyWBytes;
@@ -1106,7 +1106,8 @@ int pnp_set_tuning(pnp_ctx* ctx, int key, int value) {
       return;
     }
     if (key == PNP_TUNE_BODY_LAYERS) {
-      if (value < 0 || value > 3) fail(ctx, PNP_E_ARG, "body layers per launch must be 0 (auto), 1, 2 or 3 (all)");
+      if (value < 0 || value > 4)
+        fail(ctx, PNP_E_ARG, "body layers per launch must be 0 (auto), 1, 2, 3 (all) or 4 (all, one per hand-off)");
       ctx->body_layers = value;
       return;
     }

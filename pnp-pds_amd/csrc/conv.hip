@@ -960,6 +960,249 @@ template __global__ void conv_stack16_kernel<1>(half_t* __restrict__, half_t* __
                                                 int* __restrict__);
 
 // ------------------------------------------------------------------------------------
+// conv_stack16x2: conv_stack16 with TWO body layers per hand-off (small batches, round 3).
+// Per layer the persistent chain costs a neighbour wait, the halo DMA and the device-scope
+// store round trip besides its ~2 us of MFMA work (9.1 us per layer at B = 1 RGB 256^2,
+// profiles/r03/stack_stamps.txt); here a tile computes layers l and l+1 from one 12 x 36 input
+// halo (2 pixels of border: the activation images' zero border is 2 pixels wide), the 10 x 34
+// intermediate of layer l staying in LDS, so the chain has half as many links.  Layer l costs
+// 11 N-tiles instead of 8 (the intermediate's border: 10 rows of 32 columns + one N-tile of its
+// 20 edge pixels, columns 0 and 33).  Wave w (one per SIMD): M-tile m = w & 1; layer l rows
+// 0..4 + the edge N-tile (w >> 1 == 0) or rows 5..9, in groups of at most 3 N-tiles; layer l+1
+// as conv_stack16 (rows 4 (w >> 1) .. +3).  Same MFMA chains and fp16 roundings as the
+// per-layer launches (the intermediate is zero outside the image = the next layer's padding),
+// so the results are bit-identical (tests/test_gpu_graph.py).  The pairs ping-pong A -> B -> A:
+// after an odd number of pairs the output is in actB (launch_conv_stack16x2 returns which).
+// ------------------------------------------------------------------------------------
+#ifndef X2_WEARLY
+#define X2_WEARLY 0   // K-steps of layer 2p + 1's weights loaded during layer 2p's last epilogue (A/B; more spill)
+#endif
+constexpr int kX2InW = kTileW + 4, kX2InH = kTileH + 4;        // 36 x 12 input halo
+constexpr int kX2InPix = kX2InW * kX2InH;                      // 432 = 54 DMA slots of 8 pixels
+constexpr int kX2Slots = kX2InPix / 8;
+constexpr int kX2SlotsW = (kX2Slots + 3) / 4;                  // 14 per wave (the last 2 re-read slot 53)
+constexpr int kX2In = 4 * kX2SlotsW * 1024;                    // 57344 B per input buffer
+constexpr int kX2Mid = 2 * kX2In;                              // intermediate (10 x 34, halo_off layout)
+constexpr int kX2Lds = kX2Mid + kV3Halo;                       // 158208 B
+static_assert(kX2Lds <= 163840, "conv_stack16x2 LDS");
+
+__device__ __forceinline__ int x2_in_off(int pr, int pc, int chunk) {          // 12 x 36 input halo
+  return (pr * kX2InW + pc) * 128 + 16 * (chunk ^ ((pc >> 1) & 7));
+}
+
+template <int ACT>
+__global__ __launch_bounds__(256, 1) void conv_stack16x2_kernel(half_t* __restrict__ actA, half_t* __restrict__ actB,
+                                                                 const uint4* __restrict__ wpk,
+                                                                 const float* __restrict__ bias, int npairs,
+                                                                 ConvShape s, int* __restrict__ done, int epoch,
+                                                                 int* __restrict__ err) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int m = wave & 1, rq = wave >> 1;
+  const int h = lane >> 5, col = lane & 31;
+  unsigned char* mid = smem + kX2Mid;
+  const int G = gridDim.x;
+  const int K = (s.tiles - (int)blockIdx.x + G - 1) / G;      // this workgroup's tiles (grid <= tiles)
+  // DMA: slot g (8 pixels of the 12 x 36 halo, 1 KiB) -> lane l loads chunk (l & 7) ^ swz(pc) of
+  // pixel 8g + l / 8 to the lane-linear destination (the x2_in_off layout)
+  unsigned doff[kX2SlotsW];
+#pragma unroll
+  for (int j = 0; j < kX2SlotsW; ++j) {
+    const int g = min(4 * j + wave, kX2Slots - 1);
+    const int p = 8 * g + (lane >> 3), pr = p / kX2InW, pc = p - pr * kX2InW;
+    const int c = (lane & 7) ^ ((pc >> 1) & 7);
+    doff[j] = (unsigned)(((pr * s.Wp + pc) * kWidth + c * 8) * 2);
+  }
+  auto issue_dma = [&](unsigned char* dst, const half_t* in, int b, int ty0, int tx0) {
+    // halo origin: image pixel (ty0 - 2, tx0 - 2) = padded (ty0, tx0); bounded by the image's end
+    const size_t o = ((size_t)b * s.Hp + ty0 + s.pad - 2) * s.Wp + tx0 + s.pad - 2;
+    const size_t end = ((size_t)b + 1) * s.Hp * s.Wp;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(in + o * kWidth), (short)0, (int)min((size_t)0x7fffffff, (end - o) * 128), 0x00020000);
+#pragma unroll
+    for (int j = 0; j < kX2SlotsW; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(dst + (4 * j + wave) * 1024),
+                                               16, doff[j], 0, 0, kCpolDevice);
+  };
+
+  // One layer's weights in registers at a time: layer 2p + 1's are loaded after layer 2p, the next
+  // pair's first layer after the publish (in flight while the neighbourhood catches up).
+  // (buffer loads: one lane offset + a scalar offset per K-step, instead of a 64-bit address
+  // register per K-step that the compiler keeps live across the whole kernel)
+  half8_t w[kBodyKSteps];
+  float bl[16];
+  const unsigned wlane = (unsigned)((m * 64 + lane) * 16);
+  auto load_w = [&](int l, int ks0 = 0, int ks1 = kBodyKSteps) {
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(reinterpret_cast<const unsigned char*>(wpk) + (size_t)l * kBodyWBytes), (short)0, kBodyWBytes, 0x00020000);
+#pragma unroll
+    for (int ks = 0; ks < kBodyKSteps; ++ks)
+      if (ks >= ks0 && ks < ks1)
+        w[ks] = __builtin_bit_cast(half8_t, __builtin_amdgcn_raw_buffer_load_b128(rw, wlane, ks * 2048, 0));
+    if (ks0 == 0)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) bl[r] = bias[l * kWidth + 32 * m + 16 * h + r];
+  };
+  load_w(0);
+  for (int p = 0; p < npairs; ++p) {
+    const half_t* src = (p & 1) ? actB : actA;                 // pairs ping-pong: A -> B -> A ...
+    half_t* out = (p & 1) ? actA : actB;
+    for (int k = 0; k < K; ++k) {
+      const int t = (int)blockIdx.x + k * G;
+      int b, ty0, tx0;
+      decode_tile(t, s, b, ty0, tx0);
+      if (k > 0) load_w(2 * p);               // (more than one tile per workgroup: layer 2p again)
+      STK_STAMP(p, 0);
+      if (p > 0) {                            // the 3 x 3 neighbourhood has published pair p - 1
+        if (wave == 0) {
+          const int ny = ty0 / kTileH + lane / 3 - 1, nx = tx0 / kTileW + lane % 3 - 1;
+          const bool want = lane < 9 && ny >= 0 && ny < s.tiles_y && nx >= 0 && nx < s.tiles_x;
+          tile_wait(done, want ? (b * s.tiles_y + ny) * s.tiles_x + nx : 0, want, epoch + p, err);
+        }
+        __syncthreads();
+      }
+      STK_STAMP(p, 1);
+      unsigned char* hin = smem + (k & 1) * kX2In;
+      issue_dma(hin, src, b, ty0, tx0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      STK_STAMP(p, 2);
+      // ---- layer 2p: the 10 x 34 intermediate into LDS ----
+      // N-tile u < 10: intermediate row u, columns 1 .. 32 (lane col -> column col + 1);
+      // u == 10: the edge pixels, lane n < 20 -> row n >> 1, column (n & 1) ? 33 : 0
+      // Fragment addresses: per (tap column dx, channel quarter sub) a lane offset, opaque so the
+      // compiler keeps 12 registers per kind of N-tile instead of hoisting every (N-tile, K-step)
+      // address out of the pair / tile loops (that spilled); tap rows and N-tile rows are immediates.
+      const int e = min(col, 19);                          // edge N-tile: lane -> row e >> 1, column 0 / 33
+      const int epr = e >> 1, epc = (e & 1) ? kHaloW - 1 : 0;
+      int cor[3][4], coe[3][4];
+#pragma unroll
+      for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+        for (int sub = 0; sub < 4; ++sub) {
+          cor[dx][sub] = x2_in_off(0, col + 1 + dx, 2 * sub + h);
+          coe[dx][sub] = x2_in_off(epr, epc + dx, 2 * sub + h);
+          asm volatile("" : "+v"(cor[dx][sub]), "+v"(coe[dx][sub]));
+        }
+      auto group = [&](auto ntc, int u0, int u1, int u2, bool last) {
+        constexpr int NT = decltype(ntc)::value;
+        int pr[NT], pc[NT], uu[NT];
+#pragma unroll
+        for (int n = 0; n < NT; ++n) {
+          const int u = n == 0 ? u0 : n == 1 ? u1 : u2;
+          uu[n] = u;
+          pr[n] = u < 10 ? u : epr;
+          pc[n] = u < 10 ? col + 1 : epc;
+        }
+        auto ldB = [&](int ks, int n) {
+          const int tap = ks >> 2, sub = ks & 3, dy = tap / 3, dx = tap - 3 * dy;
+          const int o = uu[n] < 10 ? cor[dx][sub] + (uu[n] + dy) * (kX2InW * 128) : coe[dx][sub] + dy * (kX2InW * 128);
+          return *reinterpret_cast<const half8_t*>(hin + o);
+        };
+        floatx16 acc[NT];
+        half8_t fb[2][NT];
+#pragma unroll
+        for (int n = 0; n < NT; ++n) fb[0][n] = ldB(0, n);
+#pragma unroll
+        for (int ks = 0; ks < kBodyKSteps; ++ks) {
+          const int r = ks & 1;
+          if (ks + 1 < kBodyKSteps) {
+#pragma unroll
+            for (int n = 0; n < NT; ++n) fb[r ^ 1][n] = ldB(ks + 1, n);
+          }
+#pragma unroll
+          for (int n = 0; n < NT; ++n)
+            acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(w[ks], fb[r][n], ks == 0 ? bias16(bl) : acc[n], 0, 0, 0);
+        }
+        if (last && X2_WEARLY) {           // part of layer 2p + 1's weights, in flight during this epilogue;
+          __builtin_amdgcn_sched_barrier(0);   // the barrier keeps the loads below the MFMAs
+          load_w(2 * p + 1, 0, X2_WEARLY);
+        }
+#pragma unroll
+        for (int n = 0; n < NT; ++n) {
+          const int y = ty0 - 1 + pr[n], x = tx0 - 1 + pc[n];
+          const bool inside = y >= 0 && y < s.H && x >= 0 && x < s.W;
+          half8_t v0 = act8_h<ACT>(acc[n], 0), v1 = act8_h<ACT>(acc[n], 8);
+          if (!inside) v0 = v1 = half8_t{};                 // the next layer's zero padding
+          if (uu[n] < 10 || col < 20) {
+            *reinterpret_cast<half8_t*>(mid + halo_off(pr[n], pc[n], 4 * m + 2 * h)) = v0;
+            *reinterpret_cast<half8_t*>(mid + halo_off(pr[n], pc[n], 4 * m + 2 * h + 1)) = v1;
+          }
+        }
+      };
+      using I2 = std::integral_constant<int, 2>;
+      using I3 = std::integral_constant<int, 3>;
+      if (rq == 0) {                                      // rows 0..4 + the edge N-tile
+        group(I3{}, 0, 1, 2, false);
+        group(I3{}, 3, 4, 10, true);
+      } else {                                            // rows 5..9
+        group(I3{}, 5, 6, 7, false);
+        group(I2{}, 8, 9, 9, true);
+      }
+      __syncthreads();
+      STK_STAMP(p, 3);
+      load_w(2 * p + 1, X2_WEARLY, kBodyKSteps);
+      // ---- layer 2p + 1: the 8 x 32 tile from the intermediate (conv_stack16's K-loop) ----
+      {
+        int com[3][4];
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+          for (int sub = 0; sub < 4; ++sub) {
+            com[dx][sub] = halo_off(4 * rq, col + dx, 2 * sub + h);
+            asm volatile("" : "+v"(com[dx][sub]));
+          }
+        auto ldB = [&](int ks, int n) {
+          const int tap = ks >> 2, sub = ks & 3, dy = tap / 3, dx = tap - 3 * dy;
+          return *reinterpret_cast<const half8_t*>(mid + com[dx][sub] + (n + dy) * (kHaloW * 128));
+        };
+        floatx16 acc[4];
+        half8_t fb[2][4];
+#pragma unroll
+        for (int n = 0; n < 4; ++n) fb[0][n] = ldB(0, n);
+#pragma unroll
+        for (int ks = 0; ks < kBodyKSteps; ++ks) {
+          const int r = ks & 1;
+          if (ks + 1 < kBodyKSteps) {
+#pragma unroll
+            for (int n = 0; n < 4; ++n) fb[r ^ 1][n] = ldB(ks + 1, n);
+          }
+#pragma unroll
+          for (int n = 0; n < 4; ++n)
+            acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(w[ks], fb[r][n], ks == 0 ? bias16(bl) : acc[n], 0, 0, 0);
+        }
+        STK_STAMP(p, 4);
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+          const int y = ty0 + 4 * rq + n;
+          const half8_t v0 = act8_h<ACT>(acc[n], 0), v1 = act8_h<ACT>(acc[n], 8);
+          half_t* row = out + (((size_t)b * s.Hp + y + s.pad) * s.Wp + tx0 + s.pad) * kWidth;
+          const __amdgpu_buffer_rsrc_t rs =
+              __builtin_amdgcn_make_buffer_rsrc(row, (short)0, y < s.H ? min(kTileW, s.W - tx0) * 128 : 0, 0x00020000);
+          const unsigned off = (unsigned)(col * 128 + 64 * m + 32 * h);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i_t, v0), rs, off, 0, kCpolDevice);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i_t, v1), rs, off + 16, 0, kCpolDevice);
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's stores done (device scope)
+      __syncthreads();
+      if (tid == 0) tile_publish(done + t, epoch + p + 1);
+      STK_STAMP(p, 5);
+    }
+    // the next pair's weights: in flight while the neighbourhood catches up
+    if (p + 1 < npairs) load_w(2 * p + 2);
+  }
+}
+
+template __global__ void conv_stack16x2_kernel<0>(half_t* __restrict__, half_t* __restrict__,
+                                                  const uint4* __restrict__, const float* __restrict__, int, ConvShape,
+                                                  int* __restrict__, int, int* __restrict__);
+template __global__ void conv_stack16x2_kernel<1>(half_t* __restrict__, half_t* __restrict__,
+                                                  const uint4* __restrict__, const float* __restrict__, int, ConvShape,
+                                                  int* __restrict__, int, int* __restrict__);
+
+// ------------------------------------------------------------------------------------
 // Head layer C -> 64 (basic_models.py:16,27-28).  Input: the fp32 NCHW denoiser input u32
 // (the same buffer the tail's residual reads), converted to fp16 (round to nearest even, as
 // every fp16 cast here) while the halo is written to LDS as one 8-B quad per pixel (channels
@@ -1400,6 +1643,10 @@ hipError_t conv_kernels_init() {
     e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kStkLds);
     if (e != hipSuccess) return e;
   }
+  for (const void* k : {(const void*)conv_stack16x2_kernel<0>, (const void*)conv_stack16x2_kernel<1>}) {
+    e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kX2Lds);
+    if (e != hipSuccess) return e;
+  }
   for (const void* k : {(const void*)conv_tail_kernel<false>, (const void*)conv_tail_kernel<true>}) {
     e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kTailLds);
     if (e != hipSuccess) return e;
@@ -1474,15 +1721,26 @@ void launch_conv_body(const half_t* in, half_t* out, const void* w, const float*
 #undef V3
 }
 
-void launch_conv_stack16(half_t* a, half_t* b, const void* w, const float* bias, int nbody, const ConvShape& s,
-                         int act, int num_cus, int* done, int epoch, int* err, hipStream_t st) {
+int launch_conv_stack16(half_t* a, half_t* b, const void* w, const float* bias, int nbody, const ConvShape& s,
+                        int act, int num_cus, int* done, int epoch, int* err, bool pairs, hipStream_t st) {
   const int grid = s.tiles < num_cus ? s.tiles : num_cus;
+  if (pairs && nbody >= 2 && (nbody & 1) == 0) {   // two layers per hand-off
+    const int np = nbody / 2;
+    if (act == 0)
+      hipLaunchKernelGGL((conv_stack16x2_kernel<0>), dim3(grid), dim3(256), kX2Lds, st, a, b, (const uint4*)w, bias,
+                         np, s, done, epoch, err);
+    else
+      hipLaunchKernelGGL((conv_stack16x2_kernel<1>), dim3(grid), dim3(256), kX2Lds, st, a, b, (const uint4*)w, bias,
+                         np, s, done, epoch, err);
+    return np & 1;
+  }
   if (act == 0)
     hipLaunchKernelGGL((conv_stack16_kernel<0>), dim3(grid), dim3(256), kStkLds, st, a, b, (const uint4*)w, bias, nbody,
                        s, done, epoch, err);
   else
     hipLaunchKernelGGL((conv_stack16_kernel<1>), dim3(grid), dim3(256), kStkLds, st, a, b, (const uint4*)w, bias, nbody,
                        s, done, epoch, err);
+  return nbody & 1;
 }
 
 void launch_conv_tail(const half_t* in, const float* xin, float* xout, const void* w, const void* w_lo,

@@ -38,11 +38,12 @@ void launch_conv_tail(const half_t* in, const float* xin, float* xout, const voi
 void launch_conv_body_f2(const half_t* in, half_t* out, const void* w16_1, const void* w16_2, const void* w32_1,
                          const void* w32_2, const float* b1, const float* b2, const ConvShape& s, int act,
                          int num_cus, hipStream_t st);
-// all nbody 64 -> 64 layers in one launch for small batches (grid = min(tiles, CUs)); the
-// result ends in a if nbody is even, else in b.  done: s.tiles progress words (zeroed once),
-// epoch: this launch's tag (advance by >= nbody + 1 per launch); err: set on a stuck wait.
-void launch_conv_stack16(half_t* a, half_t* b, const void* w, const float* bias, int nbody, const ConvShape& s,
-                         int act, int num_cus, int* done, int epoch, int* err, hipStream_t st);
+// all nbody 64 -> 64 layers in one launch for small batches (grid = min(tiles, CUs)); returns
+// where the result is (0: a, 1: b).  pairs: two layers per hand-off (conv_stack16x2, even
+// nbody), else one.  done: s.tiles progress words (zeroed once), epoch: this launch's tag
+// (advance by >= nbody + 1 per launch); err: set on a stuck wait.
+int launch_conv_stack16(half_t* a, half_t* b, const void* w, const float* bias, int nbody, const ConvShape& s,
+                        int act, int num_cus, int* done, int epoch, int* err, bool pairs, hipStream_t st);
 // one 64 -> 64 layer with split weights W_hi + W_lo (PNP_PREC_FP16W2)
 void launch_conv_body_w2(const half_t* in, half_t* out, const void* w, const void* w_lo, const float* bias,
                          const ConvShape& s, int act, int num_cus, hipStream_t st);

@@ -254,7 +254,8 @@ class Context:
     def set_body_layers(self, n: int):
         """64->64 denoiser layers per launch: 0 = auto (default: all in one persistent launch for
         batches with at most 2 tiles per CU, fused pairs when the batch has a 32-column strip per
-        CU), 1, 2 or 3 (all).  Same bits either way."""
+        CU), 1, 2, 3 (all, two layers per tile hand-off) or 4 (all, one per hand-off).  Same bits
+        either way."""
         self._check(self.lib.pnp_set_tuning(self.h, TUNE_BODY_LAYERS, int(n)))
 
     def set_ablate(self, bits: int):

@@ -205,16 +205,19 @@ def test_body_two_layers_per_launch_bit_identical(gpu_ctx, name, B, C, H, W):
                                           ("dncnn_15", 2, 1, 37, 45),                         # odd layer count
                                           ("dncnn_color_blind", 1, 3, 9, 33),                 # ReLU, tiny image
                                           ("DnCNN_nobn_nch_3_nlev_0.01", 3, 3, 50, 70)])      # ragged tiles
-def test_body_all_layers_one_launch_bit_identical(gpu_ctx, name, B, C, H, W):
-    """conv_stack16 (every body layer in one persistent launch, tiles handed between
-    workgroups through per-tile progress words) gives the one-layer launches' bits."""
+@pytest.mark.parametrize("mode", [3, 4])
+def test_body_all_layers_one_launch_bit_identical(gpu_ctx, name, B, C, H, W, mode):
+    """Every body layer in one persistent launch, tiles handed between workgroups through
+    per-tile progress words: conv_stack16x2 (mode 3: two layers per hand-off, the intermediate
+    in LDS; odd layer counts fall back to one) and conv_stack16 (mode 4: one layer per hand-off)
+    give the one-layer launches' bits."""
     rng = np.random.default_rng(12)
     w = DenoiserWeights.load_npz(os.path.join(WEIGHTS_DIR, name + ".npz"))
     x = rng.uniform(0, 1, (B, C, H, W)).astype(np.float32)
     try:
         gpu_ctx.set_body_layers(1)
         single = run_denoise(gpu_ctx, w, x)
-        gpu_ctx.set_body_layers(3)
+        gpu_ctx.set_body_layers(mode)
         stack = run_denoise(gpu_ctx, w, x)
         stack2 = run_denoise(gpu_ctx, w, x)          # a second launch: the next epoch of the progress words
     finally:

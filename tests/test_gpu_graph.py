@@ -129,14 +129,15 @@ def test_op_l1_ball_side_stream_fresh_context():
 @pytest.mark.parametrize("case", ["A_blur", "A_gray", "B_blur"])
 def test_single_image_stack_equals_per_layer(case):
     """B = 1 (the reference's call pattern): the auto choice for a single image, all body
-    layers in one persistent launch (conv_stack16), against one launch per layer, through the
+    layers in one persistent launch (conv_stack16x2, two layers per hand-off; conv_stack16, one),
+    against one launch per layer, through the
     solver: x, s and every metric, same bits; and with graph replay on (captured steps fall
     back to per-layer launches, the plain ones keep the persistent launch)."""
     ctx, m, prm, x0, xo, xt = _setup(case, 1)
     ctx.set_precision("fp16")
     ctx.set_body_layers(1)
     ref = ctx.run(m, prm, x0, xo, xt, 7)
-    for mode, graph in ((0, 0), (3, 0), (0, 1)):
+    for mode, graph in ((0, 0), (3, 0), (4, 0), (0, 1)):
         ctx.set_body_layers(mode)
         ctx.set_graph(graph)
         got = ctx.run(m, prm, x0, xo, xt, 7)
