@@ -839,8 +839,8 @@ void graph_build(pnp_ctx* ctx) {
 // buffer 0, then graph replays of two iterations, then a plain step for an odd remainder.
 // PNP_PREC_AUTO: fp16 operands where the reference's long trajectories show
 // them within 0.01 dB — ours-A / ours-B / comparisonB-2 on the blur operator (A blur 1200
-// iterations at sigma 0.01 and 0.0025: 0.0043 / 0.0023 dB; B blur 300: 0.0005; comparisonB-2
-// at m1 = 35, m2 = 5, 30 outer iterations: 0.0039) — and split fp16 (fp16x3, three MFMAs per
+// iterations at sigma 0.01 and 0.0025: 0.0028 / 0.0039 dB; B blur 300: 0.0012; comparisonB-2
+// at m1 = 35, m2 = 5, 30 outer iterations: 0.0060) — and split fp16 (fp16x3, three MFMAs per
 // product, near-fp32) everywhere else: the Id and random-sampling operators, whose
 // restorations reach 42-50 dB (fp16: gray Id 256^2 0.037 dB over 1200, A random sampling
 // 0.051 dB at sigma 0.01 and 0.113 at 0.0025 over 3000), the Poisson methods (ours-C: 0.19 dB

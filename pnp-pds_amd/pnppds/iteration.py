@@ -64,8 +64,8 @@ BM3D_METHODS = ("A-PnPPDS-BM3D", "A-PnPFBS-BM3D", "comparisonB-1", "C-PnPPDS-BM3
 # Denoiser operand precision.  'auto' (the default) leaves the choice to the library, per solve
 # (include/pnppds.h PNP_PREC_AUTO, capi.hip auto_precision), from the reference's own long
 # trajectories (tests/test_gpu_long.py): fp16 operands hold every iteration
-# within 0.01 dB only for ours-A / ours-B / comparisonB-2 on the blur operator (0.0043 dB over
-# 1200 blur iterations at sigma 0.01, 0.0023 at 0.0025; comparisonB-2 0.0039 over 30 outer); on Id and random sampling (42-50 dB
+# within 0.01 dB only for ours-A / ours-B / comparisonB-2 on the blur operator (0.0028 dB over
+# 1200 blur iterations at sigma 0.01, 0.0039 at 0.0025; comparisonB-2 0.0060 over 30 outer); on Id and random sampling (42-50 dB
 # restorations: gray Id 0.067 dB, A random sampling 0.05-0.11 dB over 3000) and for the Poisson
 # method (0.19 dB) they do not, and those run split fp16 (fp16x3: activations and weights as
 # fp16 hi + lo pairs, three MFMAs per product; <= 0.002 dB on every long golden).
