@@ -403,10 +403,13 @@ __device__ unsigned long long x8_clock[1024][2];   // per workgroup: shader-cloc
 #ifndef X8_OPQ
 #define X8_OPQ 1      // fragment addresses as opaque VGPRs (A/B builds: 0)
 #endif
+#ifndef X8_G3
+#define X8_G3 5       // groups of 3 N-subtiles in layer l (1) / layer l+1 (4): fewer group transitions; 2: prefetch depth 2 for them (A/B)
+#endif
 #ifndef X8_PADBR
 #define X8_PADBR 1    // layer l's zero-padding select skipped on interior steps by a uniform branch (A/B builds: 0)
 #endif
-template <int NT, int PLANE, class Side>
+template <int NT, int PLANE, class Side, int D = 2>
 __device__ __forceinline__ void x8_kloop(const half8_t (&wA)[kX8KSteps][2], const unsigned char* ring,
                                          const int (&ad)[NT][3], floatx4 (&acc)[NT][2], Side&& side,
                                          const floatx4 (&c0)[2]) {
@@ -426,7 +429,6 @@ __device__ __forceinline__ void x8_kloop(const half8_t (&wA)[kX8KSteps][2], cons
     const int tap = ks >> 1, hs = ks & 1, dy = tap / 3, dx = tap - 3 * dy;
     return *(lds_h8p)(size_t)(unsigned)(av[n][dy] + (4 * hs * PLANE + 16 * dx));
   };
-  constexpr int D = 2;
   half8_t fb[D + 1][NT];
 #pragma unroll
   for (int d = 0; d < D; ++d)
@@ -572,12 +574,14 @@ __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __re
         const bool all_in = 8 * jb + 8 <= s.H && x0 + kTileW <= s.W;   // rows and columns of u < 16 inside
         // N-subtile u < 16: row u >> 1, columns 1 + 16 (u & 1) .. +15; u == 16: the strip halo
         // (columns 0 and 33 of the 8 rows: pixel px -> row px >> 1, column px & 1 ? 33 : 0)
-        auto group = [&](auto ntc, int u0, int u1, bool first) {
+        auto group = [&](auto ntc, int u0, int u1, int u2, bool first) {
           constexpr int NT = decltype(ntc)::value;
-          int ad[NT][3], prow[NT], pcol[NT];
+          constexpr int DP = NT >= 3 && !(X8_G3 & 2) ? 1 : 2;   // fragment prefetch depth (registers)
+          int ad[NT][3], prow[NT], pcol[NT], uu[NT];
 #pragma unroll
           for (int n = 0; n < NT; ++n) {
-            const int u = n == 0 ? u0 : u1;
+            const int u = n == 0 ? u0 : n == 1 ? u1 : u2;
+            uu[n] = u;
             prow[n] = u < 16 ? u >> 1 : px >> 1;
             pcol[n] = u < 16 ? 1 + 16 * (u & 1) + px : ((px & 1) ? kF2MidW - 1 : 0);
 #pragma unroll
@@ -589,15 +593,15 @@ __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __re
             }
           }
           floatx4 acc[NT][2];
-          if (first) x8_kloop<NT, kF2InPlane>(wA, ring, ad, acc, side, c0);
-          else x8_kloop<NT, kF2InPlane>(wA, ring, ad, acc, noside, c0);
+          if (first) x8_kloop<NT, kF2InPlane, decltype(side)&, DP>(wA, ring, ad, acc, side, c0);
+          else x8_kloop<NT, kF2InPlane, decltype(noside)&, DP>(wA, ring, ad, acc, noside, c0);
           auto epi = [&](bool masked) {
 #pragma unroll
             for (int n = 0; n < NT; ++n) {
               const int x = x0 - 1 + pcol[n];
               const bool inside = 8 * jb + prow[n] < s.H && x >= 0 && x < s.W;
               half8_t v = x8_act<ACT>(acc[n]);
-              if ((masked || (n == 0 ? u0 : u1) == 16) && !inside) v = half8_t{};   // the next layer's zero padding
+              if ((masked || uu[n] == 16) && !inside) v = half8_t{};   // the next layer's zero padding
               *reinterpret_cast<half8_t*>(mid + (4 * m + g) * kF2MidPlane +
                                           (f2_slot(8 * J + prow[n]) * kF2MidW + pcol[n]) * 16) = v;
             }
@@ -608,17 +612,28 @@ __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __re
         };
         using I1 = std::integral_constant<int, 1>;
         using I2 = std::integral_constant<int, 2>;
-        if (half == 0) {                                 // rows 0-3 + the halo: 9 N-subtiles
-          group(I2{}, 0, 1, true);
-          group(I2{}, 2, 3, false);
-          group(I2{}, 4, 5, false);
-          group(I2{}, 6, 7, false);
-          group(I1{}, 16, 16, false);
+        using I3 = std::integral_constant<int, 3>;
+        if (X8_G3 & 1) {                                 // groups of 3 N-subtiles: fewer group transitions
+          if (half == 0) {
+            group(I3{}, 0, 1, 2, true);
+            group(I3{}, 3, 4, 5, false);
+            group(I3{}, 6, 7, 16, false);
+          } else {
+            group(I3{}, 8, 9, 10, true);
+            group(I3{}, 11, 12, 13, false);
+            group(I2{}, 14, 15, 15, false);
+          }
+        } else if (half == 0) {                          // rows 0-3 + the halo: 9 N-subtiles
+          group(I2{}, 0, 1, 1, true);
+          group(I2{}, 2, 3, 3, false);
+          group(I2{}, 4, 5, 5, false);
+          group(I2{}, 6, 7, 7, false);
+          group(I1{}, 16, 16, 16, false);
         } else {                                         // rows 4-7: 8
-          group(I2{}, 8, 9, true);
-          group(I2{}, 10, 11, false);
-          group(I2{}, 12, 13, false);
-          group(I2{}, 14, 15, false);
+          group(I2{}, 8, 9, 9, true);
+          group(I2{}, 10, 11, 11, false);
+          group(I2{}, 12, 13, 13, false);
+          group(I2{}, 14, 15, 15, false);
         }
       } else {
 #pragma unroll 1
@@ -641,34 +656,50 @@ __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __re
           sl = sl == kF2Ring - 1 ? 0 : sl + 1;
         }
         const int lb = g * kF2MidPlane + px * 16;
-        auto group = [&](int t, bool first) {
-          int ad[2][3];
-#pragma unroll
-          for (int n = 0; n < 2; ++n)
-#pragma unroll
-            for (int dy = 0; dy < 3; ++dy) ad[n][dy] = lb + rowoff[t + dy] + 16 * 16 * n;
-          floatx4 acc[2][2];
-          if (first) x8_kloop<2, kF2MidPlane>(wA, mid, ad, acc, side, c0);
-          else x8_kloop<2, kF2MidPlane>(wA, mid, ad, acc, noside, c0);
+        auto rowrs = [&](int t) {                      // output row t's store descriptor
           const int R = 8 * J - 9 + 4 * half + t;
           int k, r;
           locate(R, kJ, k, r);
           const bool ok = R >= 0 && k < K && r < s.H;
           const SGeom G = pick(k);
           half_t* row = out + (((size_t)G.b * s.Hp + r + s.pad) * s.Wp + G.x0 + s.pad) * kWidth;
-          const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-              ok ? (void*)row : (void*)out, (short)0, ok ? min(kTileW, s.W - G.x0) * 128 : 0, 0x00020000);
+          return __builtin_amdgcn_make_buffer_rsrc(ok ? (void*)row : (void*)out, (short)0,
+                                                   ok ? min(kTileW, s.W - G.x0) * 128 : 0, 0x00020000);
+        };
+        // N-subtile v = 0..7: output row t = v >> 1, columns 16 (v & 1) .. +15
+        auto group = [&](auto ntc, int v0, int v1, int v2, bool first) {
+          constexpr int NT = decltype(ntc)::value;
+          constexpr int DP = NT >= 3 && !(X8_G3 & 2) ? 1 : 2;
+          int ad[NT][3], vv[NT];
 #pragma unroll
-          for (int n = 0; n < 2; ++n) {
+          for (int n = 0; n < NT; ++n) {
+            vv[n] = n == 0 ? v0 : n == 1 ? v1 : v2;
+#pragma unroll
+            for (int dy = 0; dy < 3; ++dy) ad[n][dy] = lb + rowoff[(vv[n] >> 1) + dy] + 16 * 16 * (vv[n] & 1);
+          }
+          floatx4 acc[NT][2];
+          if (first) x8_kloop<NT, kF2MidPlane, decltype(side)&, DP>(wA, mid, ad, acc, side, c0);
+          else x8_kloop<NT, kF2MidPlane, decltype(noside)&, DP>(wA, mid, ad, acc, noside, c0);
+#pragma unroll
+          for (int n = 0; n < NT; ++n) {
             const half8_t v = x8_act<ACT>(acc[n]);
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i_t, v), rs,
-                                                   (unsigned)((16 * n + px) * 128 + 64 * m + 16 * g), 0, kNtX8);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i_t, v), rowrs(vv[n] >> 1),
+                                                   (unsigned)((16 * (vv[n] & 1) + px) * 128 + 64 * m + 16 * g), 0,
+                                                   kNtX8);
           }
         };
-        group(0, true);
-        group(1, false);
-        group(2, false);
-        group(3, false);
+        using I2 = std::integral_constant<int, 2>;
+        using I3 = std::integral_constant<int, 3>;
+        if (X8_G3 & 4) {
+          group(I3{}, 0, 1, 2, true);
+          group(I3{}, 3, 4, 5, false);
+          group(I2{}, 6, 7, 7, false);
+        } else {
+          group(I2{}, 0, 1, 1, true);
+          group(I2{}, 2, 3, 3, false);
+          group(I2{}, 4, 5, 5, false);
+          group(I2{}, 6, 7, 7, false);
+        }
         asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // the DMAs (older than the 8 stores) landed
       } else {
 #pragma unroll 1
@@ -1656,6 +1687,7 @@ hipError_t conv_kernels_init() {
 
 void launch_conv_head(const float* in32, int C, half_t* out, const void* w, const void* w_lo, const float* bias,
                       const ConvShape& s, int act, int num_cus, int blocks_per_cu, hipStream_t st, half_t* out_lo) {
+  // (grid of 2 / 3 / 4 / 6 blocks per CU at the metric: 0.453 / 0.548 / 0.461 / 0.459 ms, r03)
   const int grid = s.tiles < num_cus * blocks_per_cu ? s.tiles : num_cus * blocks_per_cu;
 #define HEAD(PV, NCV)                                                                                            \
   hipLaunchKernelGGL((conv_head_kernel<PV, NCV>), dim3(grid), dim3(256), 0, st, in32, C, out, out_lo,              \
