@@ -75,6 +75,27 @@ __device__ __forceinline__ int xcd_block_s3(int b, int G) {   // as conv.hip xcd
 }
 
 // MODE 0: body 64 -> 64 (hi/lo out).  MODE 1: tail 64 -> C + residual + clamp (fp32 NCHW out).
+#ifndef S3_EPI
+#define S3_EPI 3      // body epilogue: 1 = bias as the first MFMA's C operand, 2 = activation max without
+#endif                // the compiler's canonicalizing v_max (A/B builds: 0)
+// C operand of a tile's first MFMA: the bias (body, S3_EPI & 1) or zero (the tail adds its own)
+template <int MODE>
+__device__ __forceinline__ floatx4 s3_c0(const float* bl) {
+  if (MODE == 0 && (S3_EPI & 1)) return floatx4{bl[0], bl[1], bl[2], bl[3]};
+  return floatx4{};
+}
+// bias (unless already in the accumulator) + activation in fp32, then the hi / lo fp16 halves
+template <int ACT>
+__device__ __forceinline__ void s3_split(float a, float b, h4_t& hi, h4_t& lo, int i) {
+  float v = (S3_EPI & 1) ? a : a + b;
+  const float t = ACT == 0 ? v * 0.01f : 0.f;
+  if (S3_EPI & 2) asm("v_max_f32 %0, %1, %2" : "=v"(v) : "v"(v), "v"(t));
+  else v = fmaxf(v, t);
+  const half_t h = (half_t)v;
+  hi[i] = h;
+  lo[i] = (half_t)(v - (float)h);
+}
+
 template <int MODE, int ACT>
 __global__ __launch_bounds__(512, 1) void conv_s3_kernel(const half_t* __restrict__ in_hi,
                                                           const half_t* __restrict__ in_lo,
@@ -203,7 +224,7 @@ __global__ __launch_bounds__(512, 1) void conv_s3_kernel(const half_t* __restric
       }
 #pragma unroll
       for (int n = 0; n < NT; ++n)
-        acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wH[ks], bh[r][n], ks == 0 ? floatx4{} : acc[n], 0, 0, 0);
+        acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wH[ks], bh[r][n], ks == 0 ? s3_c0<MODE>(bl) : acc[n], 0, 0, 0);
 #pragma unroll
       for (int n = 0; n < NT; ++n) acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wL[ks], bh[r][n], acc[n], 0, 0, 0);
 #pragma unroll
@@ -224,12 +245,7 @@ __global__ __launch_bounds__(512, 1) void conv_s3_kernel(const half_t* __restric
         const int y = ty0 + row0 + n;
         h4_t hi, lo;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          float v = acc[n][i] + bl[i];
-          v = ACT == 0 ? fmaxf(v, v * 0.01f) : fmaxf(v, 0.f);
-          hi[i] = (half_t)v;
-          lo[i] = (half_t)(v - (float)hi[i]);
-        }
+        for (int i = 0; i < 4; ++i) s3_split<ACT>(acc[n][i], bl[i], hi, lo, i);
         const size_t rowb = (((size_t)b * s.Hp + y + s.pad) * s.Wp + tx0 + s.pad) * kWidth;
         const int nrec = y < s.H ? min(kS3TileW, s.W - tx0) * 128 : 0;
         const unsigned off = (unsigned)(px * 128 + (16 * mt + 4 * grp) * 2);
@@ -391,7 +407,7 @@ __global__ __launch_bounds__(256, 1) void conv_stack_s3_kernel(half_t* __restric
           }
 #pragma unroll
           for (int n = 0; n < 4; ++n)
-            acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wH[ks], bh[r][n], ks == 0 ? floatx4{} : acc[n], 0, 0, 0);
+            acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wH[ks], bh[r][n], ks == 0 ? s3_c0<0>(bl) : acc[n], 0, 0, 0);
 #pragma unroll
           for (int n = 0; n < 4; ++n) acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wL[ks], bh[r][n], acc[n], 0, 0, 0);
 #pragma unroll
@@ -402,12 +418,7 @@ __global__ __launch_bounds__(256, 1) void conv_stack_s3_kernel(half_t* __restric
           const int y = ty0 + 4 * gq + n;
           h4_t hi, lo;
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            float v = acc[n][i] + bl[i];
-            v = ACT == 0 ? fmaxf(v, v * 0.01f) : fmaxf(v, 0.f);
-            hi[i] = (half_t)v;
-            lo[i] = (half_t)(v - (float)hi[i]);
-          }
+          for (int i = 0; i < 4; ++i) s3_split<ACT>(acc[n][i], bl[i], hi, lo, i);
           const size_t rowb = (((size_t)b * s.Hp + y + s.pad) * s.Wp + tx0 + s.pad) * kWidth;
           const int nrec = y < s.H ? min(kS3TileW, s.W - tx0) * 128 : 0;
           const unsigned off = (unsigned)(px * 128 + (16 * mt + 4 * grp) * 2);
