@@ -233,6 +233,7 @@ OpDesc op_desc(pnp_ctx* ctx) {
   d.dense_adj = ctx->op_kind == PNP_OP_BLUR ? P<const float>(ctx->dense_adj) : nullptr;
   d.Rd = ctx->op_kind == PNP_OP_BLUR ? dense_radius(ctx->op_R) : 0;
   d.taps_id = ctx->op_kind == PNP_OP_BLUR ? ctx->op_taps_id : TAPS_DENSE;
+  d.num_cus = ctx->num_cus;
   return d;
 }
 

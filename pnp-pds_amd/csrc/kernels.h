@@ -91,6 +91,7 @@ struct OpDesc {
   const float* dense_adj; //   [p = 0..Rd][oy + Rd][2][2], see pack_tap_pairs
   int Rd;                 // radius of the dense tables: smallest of {2, 4, 8} >= R, 0 if R > 8
   int taps_id;            // compile-time tap pattern (TAPS_*) the stencils are specialised on, 0 = dense
+  int num_cus;            // the device's CUs (grids smaller than this take the latency variants)
 };
 inline int dense_radius(int R) { return R <= 2 ? 2 : R <= 4 ? 4 : R <= 8 ? 8 : 0; }
 enum { TAPS_DENSE = 0, TAPS_BLUR_1 = 1, TAPS_SQUARE_MINI = 2 };

@@ -1001,7 +1001,9 @@ struct RbRows {
 // K1: u = [clamp](x - g1 Phi^T y) -> u32 (the denoiser's input; its head converts to fp16);
 // B (MB): w = s - g1 y.  Block = one (plane, 64 x 64 tile).  B's y comes
 // from the halo in LDS (it is the stencil's input), so K1 reads y once.
-template <class T, bool MB>
+// LAT (small grids, fewer blocks than CUs: B = 1): every halo load of a thread in flight at
+// once instead of in batches of 8 (the batches keep registers low for 6 blocks per CU).
+template <class T, bool MB, int LAT = 0>
 __global__ __launch_bounds__(256) void k1_blur_rb(const float* __restrict__ x, const float* __restrict__ y,
                                                    const float* __restrict__ s, float* __restrict__ u32,
                                                    float* __restrict__ w, const f2_t* __restrict__ wd_adj, int H, int W,
@@ -1018,7 +1020,7 @@ __global__ __launch_bounds__(256) void k1_blur_rb(const float* __restrict__ x, c
   RbRows rw;
   rw.init(pb, i0, j, H, W);
   const float* yp = y + pb;
-  rb_fill_cols<G>(lds, i0, j0, H, W, [&](int k) { return yp[k]; });
+  rb_fill_cols<G, LAT ? 32 : kRbFill>(lds, i0, j0, H, W, [&](int k) { return yp[k]; });
   __syncthreads();
   f2_t g[kRbRows];
   rb_stencil<T>(lds, wd_adj, g);
@@ -1087,17 +1089,17 @@ __global__ __launch_bounds__(256) void k0_blur_rb(const float* __restrict__ x, f
 // tile's own pixels from the same loads: e2 = sum (xn - xo)^2, n2 = sum xo^2 (c_n,
 // iteration.py:187) and t2 = sum (xt - xn)^2 (PSNR, :188; x_true loaded for those pixels
 // only).  Each batch's <= kRbFill terms are summed in fp32, then added once into fp64.
-template <class G, int K0 = 0>
+template <class G, int FB = kRbFill, int K0 = 0>
 __device__ __forceinline__ void rb_fill_k2(float* lds, int i0, int j0, int H, int W, const float* xnp,
                                            const float* xop, const float* xtp, bool record, double& e2, double& n2,
                                            double& t2, float& lo, float& hi) {
-  constexpr int K1 = K0 + kRbFill < G::NF ? K0 + kRbFill : G::NF;
+  constexpr int K1 = K0 + FB < G::NF ? K0 + FB : G::NF;
   const int tid = threadIdx.x;
   const int ly0 = tid / G::LW, lx0 = tid - ly0 * G::LW;
   const int ci = i0 - G::R, cj = j0 - G::R + G::kOff;
   const int ie = min(i0 + kRbH, H), je = min(j0 + kRbW, W);
-  float a[kRbFill], bb[kRbFill], t[kRbFill];
-  bool in[kRbFill];
+  float a[FB], bb[FB], t[FB];
+  bool in[FB];
 #pragma unroll
   for (int k = K0; k < K1; ++k) {
     const int dy = (256 * k) / G::LW, dx = (256 * k) % G::LW;
@@ -1121,9 +1123,17 @@ __device__ __forceinline__ void rb_fill_k2(float* lds, int i0, int j0, int H, in
     in[k - K0] = record && valid && ui >= i0 && ui < ie && uj >= j0 && uj < je;
     t[k - K0] = (in[k - K0] && xtp) ? xtp[idx] : 0.f;
   }
+  // the fp32 partial sums are flushed into fp64 every kRbFill elements (of the absolute index k),
+  // so the sums are the same bits whatever the load batch FB
   float be = 0.f, bn = 0.f, bt = 0.f;
 #pragma unroll
   for (int k = K0; k < K1; ++k) {
+    if (k > K0 && k % kRbFill == 0) {
+      e2 += be;
+      n2 += bn;
+      t2 += bt;
+      be = bn = bt = 0.f;
+    }
     const int q = tid + 256 * k;
     const float av = a[k - K0], bv = bb[k - K0];
     if (G::N % 256 == 0 || q < G::N) lds[q] = 2.f * av - bv;
@@ -1138,7 +1148,7 @@ __device__ __forceinline__ void rb_fill_k2(float* lds, int i0, int j0, int H, in
   e2 += be;
   n2 += bn;
   t2 += bt;
-  if constexpr (K1 < G::NF) rb_fill_k2<G, K1>(lds, i0, j0, H, W, xnp, xop, xtp, record, e2, n2, t2, lo, hi);
+  if constexpr (K1 < G::NF) rb_fill_k2<G, FB, K1>(lds, i0, j0, H, W, xnp, xop, xtp, record, e2, n2, t2, lo, hi);
 }
 
 // K2: v = y + g2 (Phi(2x+ - x) [+ 2 s+ - s]), s+ = shrink(w, theta) (B), the GKL prox (C),
@@ -1148,7 +1158,7 @@ __device__ __forceinline__ void rb_fill_k2(float* lds, int i0, int j0, int H, in
 // x_obs (and B's s, w) and nothing is read twice.  partials: [B][cells][C][4] (per 32 x 32
 // cell and channel), reduced by k3 in that order: d2 per cell, e2 / n2 / t2 per tile in the
 // tile's first cell (zeros in the others).
-template <class T, int METHOD>
+template <class T, int METHOD, int LAT = 0>   // LAT: as k1_blur_rb, and all 8 epilogue rows' loads in flight
 __global__ __launch_bounds__(256) void k2_blur_rb(const float* __restrict__ xn, const float* __restrict__ xo,
                                                    float* __restrict__ y, const float* __restrict__ xobs,
                                                    const float* __restrict__ xtrue, float* __restrict__ s,
@@ -1175,7 +1185,7 @@ __global__ __launch_bounds__(256) void k2_blur_rb(const float* __restrict__ xn, 
   {
     double e2 = 0, n2 = 0, t2 = 0;
     float lo = __builtin_inff(), hi = -__builtin_inff();
-    rb_fill_k2<G>(lds, i0, j0, H, W, xn + (size_t)bc * plane, xo + (size_t)bc * plane,
+    rb_fill_k2<G, LAT ? G::NF : kRbFill>(lds, i0, j0, H, W, xn + (size_t)bc * plane, xo + (size_t)bc * plane,
                   xtrue ? xtrue + (size_t)bc * plane : nullptr, record != 0, e2, n2, t2, lo, hi);
     if (record) {                            // reduced here, so no fill value stays live past the fill
       e2 = wave_sum(e2);
@@ -1203,12 +1213,13 @@ __global__ __launch_bounds__(256) void k2_blur_rb(const float* __restrict__ xn, 
   double d2 = 0;
   {
     const float th = METHOD == M_B ? theta[b] : 0.f;
-    // kRbBatch rows at a time: every stream's loads of the batch are issued before the first use
+    // EB rows at a time: every stream's loads of the batch are issued before the first use
+    constexpr int EB = LAT ? kRbRows : kRbBatch;
 #pragma unroll
-    for (int rb = 0; rb < kRbRows; rb += kRbBatch) {
-      f2_t yv[kRbBatch], bv[kRbBatch], sv[kRbBatch], wv[kRbBatch];
+    for (int rb = 0; rb < kRbRows; rb += EB) {
+      f2_t yv[EB], bv[EB], sv[EB], wv[EB];
 #pragma unroll
-      for (int k = 0; k < kRbBatch; ++k) {
+      for (int k = 0; k < EB; ++k) {
         const bool vec = al && rw.nv(rb + k) == 2;
         yv[k] = ld2g(y, rw.ix(rb + k), rw.nv(rb + k), vec);
         bv[k] = ld2g(xobs, rw.ix(rb + k), rw.nv(rb + k), vec);
@@ -1218,7 +1229,7 @@ __global__ __launch_bounds__(256) void k2_blur_rb(const float* __restrict__ xn, 
         }
       }
 #pragma unroll
-      for (int k = 0; k < kRbBatch; ++k) {
+      for (int k = 0; k < EB; ++k) {
         const int r = rb + k;
         f2_t yo = yv[k], so = {0.f, 0.f};
 #pragma unroll
@@ -1555,12 +1566,13 @@ template <class T>
 static void launch_k1_rb(hipStream_t st, const float* x, const float* y, const float* s, float* u32, float* w,
                          const OpDesc& op, int B, int C, int H, int W, float gamma1, int clamp_in, int method_b) {
   const int tx = (W + kRbW - 1) / kRbW, tiles = tx * ((H + kRbH - 1) / kRbH);
-  if (method_b)
-    hipLaunchKernelGGL((k1_blur_rb<T, true>), dim3(B * C * tiles), dim3(256), 0, st, x, y, s, u32, w,
-                       reinterpret_cast<const f2_t*>(op.dense_adj), H, W, tx, tiles, gamma1, clamp_in);
-  else
-    hipLaunchKernelGGL((k1_blur_rb<T, false>), dim3(B * C * tiles), dim3(256), 0, st, x, y, s, u32, w,
-                       reinterpret_cast<const f2_t*>(op.dense_adj), H, W, tx, tiles, gamma1, clamp_in);
+  const bool lat = B * C * tiles < op.num_cus;     // one block per CU at most: latency-bound
+#define K1RBL(MBV, L)                                                                                      \
+  hipLaunchKernelGGL((k1_blur_rb<T, MBV, L>), dim3(B * C * tiles), dim3(256), 0, st, x, y, s, u32, w,       \
+                     reinterpret_cast<const f2_t*>(op.dense_adj), H, W, tx, tiles, gamma1, clamp_in)
+  if (method_b) { if (lat) K1RBL(true, 1); else K1RBL(true, 0); }
+  else { if (lat) K1RBL(false, 1); else K1RBL(false, 0); }
+#undef K1RBL
 }
 
 void launch_k1(int kind, const float* x, const float* y, const float* s, float* u32, float* w,
@@ -1627,11 +1639,16 @@ static void launch_k2_rb(int method, hipStream_t st, const float* xn, const floa
                          double gkl_gamma, double gkl_alpha, int record, float* mm) {
   const int tx = (W + kRbW - 1) / kRbW, tiles = tx * ((H + kRbH - 1) / kRbH);
   const dim3 grid(B * C * tiles);
+  const bool lat = B * C * tiles < op.num_cus;     // one block per CU at most: latency-bound
 #define K2RB_ARGS xn, xo, y, xobs, xtrue, s, w, theta, partials, reinterpret_cast<const f2_t*>(op.dense_fwd), C, H, W, \
                   tx, tiles, cells_x, cells, gamma2, 1.0 / gamma2, gkl_gamma, gkl_alpha, record, mm
-  if (method == M_A) hipLaunchKernelGGL((k2_blur_rb<T, M_A>), grid, dim3(256), 0, st, K2RB_ARGS);
-  else if (method == M_B) hipLaunchKernelGGL((k2_blur_rb<T, M_B>), grid, dim3(256), 0, st, K2RB_ARGS);
-  else hipLaunchKernelGGL((k2_blur_rb<T, M_C>), grid, dim3(256), 0, st, K2RB_ARGS);
+#define K2RBL(M)                                                                                              \
+  if (lat) hipLaunchKernelGGL((k2_blur_rb<T, M, 1>), grid, dim3(256), 0, st, K2RB_ARGS);                       \
+  else hipLaunchKernelGGL((k2_blur_rb<T, M, 0>), grid, dim3(256), 0, st, K2RB_ARGS);
+  if (method == M_A) { K2RBL(M_A) }
+  else if (method == M_B) { K2RBL(M_B) }
+  else { K2RBL(M_C) }
+#undef K2RBL
 #undef K2RB_ARGS
 }
 
