@@ -541,7 +541,7 @@ __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __re
   auto dma_plane = [&](int c) {
     if (lane < kF2InW)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(dsrc, (__attribute__((address_space(3))) void*)(ddst + c * kF2InPlane),
-                                               16, dvo + 16 * c, 0, 0, 0);
+                                               16, dvo + 16 * c, 0, 0, 0);   // (nt: 2.17 -> 2.52 ms, r03)
   };
   for (int r = wave; r < 10; r += 8) {
     dma_at(r - 1, 0);
