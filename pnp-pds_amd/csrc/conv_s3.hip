@@ -67,6 +67,35 @@ __device__ __forceinline__ void s3_decode(int t, const S3Geom& g, int& b, int& t
   tx0 = (r - ty * g.tiles_x) * kS3TileW;
 }
 
+// Tile t -> (b, ty0, tx0) stepped by the grid stride G without divisions (two runtime divisions
+// per decode cost ~50 instructions per tile and wave): G's mixed-radix digits are added with
+// carries; past the last tile the coordinates stay on it (the clamped DMA of the last tiles).
+struct S3Iter {
+  int t, b, ty, tx, gb, gty, gtx, tiles, tiles_x, tiles_y;
+  __device__ __forceinline__ void init(int t0, int G, const S3Geom& g) {
+    t = t0;
+    tiles = g.tiles;
+    tiles_x = g.tiles_x;
+    tiles_y = g.tiles_y;
+    const int per = g.tiles_x * g.tiles_y, tc = min(t0, g.tiles - 1);
+    b = tc / per;
+    ty = (tc - b * per) / g.tiles_x;
+    tx = tc - b * per - ty * g.tiles_x;
+    gb = G / per;
+    gty = (G - gb * per) / g.tiles_x;
+    gtx = G - gb * per - gty * g.tiles_x;
+  }
+  __device__ __forceinline__ void next(int G) {
+    t += G;
+    if (t >= tiles) return;                              // stays on the last tile
+    tx += gtx;
+    if (tx >= tiles_x) { tx -= tiles_x; ++ty; }
+    ty += gty;
+    if (ty >= tiles_y) { ty -= tiles_y; ++b; }
+    b += gb;
+  }
+};
+
 // chunk swizzle of halo column pc: f = {0,1,2,4,5,6,2,6,0}[pc >> 1], 3 bits each
 __device__ __forceinline__ int s3_swz(int pc) { return (0x00CB5888u >> (3 * (pc >> 1))) & 7; }
 
@@ -139,9 +168,8 @@ __global__ __launch_bounds__(512, 1) void conv_s3_kernel(const half_t* __restric
     const int pr = p / kS3HaloW, pc = p - pr * kS3HaloW;
     doff[j] = (unsigned)(((pr * s.Wp + pc) * kWidth + 8 * ((lane & 7) ^ s3_swz(pc))) * 2);
   }
-  auto issue = [&](int tt, int bi) {                    // clamped: always kS3Pieces instructions
-    int b, ty0, tx0;
-    s3_decode(tt < g.tiles ? tt : g.tiles - 1, g, b, ty0, tx0);
+  auto issue = [&](const S3Iter& ti, int bi) {          // clamped: always kS3Pieces instructions
+    const int b = ti.b, ty0 = ti.ty * kS3TileH, tx0 = ti.tx * kS3TileW;
     const size_t base = (((size_t)b * s.Hp + ty0 + s.pad - 1) * s.Wp + tx0 + s.pad - 1) * kWidth;
     const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc((void*)(in_hi + base), (short)0, 0x7fffffff,
                                                                         0x00020000);
@@ -166,17 +194,22 @@ __global__ __launch_bounds__(512, 1) void conv_s3_kernel(const half_t* __restric
       lofs[dx][hs] = (unsigned)((px + dx) * 128 + 16 * ((4 * hs + grp) ^ s3_swz(px + dx)));
   const int G = gridDim.x;
   int t = xcd_block_s3(blockIdx.x, G);
+  S3Iter it, itd;                                       // this tile; the tile two strides ahead (DMA)
+  it.init(t, G, g);
+  itd.init(t, G, g);
   if (t < g.tiles) {
-    issue(t, 0);
-    issue(t + G, 1);
+    issue(itd, 0);
+    itd.next(G);
+    issue(itd, 1);
+    itd.next(G);
     asm volatile("s_waitcnt vmcnt(6)" ::: "memory");   // tile t landed
   }
   __syncthreads();
   const unsigned plane = (unsigned)(s.H * s.W);
   int cur = 0;
   for (; t < g.tiles; t += G) {
-    int b, ty0, tx0;
-    s3_decode(t, g, b, ty0, tx0);
+    const int b = it.b, ty0 = it.ty * kS3TileH, tx0 = it.tx * kS3TileW;
+    it.next(G);
     // tail: the residual input, loaded before this tile's DMA issue (so waiting for it never
     // waits on the DMA); always kMaxC loads (c >= C: zero-size descriptor)
     float xi[MODE == 1 ? kMaxC : 1];
@@ -193,7 +226,8 @@ __global__ __launch_bounds__(512, 1) void conv_s3_kernel(const half_t* __restric
       }
       __builtin_amdgcn_sched_barrier(0);
     }
-    issue(t + 2 * G, cur >= 1 ? cur - 1 : 2);
+    issue(itd, cur >= 1 ? cur - 1 : 2);
+    itd.next(G);
     const unsigned char* fb = smem + cur * kS3Buf + row0 * kS3HaloW * 128;
     auto ldB = [&](int ks, int n, int lo) {
       const int tap = ks >> 1, dy = tap / 3, dx = tap - 3 * dy;
