@@ -406,10 +406,14 @@ __device__ unsigned long long x8_clock[1024][2];   // per workgroup: shader-cloc
 #ifndef X8_G3
 #define X8_G3 5       // groups of 3 N-subtiles in layer l (1) / layer l+1 (4): fewer group transitions; 2: prefetch depth 2 for them (A/B)
 #endif
+#ifndef X8_HSPLIT
+#define X8_HSPLIT 1   // the strip-halo N-subtile's two A-subtiles on the two halves' waves: 306 MFMAs per SIMD-pair and step each instead of 324 / 288 (A/B builds: 0)
+#endif
 #ifndef X8_PADBR
 #define X8_PADBR 1    // layer l's zero-padding select skipped on interior steps by a uniform branch (A/B builds: 0)
 #endif
-template <int NT, int PLANE, class Side, int D = 2>
+// QL: the A-subtiles (bit q) computed for the last N-subtile (the strip halo's split, X8_HSPLIT).
+template <int NT, int PLANE, class Side, int D = 2, int QL = 3>
 __device__ __forceinline__ void x8_kloop(const half8_t (&wA)[kX8KSteps][2], const unsigned char* ring,
                                          const int (&ad)[NT][3], floatx4 (&acc)[NT][2], Side&& side,
                                          const floatx4 (&c0)[2]) {
@@ -444,8 +448,9 @@ __device__ __forceinline__ void x8_kloop(const half8_t (&wA)[kX8KSteps][2], cons
     for (int n = 0; n < NT; ++n)
 #pragma unroll
       for (int q = 0; q < 2; ++q)
-        acc[n][q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wA[ks][q], fb[ks % (D + 1)][n],
-                                                           ks == 0 ? c0[q] : acc[n][q], 0, 0, 0);
+        if (n < NT - 1 || ((QL >> q) & 1))
+          acc[n][q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wA[ks][q], fb[ks % (D + 1)][n],
+                                                             ks == 0 ? c0[q] : acc[n][q], 0, 0, 0);
     side(ks);
     __builtin_amdgcn_sched_barrier(0);
   }
@@ -574,8 +579,10 @@ __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __re
         const bool all_in = 8 * jb + 8 <= s.H && x0 + kTileW <= s.W;   // rows and columns of u < 16 inside
         // N-subtile u < 16: row u >> 1, columns 1 + 16 (u & 1) .. +15; u == 16: the strip halo
         // (columns 0 and 33 of the 8 rows: pixel px -> row px >> 1, column px & 1 ? 33 : 0)
-        auto group = [&](auto ntc, int u0, int u1, int u2, bool first) {
-          constexpr int NT = decltype(ntc)::value;
+        // QL (qlc): the A-subtiles computed for the group's last N-subtile (X8_HSPLIT: the strip
+        // halo's q = 0 on half 0's wave, q = 1 on half 1's; each writes its 4 channels, 8 B)
+        auto group = [&](auto ntc, auto qlc, int u0, int u1, int u2, bool first) {
+          constexpr int NT = decltype(ntc)::value, QL = decltype(qlc)::value;
           constexpr int DP = NT >= 3 && !(X8_G3 & 2) ? 1 : 2;   // fragment prefetch depth (registers)
           int ad[NT][3], prow[NT], pcol[NT], uu[NT];
 #pragma unroll
@@ -593,13 +600,23 @@ __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __re
             }
           }
           floatx4 acc[NT][2];
-          if (first) x8_kloop<NT, kF2InPlane, decltype(side)&, DP>(wA, ring, ad, acc, side, c0);
-          else x8_kloop<NT, kF2InPlane, decltype(noside)&, DP>(wA, ring, ad, acc, noside, c0);
+          if (first) x8_kloop<NT, kF2InPlane, decltype(side)&, DP, QL>(wA, ring, ad, acc, side, c0);
+          else x8_kloop<NT, kF2InPlane, decltype(noside)&, DP, QL>(wA, ring, ad, acc, noside, c0);
           auto epi = [&](bool masked) {
 #pragma unroll
             for (int n = 0; n < NT; ++n) {
               const int x = x0 - 1 + pcol[n];
               const bool inside = 8 * jb + prow[n] < s.H && x >= 0 && x < s.W;
+              if (n == NT - 1 && QL != 3) {              // one A-subtile: channels 8g + 4q .. +3
+                constexpr int q = QL == 1 ? 0 : 1;
+                const h2v_t h0 = act_h2<ACT>(f2v_t{acc[n][q][0], acc[n][q][1]});
+                const h2v_t h1 = act_h2<ACT>(f2v_t{acc[n][q][2], acc[n][q][3]});
+                half4_t v = half4_t{h0.x, h0.y, h1.x, h1.y};
+                if (!inside) v = half4_t{};
+                *reinterpret_cast<half4_t*>(mid + (4 * m + g) * kF2MidPlane +
+                                            (f2_slot(8 * J + prow[n]) * kF2MidW + pcol[n]) * 16 + 8 * q) = v;
+                continue;
+              }
               half8_t v = x8_act<ACT>(acc[n]);
               if ((masked || uu[n] == 16) && !inside) v = half8_t{};   // the next layer's zero padding
               *reinterpret_cast<half8_t*>(mid + (4 * m + g) * kF2MidPlane +
@@ -613,27 +630,37 @@ __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __re
         using I1 = std::integral_constant<int, 1>;
         using I2 = std::integral_constant<int, 2>;
         using I3 = std::integral_constant<int, 3>;
-        if (X8_G3 & 1) {                                 // groups of 3 N-subtiles: fewer group transitions
+        if (X8_HSPLIT) {                                 // 8 N-subtiles + one A-subtile of the halo each
           if (half == 0) {
-            group(I3{}, 0, 1, 2, true);
-            group(I3{}, 3, 4, 5, false);
-            group(I3{}, 6, 7, 16, false);
+            group(I3{}, I3{}, 0, 1, 2, true);
+            group(I3{}, I3{}, 3, 4, 5, false);
+            group(I3{}, I1{}, 6, 7, 16, false);
           } else {
-            group(I3{}, 8, 9, 10, true);
-            group(I3{}, 11, 12, 13, false);
-            group(I2{}, 14, 15, 15, false);
+            group(I3{}, I3{}, 8, 9, 10, true);
+            group(I3{}, I3{}, 11, 12, 13, false);
+            group(I3{}, I2{}, 14, 15, 16, false);
+          }
+        } else if (X8_G3 & 1) {                          // groups of 3 N-subtiles: fewer group transitions
+          if (half == 0) {
+            group(I3{}, I3{}, 0, 1, 2, true);
+            group(I3{}, I3{}, 3, 4, 5, false);
+            group(I3{}, I3{}, 6, 7, 16, false);
+          } else {
+            group(I3{}, I3{}, 8, 9, 10, true);
+            group(I3{}, I3{}, 11, 12, 13, false);
+            group(I2{}, I3{}, 14, 15, 15, false);
           }
         } else if (half == 0) {                          // rows 0-3 + the halo: 9 N-subtiles
-          group(I2{}, 0, 1, 1, true);
-          group(I2{}, 2, 3, 3, false);
-          group(I2{}, 4, 5, 5, false);
-          group(I2{}, 6, 7, 7, false);
-          group(I1{}, 16, 16, 16, false);
+          group(I2{}, I3{}, 0, 1, 1, true);
+          group(I2{}, I3{}, 2, 3, 3, false);
+          group(I2{}, I3{}, 4, 5, 5, false);
+          group(I2{}, I3{}, 6, 7, 7, false);
+          group(I1{}, I3{}, 16, 16, 16, false);
         } else {                                         // rows 4-7: 8
-          group(I2{}, 8, 9, 9, true);
-          group(I2{}, 10, 11, 11, false);
-          group(I2{}, 12, 13, 13, false);
-          group(I2{}, 14, 15, 15, false);
+          group(I2{}, I3{}, 8, 9, 9, true);
+          group(I2{}, I3{}, 10, 11, 11, false);
+          group(I2{}, I3{}, 12, 13, 13, false);
+          group(I2{}, I3{}, 14, 15, 15, false);
         }
       } else {
 #pragma unroll 1
