@@ -3,12 +3,7 @@
 set -e
 mkdir -p gpurun_out/r03/bench gpurun_out/r03/configs
 export TMPDIR=/tmp
-bash tools/profile_bench.sh gpurun_out/r03/bench
-F=$(find gpurun_out/r03/bench -name "pmc_fetch_counter_collection.csv" | head -1)
-W=$(find gpurun_out/r03/bench -name "pmc_write_counter_collection.csv" | head -1)
-python3 tools/traffic_from_pmc.py $F $W --out gpurun_out/r03/bench/traffic.json > /dev/null
-python3 tools/pmc_summary.py $(find gpurun_out/r03/bench -name "pmc_*_counter_collection.csv") > gpurun_out/r03/bench/pmc_summary.txt
-python3 -c "import json; d=json.load(open('gpurun_out/r03/bench/bench.json')); print('metric', d['value'], d['ms_per_step'], d['roofline']['frac'], d.get('prox_hbm'))"
+[ -n "$SKIP_BENCH" ] || bash tools/gpu_r03_bench.sh
 for c in cfg1 cfg2 cfg3 cfg4; do
   timeout -k 10 300 python3 -u bench.py --config $c > gpurun_out/r03/configs/bench_$c.json 2> gpurun_out/r03/configs/bench_$c.err
   python3 -c "import json; d=json.load(open('gpurun_out/r03/configs/bench_$c.json')); print('$c', d['value'], d['ms_per_step'], d['config']['precision'], d.get('psnr_delta_db_vs_oracle'))"
