@@ -1020,20 +1020,25 @@ __global__ __launch_bounds__(256) void k1_blur_rb(const float* __restrict__ x, c
   RbRows rw;
   rw.init(pb, i0, j, H, W);
   const float* yp = y + pb;
-  rb_fill_cols<G, LAT ? 32 : kRbFill>(lds, i0, j0, H, W, [&](int k) { return yp[k]; });
-  __syncthreads();
-  f2_t g[kRbRows];
-  rb_stencil<T>(lds, wd_adj, g);
-  const float* yc = lds + (ty * kRbRows + G::R) * G::LW + 2 * tx + G::R - G::kOff;   // y at (row 0, col j)
-#pragma unroll
-  for (int rb = 0; rb < kRbRows; rb += kRb1Batch) {   // the loads of kRb1Batch rows in flight together
-    f2_t xv[kRb1Batch], sv[kRb1Batch];
+  f2_t xv[kRb1Batch], sv[kRb1Batch];
+  auto load_epi = [&](int rb) {                       // the loads of kRb1Batch rows in flight together
 #pragma unroll
     for (int k = 0; k < kRb1Batch; ++k) {
       const bool vec = al && rw.nv(rb + k) == 2;
       xv[k] = ld2g(x, rw.ix(rb + k), rw.nv(rb + k), vec);
       if (MB) sv[k] = ld2g(s, rw.ix(rb + k), rw.nv(rb + k), vec);
     }
+  };
+  if (LAT) load_epi(0);                               // LAT: issued before the halo fill
+  rb_fill_cols<G, LAT ? 32 : kRbFill>(lds, i0, j0, H, W, [&](int k) { return yp[k]; });
+  __syncthreads();
+  f2_t g[kRbRows];
+  rb_stencil<T>(lds, wd_adj, g);
+  const float* yc = lds + (ty * kRbRows + G::R) * G::LW + 2 * tx + G::R - G::kOff;   // y at (row 0, col j)
+  static_assert(!LAT || kRb1Batch == kRbRows, "LAT preloads every epilogue row");
+#pragma unroll
+  for (int rb = 0; rb < kRbRows; rb += kRb1Batch) {
+    if (!LAT) load_epi(rb);
 #pragma unroll
     for (int k = 0; k < kRb1Batch; ++k) {
       const int r = rb + k;
@@ -1182,6 +1187,23 @@ __global__ __launch_bounds__(256) void k2_blur_rb(const float* __restrict__ xn, 
   RbRows rw;
   rw.init((size_t)bc * plane, i0, j, H, W);
   __shared__ float redr[4][2];
+  // EB rows at a time: every stream's loads of the batch are issued before the first use.
+  // LAT: all 8 rows, issued before the halo fill (their latency hides behind it)
+  constexpr int EB = LAT ? kRbRows : kRbBatch;
+  f2_t yv[EB], bv[EB], sv[EB], wv[EB];
+  auto load_epi = [&](int rb) {
+#pragma unroll
+    for (int k = 0; k < EB; ++k) {
+      const bool vec = al && rw.nv(rb + k) == 2;
+      yv[k] = ld2g(y, rw.ix(rb + k), rw.nv(rb + k), vec);
+      bv[k] = ld2g(xobs, rw.ix(rb + k), rw.nv(rb + k), vec);
+      if (METHOD == M_B) {
+        sv[k] = ld2g(s, rw.ix(rb + k), rw.nv(rb + k), vec);
+        wv[k] = ld2g(w, rw.ix(rb + k), rw.nv(rb + k), vec);
+      }
+    }
+  };
+  if (LAT) load_epi(0);
   {
     double e2 = 0, n2 = 0, t2 = 0;
     float lo = __builtin_inff(), hi = -__builtin_inff();
@@ -1213,21 +1235,9 @@ __global__ __launch_bounds__(256) void k2_blur_rb(const float* __restrict__ xn, 
   double d2 = 0;
   {
     const float th = METHOD == M_B ? theta[b] : 0.f;
-    // EB rows at a time: every stream's loads of the batch are issued before the first use
-    constexpr int EB = LAT ? kRbRows : kRbBatch;
 #pragma unroll
     for (int rb = 0; rb < kRbRows; rb += EB) {
-      f2_t yv[EB], bv[EB], sv[EB], wv[EB];
-#pragma unroll
-      for (int k = 0; k < EB; ++k) {
-        const bool vec = al && rw.nv(rb + k) == 2;
-        yv[k] = ld2g(y, rw.ix(rb + k), rw.nv(rb + k), vec);
-        bv[k] = ld2g(xobs, rw.ix(rb + k), rw.nv(rb + k), vec);
-        if (METHOD == M_B) {
-          sv[k] = ld2g(s, rw.ix(rb + k), rw.nv(rb + k), vec);
-          wv[k] = ld2g(w, rw.ix(rb + k), rw.nv(rb + k), vec);
-        }
-      }
+      if (!LAT) load_epi(rb);
 #pragma unroll
       for (int k = 0; k < EB; ++k) {
         const int r = rb + k;
