@@ -367,6 +367,23 @@ PNP_V3_INST(6, 0)
 // twice, so the result is bit-identical to two one-layer launches.
 // LDS: input ring 18 x 36 px + intermediate ring 18 x 34 px, 128 B per pixel = 161280 B.
 // ------------------------------------------------------------------------------------
+// Workgroup barrier for an LDS hand-off: this wave's LDS accesses complete (lgkmcnt(0)), then
+// s_barrier.  __syncthreads' release fence also waits vmcnt(0), i.e. for every outstanding
+// global store and load of the wave (measured in the ISA: the step barrier of conv_body_x8
+// drained the layer-l+1 waves' HBM stores every step); callers wait for their LDS-DMA with a
+// counted vmcnt themselves.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+#ifndef X8_SBAR
+#define X8_SBAR 1     // conv_body_x8's step barrier without the store drain (A/B builds: 0)
+#endif
+#ifndef HEAD_SBAR
+#define HEAD_SBAR 1   // conv_head's tile barriers without the store drain (A/B builds: 0)
+#endif
+
 constexpr int kF2Ring = 18;                                    // rows per ring
 struct SGeom { int b, x0; };
 constexpr int kF2InW = kTileW + 4, kF2MidW = kTileW + 2;       // 36, 34 pixels per ring row
@@ -734,7 +751,8 @@ __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __re
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
     }
-    __syncthreads();
+    if (X8_SBAR) lds_barrier();     // the layer-l+1 stores stay in flight (vmcnt above, per role)
+    else __syncthreads();
     if (++jb == sb) {
       jb = 0;
       ++kJ;
@@ -1335,14 +1353,18 @@ __global__ __launch_bounds__(256) void conv_head_kernel(const float* __restrict_
   for (int t = blockIdx.x; t < s.tiles; t += gridDim.x) {
     int b, ty0, tx0;
     decode_tile(t, s, b, ty0, tx0);
-    __syncthreads();
+    // (lds_barrier: the previous tile's stores stay in flight; the halo registers' loads are
+    // waited for where they are used)
+    if (HEAD_SBAR) lds_barrier();
+    else __syncthreads();
 #pragma unroll
     for (int k = 0; k < 2; ++k)
       if (tid + 256 * k < kHaloPix) {
         hl[tid + 256 * k] = quad(k, false);
         if (X3) hlo[tid + 256 * k] = quad(k, true);
       }
-    __syncthreads();
+    if (HEAD_SBAR) lds_barrier();
+    else __syncthreads();
     load_halo(t + gridDim.x);
     floatx16 acc00 = {}, acc01 = {}, acc10 = {}, acc11 = {};
 #pragma unroll
