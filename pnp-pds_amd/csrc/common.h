@@ -87,6 +87,17 @@ __device__ __forceinline__ void tile_wait(const int* flags, int idx, bool want, 
   if ((threadIdx.x & 63) == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Workgroup barrier for an LDS hand-off: this wave's LDS accesses complete (lgkmcnt(0)), then
+// s_barrier.  __syncthreads' release fence also waits vmcnt(0), i.e. for every outstanding
+// global store and load of the wave (measured in the ISA: the step barrier of conv_body_x8
+// drained the layer-l+1 waves' HBM stores every step); callers wait for their LDS-DMA with a
+// counted vmcnt themselves.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 // ---- block reductions ------------------------------------------------------------------
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {

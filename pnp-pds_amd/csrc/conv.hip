@@ -367,16 +367,6 @@ PNP_V3_INST(6, 0)
 // twice, so the result is bit-identical to two one-layer launches.
 // LDS: input ring 18 x 36 px + intermediate ring 18 x 34 px, 128 B per pixel = 161280 B.
 // ------------------------------------------------------------------------------------
-// Workgroup barrier for an LDS hand-off: this wave's LDS accesses complete (lgkmcnt(0)), then
-// s_barrier.  __syncthreads' release fence also waits vmcnt(0), i.e. for every outstanding
-// global store and load of the wave (measured in the ISA: the step barrier of conv_body_x8
-// drained the layer-l+1 waves' HBM stores every step); callers wait for their LDS-DMA with a
-// counted vmcnt themselves.
-__device__ __forceinline__ void lds_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
 #ifndef X8_SBAR
 #define X8_SBAR 1     // conv_body_x8's step barrier without the store drain (A/B builds: 0)
 #endif
