@@ -158,17 +158,27 @@ def measured_traffic(kernel, cfg_name, B):
     return None, None
 
 
-def prox_bytes(method, B, C, H, W):
-    """Algorithmic HBM bytes per launch of the fused passes (fp32 state)."""
+def prox_bytes(method, B, C, H, W, op="blur"):
+    """Algorithmic HBM bytes per launch of the fused passes (fp32 state).  On the
+    blur operator ours-A / ours-B run K3 inside the next K1's halo fill (k1_blur_rb PEND), so
+    K1 reads v and x_obs instead of y, writes y, and K3 is a per-image norm kernel (k3_norm)."""
     n = B * C * H * W
+    fused = op == "blur"
     if method == "A-Proposed":
+        if fused:
+            return {"k1_primal_pre": 4 * n * 5,            # read x, v, xobs; write u32, y
+                    "k2_dual": 4 * n * 6}                  # read x+, x, y, xobs, xtrue; write v
         return {"k1_primal_pre": 4 * n * 3,                # read x, y; write u32 (the denoiser head reads it)
                 "k2_dual": 4 * n * 6,                      # read x+, x, y, xobs, xtrue; write v
                 "k3_dual": 4 * n * 3}                      # read v, xobs; write y
     if method == "B-Proposed":
+        if fused:
+            return {"k1_primal_pre": 4 * n * 7,            # read x, v, xobs, s; write u32, w, y
+                    "l1_select": 4 * n * 3,                # 3 radix-level histogram passes over w
+                    "k2_dual": 4 * n * 9}                  # read x+, x, y, xobs, xtrue, s, w; write v, s+
         return {"k1_primal_pre": 4 * n * 5,                # read x, y, s; write u32, w
-                "l1_select": 4 * n * 3,                    # 3 radix-level histogram passes over w
-                "k2_dual": 4 * n * 9,                      # read x+, x, y, xobs, xtrue, s, w; write v, s+
+                "l1_select": 4 * n * 3,
+                "k2_dual": 4 * n * 9,
                 "k3_dual": 4 * n * 3}
     if method == "C-Proposed":
         return {"k1_primal_pre": 4 * n * 3,
@@ -433,7 +443,7 @@ def main():
                                         "bytes_per_launch": by, "flops_per_launch": fl,
                                         "mfma_tflops": round(tfl, 1), "mfma_frac": round(tfl / FP16_PEAK_TFLOPS, 4),
                                         "traffic_source": src}
-            pb = prox_bytes(cfg["method"], B, C, H, W)
+            pb = prox_bytes(cfg["method"], B, C, H, W, cfg["op"])
             copy_gbs = stream_copy_gbs(torch, ctx, f"cuda:{local}")
             line["hbm_copy_gbs"] = round(copy_gbs, 1)
             line["prox_hbm"] = {k: {"GB/s": round(pb[k] / (prof[k][0] * 1e-3) / 1e9, 1),

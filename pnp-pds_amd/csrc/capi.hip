@@ -72,6 +72,11 @@ struct pnp_ctx {
   pnp_params prm{};
   int cur = 0;
   DevBuf x[2], y, s, w, xobs, xtrue, u32, act[2], partials, metrics, theta;
+  // A / B on the blur operator (k1_fused_ok): K3 runs inside the next K1 (launch_k1_fused). The
+  // dual then alternates between y (cur 0) and y2 (cur 1) like x; ypend: it holds v, K2's dual
+  // before the l2-ball step, and omf[b] = 1 - f (finalize_dual applies it in place).
+  DevBuf y2, omf;
+  bool ypend = false;
   DevBuf act_lo[2]; // low halves of the hidden activations (PNP_PREC_FP16X3)
   DevBuf z, p, t;   // comparisonB-2 and the other comparison methods
   DevBuf y1, d, c1; // TV dual [B][2C][H][W]; Poisson-ADMM d and Phi^T 1
@@ -528,6 +533,25 @@ void record_ssim(pnp_ctx* ctx, const float* xn, hipStream_t st, int mm_chunks = 
   check_launch(ctx, "ssim");
 }
 
+// K3 fused into the next K1 (ours-A / ours-B on the register-blocked blur path)
+bool dual_fused(pnp_ctx* ctx, const OpDesc& od) {
+  return (ctx->method == PNP_METHOD_A || ctx->method == PNP_METHOD_B) && k1_fused_ok(od, ctx->C, ctx->H, ctx->W);
+}
+float* dual_buf(pnp_ctx* ctx, int i) { return P<float>(i ? ctx->y2 : ctx->y); }
+
+// The dual state as the reference holds it: applies a pending l2-ball step (K3) in place.
+void finalize_dual(pnp_ctx* ctx) {
+  if (!ctx->ypend) return;
+  const OpDesc od = op_desc(ctx);
+  const size_t n = (size_t)ctx->C * ctx->H * ctx->W;
+  launch_k3(ctx->method, dual_buf(ctx, ctx->cur), P<float>(ctx->xobs), P<double>(ctx->partials), od, ctx->B, ctx->C,
+            ctx->H, ctx->W, ctx->prm.gamma2, l2_eps(ctx, n), P<double>(ctx->metrics), 0, ctx->cap, 0, ctx->has_true,
+            ctx->stream);
+  check_launch(ctx, "k3 (finalize)");
+  ctx->ypend = false;
+  ctx->gen++;   // a captured graph holds the pending-dual K1: the next run recaptures
+}
+
 void solver_iteration(pnp_ctx* ctx) {
   hipStream_t st = ctx->stream;
   const pnp_params& p = ctx->prm;
@@ -538,10 +562,17 @@ void solver_iteration(pnp_ctx* ctx) {
   float* xn = P<float>(ctx->x[ctx->cur ^ 1]);
   const bool mb = ctx->method == PNP_METHOD_B;
   const int record = p.record_metrics && (ctx->capturing || ctx->it < ctx->cap);
+  const bool fused = dual_fused(ctx, od);
+  float* y = fused ? dual_buf(ctx, ctx->cur ^ 1) : P<float>(ctx->y);   // the dual K2 reads and updates
   {
     ProfScope ps(ctx, "k1_primal_pre", st);
-    launch_k1(od.kind, xo, P<float>(ctx->y), P<float>(ctx->s), P<float>(ctx->u32),
-              P<float>(ctx->w), od, B, C, H, W, (float)p.gamma1, ctx->den_clamp, mb, st);
+    if (fused)
+      launch_k1_fused(xo, dual_buf(ctx, ctx->cur), P<float>(ctx->xobs), P<double>(ctx->omf), p.gamma2, ctx->ypend, y,
+                      P<float>(ctx->s), P<float>(ctx->u32), P<float>(ctx->w), od, B, C, H, W, (float)p.gamma1,
+                      ctx->den_clamp, mb, st);
+    else
+      launch_k1(od.kind, xo, P<float>(ctx->y), P<float>(ctx->s), P<float>(ctx->u32),
+                P<float>(ctx->w), od, B, C, H, W, (float)p.gamma1, ctx->den_clamp, mb, st);
     check_launch(ctx, "k1");
   }
   if (mb) {
@@ -555,13 +586,19 @@ void solver_iteration(pnp_ctx* ctx) {
   {
     ProfScope ps(ctx, "k2_dual", st);
     const double gkl_gamma = p.my_lambda / p.gamma2;   // iteration.py:63
-    mm_chunks = launch_k2(od.kind, ctx->method, xn, xo, P<float>(ctx->y), P<float>(ctx->xobs),
+    mm_chunks = launch_k2(od.kind, ctx->method, xn, xo, y, P<float>(ctx->xobs),
                           ctx->has_true ? P<float>(ctx->xtrue) : nullptr, P<float>(ctx->s), P<float>(ctx->w),
                           P<float>(ctx->theta), P<double>(ctx->partials), od, B, C, H, W, p.gamma2, gkl_gamma,
                           p.poisson_alpha, record, want_ssim(ctx) ? P<float>(ctx->ssim_mm) : nullptr, st);
     check_launch(ctx, "k2");
   }
-  {
+  if (fused) {
+    ProfScope ps(ctx, "k3_norm", st);
+    launch_k3_norm(P<double>(ctx->partials), od, B, C, H, W, l2_eps(ctx, n), P<double>(ctx->omf),
+                   P<double>(ctx->metrics), ctx->it, ctx->cap, record, ctx->has_true, st, ctx->itp);
+    check_launch(ctx, "k3_norm");
+    ctx->ypend = true;
+  } else {
     ProfScope ps(ctx, "k3_dual", st);
     launch_k3(ctx->method, P<float>(ctx->y), P<float>(ctx->xobs), P<double>(ctx->partials), od, B, C, H, W, p.gamma2,
               l2_eps(ctx, n), P<double>(ctx->metrics), ctx->it, ctx->cap, record, ctx->has_true, st, ctx->itp);
@@ -916,6 +953,11 @@ void solver_setup(pnp_ctx* ctx, int method, const pnp_params* params, int B, int
   const size_t N = (size_t)B * C * H * W, fb = N * sizeof(float);
   for (int i = 0; i < 2; ++i) ensure(ctx, ctx->x[i], fb);
   ensure(ctx, ctx->y, fb);
+  if (method == PNP_METHOD_A || method == PNP_METHOD_B) {
+    ensure(ctx, ctx->y2, fb);
+    ensure(ctx, ctx->omf, (size_t)B * sizeof(double));
+  }
+  ctx->ypend = false;
   ensure(ctx, ctx->s, fb);
   ensure(ctx, ctx->xobs, fb);
   ensure(ctx, ctx->xtrue, fb);
@@ -950,6 +992,7 @@ void solver_reset_state(pnp_ctx* ctx) {
     fail(ctx, PNP_E_ARG, "blur kernel radius %d larger than the image", ctx->op_R);
   const size_t fb = (size_t)ctx->B * ctx->C * ctx->H * ctx->W * sizeof(float);
   HIPCHK(ctx, hipMemsetAsync(ctx->y.p, 0, fb, ctx->stream));          // iteration.py:24
+  ctx->ypend = false;
   HIPCHK(ctx, hipMemsetAsync(ctx->s.p, 0, fb, ctx->stream));          // iteration.py:27
   if (ctx->method >= PNP_METHOD_ADMM_B2) HIPCHK(ctx, hipMemsetAsync(ctx->z.p, 0, fb, ctx->stream));
   if (is_tv(ctx->method)) HIPCHK(ctx, hipMemsetAsync(ctx->y1.p, 0, 2 * fb, ctx->stream));   // iteration.py:25
@@ -1385,7 +1428,10 @@ int pnp_solver_state(pnp_ctx* ctx, const float** d_x, const float** d_y, const f
   return guarded(ctx, [&] {
     if (!ctx->loaded) fail(ctx, PNP_E_STATE, "solver not loaded");
     if (d_x) *d_x = P<const float>(ctx->x[ctx->cur]);
-    if (d_y) *d_y = P<const float>(ctx->y);
+    if (d_y) {
+      finalize_dual(ctx);
+      *d_y = dual_buf(ctx, dual_fused(ctx, op_desc(ctx)) ? ctx->cur : 0);
+    }
     if (d_s) *d_s = P<const float>(ctx->s);
   });
 }

@@ -103,6 +103,16 @@ void pack_tap_pairs(int Rd, const float* W, float* out);
 void launch_k1(int kind, const float* x, const float* y, const float* s, float* u32, float* w,
                const OpDesc& op, int B, int C, int H, int W, float gamma1, int clamp_in, int method_b,
                hipStream_t st);
+// K1 with K3 fused into its halo fill (blur operator, register-blocked path: k1_fused_ok).
+// pend: y holds v (K2's dual before the l2-ball step, omf[b] = 1 - f from launch_k3_norm) and
+// the fill applies y = (1 - f)(v - g2 xobs); else y holds the dual.  yout (!= y) receives y.
+bool k1_fused_ok(const OpDesc& op, int C, int H, int W);
+void launch_k1_fused(const float* x, const float* y, const float* xobs, const double* omf, double gamma2, bool pend,
+                     float* yout, const float* s, float* u32, float* w, const OpDesc& op, int B, int C, int H, int W,
+                     float gamma1, int clamp_in, int method_b, hipStream_t st);
+// K3's per-image part alone: omf[b] = 1 - f from K2's partials, and the metrics when record
+void launch_k3_norm(const double* partials, const OpDesc& op, int B, int C, int H, int W, double eps, double* omf,
+                    double* metrics, int it, int cap, int record, int has_true, hipStream_t st, const int* itp);
 // Returns the number of per-image (min, max) partials of xn it wrote to mm ([B][chunks][2]
 // floats, SSIM's data_range; mm may be null), 0 when this path does not produce them.
 int launch_k2(int kind, int method, const float* xn, const float* xo, float* y, const float* xobs,

@@ -460,8 +460,21 @@ __device__ __forceinline__ void write_metrics(double* metrics, int b, int it, in
 
 // =====================================================================================
 // K3 (A/B): y <- v - g2 * P_{B(xobs, eps)}(v / g2) = (1 - f)(v - g2 xobs), f = min(1, eps/|v/g2 - xobs|)
-// grid (chunks, B); each block re-reduces its image's partials (fixed order).
+// grid (chunks, B); each block re-reduces its image's partials (fixed order).  With the blur
+// operator the same update runs inside the next K1's halo fill instead (k1_blur_rb PEND) and
+// k3_norm only computes 1 - f per image; k3_l2_dual then finalizes y in place when the host
+// asks for the dual state.
 // =====================================================================================
+__device__ __forceinline__ double l2_dual_omf(const double (&a)[4], double eps) {
+  const double nrm = sqrt(a[0]);
+  const double f = nrm > eps ? eps / nrm : 1.0;
+  return 1.0 - f;
+}
+// the one expression both K3 and K1's fused fill use (same bits)
+__device__ __forceinline__ float l2_dual_y(float v, float ob, double omf, double gamma2) {
+  return (float)(omf * ((double)v - gamma2 * (double)ob));
+}
+
 __global__ __launch_bounds__(256) void k3_l2_dual(float* __restrict__ y, const float* __restrict__ xobs,
                                                    const double* __restrict__ partials, int tiles, size_t n,
                                                    double gamma2, double eps, double* __restrict__ metrics,
@@ -472,16 +485,31 @@ __global__ __launch_bounds__(256) void k3_l2_dual(float* __restrict__ y, const f
   if (itp) it = *itp;                        // graph replay: the iteration number from the device counter
   double a[4];
   reduce_partials(partials, b, tiles, a, red);
-  const double nrm = sqrt(a[0]);
-  const double f = nrm > eps ? eps / nrm : 1.0;
-  const double omf = 1.0 - f;
+  const double omf = l2_dual_omf(a, eps);
   if (record && blockIdx.x == 0 && threadIdx.x == 0) write_metrics(metrics, b, it, cap, a, (double)n, has_true);
   float* yb = y + (size_t)b * n;
   const float* ob = xobs + (size_t)b * n;
   const size_t chunk = 2048;
   const size_t beg = (size_t)blockIdx.x * chunk;
   for (size_t k = beg + threadIdx.x; k < beg + chunk && k < n; k += 256)
-    yb[k] = (float)(omf * ((double)yb[k] - gamma2 * (double)ob[k]));   // (non-temporal: 0.119 vs 0.099 ms)
+    yb[k] = l2_dual_y(yb[k], ob[k], omf, gamma2);   // (non-temporal: 0.119 vs 0.099 ms)
+}
+
+// K3 without the pass (blur operator): per image 1 - f for the next K1's fused fill, and the
+// iteration's metrics.  grid (B).
+__global__ __launch_bounds__(256) void k3_norm(const double* __restrict__ partials, int tiles, size_t n,
+                                                double eps, double* __restrict__ omf, double* __restrict__ metrics,
+                                                int it, int cap, int record, int has_true,
+                                                const int* __restrict__ itp) {
+  __shared__ double red[4];
+  const int b = blockIdx.x;
+  if (itp) it = *itp;
+  double a[4];
+  reduce_partials(partials, b, tiles, a, red);
+  if (threadIdx.x == 0) {
+    omf[b] = l2_dual_omf(a, eps);
+    if (record) write_metrics(metrics, b, it, cap, a, (double)n, has_true);
+  }
 }
 
 __global__ __launch_bounds__(256) void k3_metrics(const double* __restrict__ partials, int tiles, size_t n,
@@ -877,39 +905,12 @@ __device__ __forceinline__ void rb_stencil(const float* lds, const f2_t* __restr
     rb_pair_dispatch<T>(p, base, wp, acc, std::make_integer_sequence<int, T::kR + 1>{});
 }
 
-// Periodic ('wrap') halo gather of one plane's LH x LW tile: element q = tid + 256k of the
-// LDS image comes from global (i0 - R + q / LW, j0 - R + kOff + q % LW) wrapped once (R <= H,
-// W), then clamped (rows/columns past one wrap are only read by zero taps).  The (row,
-// column) of each k is stepped from the thread's first one by compile-time increments.
-// load(k, idx) issues the loads of element k (plane-relative index idx); all NF loads of
-// a thread are independent, so they are in flight together.
-template <class G, int K0 = 0, int K1 = G::NF, class F>
-__device__ __forceinline__ void rb_gather(int i0, int j0, int H, int W, F&& load) {
-  const int tid = threadIdx.x;
-  const int ly0 = tid / G::LW, lx0 = tid - ly0 * G::LW;
-  const int ci = i0 - G::R, cj = j0 - G::R + G::kOff;
-#pragma unroll
-  for (int k = K0; k < K1; ++k) {
-    const int dy = (256 * k) / G::LW, dx = (256 * k) % G::LW;
-    int lx = lx0 + dx, ly = ly0 + dy;
-    const bool carry = lx >= G::LW;
-    lx = carry ? lx - G::LW : lx;
-    ly = carry ? ly + 1 : ly;
-    ly = min(ly, G::LH - 1);                       // q >= N: any in-range element, never stored
-    int gi = ci + ly, gj = cj + lx;
-    gi += gi < 0 ? H : 0;
-    gi -= gi >= H ? H : 0;
-    gj += gj < 0 ? W : 0;
-    gj -= gj >= W ? W : 0;
-    gi = min(max(gi, 0), H - 1);
-    gj = min(max(gj, 0), W - 1);
-    load(k - K0, gi * W + gj);
-  }
-}
-
 // Halo fills: batches of kRbFill elements per thread (the loads of a batch in flight
 // together, then their LDS stores), so few registers are live and 6 blocks fit per CU.
-constexpr int kRbFill = 8;
+#ifndef PNP_RB_FILL
+#define PNP_RB_FILL 8        // A/B builds only
+#endif
+constexpr int kRbFill = PNP_RB_FILL;
 
 // Column-wise halo fill (K1): thread t < TPC LW owns LDS column t % LW and rows t / LW +
 // TPC i, so the column's wrap is resolved once and each row step is an add and one
@@ -998,16 +999,96 @@ struct RbRows {
   __device__ __forceinline__ size_t ix(int r) const { return base + (size_t)(r < rows_left ? r : 0) * W; }
 };
 
+// One plane as a buffer resource: loads take a 32-bit byte offset (no 64-bit address add per
+// load) and return 0 past num_records (a null plane: every load 0).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_rsrc(const float* p, int H, int W) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, p ? H * W * 4 : 0, 0x00020000);
+}
+__device__ __forceinline__ float bld(__amdgpu_buffer_rsrc_t r, int idx) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, idx * 4, 0, 0));
+}
+
+// K1's halo fill, laid out as K2's rb_fill_k2_fast (the wrapped halo rows, then the tile's own
+// rows by index adds; a ragged bottom row of tiles takes rb_fill_cols).  PEND: the plane holds
+// v, K2's dual before the l2-ball step, and the fill applies K3's update per element, y =
+// (1 - f)(v - g2 xobs) (l2_dual_y, the bits of k3_l2_dual), so K3's pass over y disappears.
+template <class G, int NB, bool PEND>
+__device__ __forceinline__ void rb_fill_k1(float* lds, int i0, int j0, int H, int W, const float* yp, const float* op,
+                                           double omf, double g2) {
+  if (i0 + kRbH > H) {
+    rb_fill_cols<G, NB>(lds, i0, j0, H, W,
+                        [&](int k) { return PEND ? l2_dual_y(yp[k], op[k], omf, g2) : yp[k]; });
+    return;
+  }
+  constexpr int R = G::R, TPC = 256 / G::LW;
+  constexpr int NH = (2 * R + TPC - 1) / TPC;        // halo rows per thread (the last may be past 2R)
+  constexpr int NT = (kRbH + TPC - 1) / TPC;         // tile rows per thread (the last may be past 64)
+  const int tid = threadIdx.x;
+  if (tid >= TPC * G::LW) return;
+  const int lx = tid % G::LW, ly0 = tid / G::LW;
+  int gj = j0 - R + G::kOff + lx;
+  gj += gj < 0 ? W : 0;
+  gj -= gj >= W ? W : 0;
+  gj = min(max(gj, 0), W - 1);
+  const __amdgpu_buffer_rsrc_t ry = plane_rsrc(yp, H, W), ro = plane_rsrc(PEND ? op : nullptr, H, W);
+  auto val = [&](float v, float o) { return PEND ? l2_dual_y(v, o, omf, g2) : v; };
+  {
+    float a[NH], bb[NH];
+#pragma unroll
+    for (int k = 0; k < NH; ++k) {
+      const int q = ly0 + TPC * k;                     // halo row q: LDS row q (above) or q + 64 (below)
+      const int ly = q < R ? q : q + kRbH;
+      int gi = i0 - R + ly;
+      gi += gi < 0 ? H : 0;
+      gi -= gi >= H ? H : 0;
+      gi = min(max(gi, 0), H - 1);
+      const int idx = gi * W + gj;
+      a[k] = bld(ry, idx);
+      bb[k] = PEND ? bld(ro, idx) : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < NH; ++k) {
+      const int q = ly0 + TPC * k;
+      const int ly = q < R ? q : q + kRbH;
+      if ((2 * R) % TPC == 0 || q < 2 * R) lds[ly * G::LW + lx] = val(a[k], bb[k]);
+    }
+  }
+  int idx = (i0 + ly0) * W + gj;
+#pragma unroll
+  for (int k0 = 0; k0 < NT; k0 += NB) {
+    float a[NB], bb[NB];
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+      if (k0 + k < NT) {
+        const int ii = (ly0 + TPC * (k0 + k) < kRbH) ? idx : idx - TPC * W;   // past row 63: any loaded row, not stored
+        a[k] = bld(ry, ii);
+        bb[k] = PEND ? bld(ro, ii) : 0.f;
+        idx += TPC * W;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+      const int r = ly0 + TPC * (k0 + k);
+      if (k0 + k < NT && (kRbH % TPC == 0 || r < kRbH)) lds[(R + r) * G::LW + lx] = val(a[k], bb[k]);
+    }
+  }
+}
+
 // K1: u = [clamp](x - g1 Phi^T y) -> u32 (the denoiser's input; its head converts to fp16);
 // B (MB): w = s - g1 y.  Block = one (plane, 64 x 64 tile).  B's y comes
 // from the halo in LDS (it is the stencil's input), so K1 reads y once.
 // LAT (small grids, fewer blocks than CUs: B = 1): every halo load of a thread in flight at
 // once instead of in batches of 8 (the batches keep registers low for 6 blocks per CU).
-template <class T, bool MB, int LAT = 0>
+// PEND: y holds v and the fill applies K3's update (omf[b] = 1 - f from k3_norm); yout
+// (nullable) receives the tile's y, the next K2's input (a separate buffer: other blocks
+// still read v's halo).
+template <class T, bool MB, int LAT = 0, bool PEND = false>
 __global__ __launch_bounds__(256) void k1_blur_rb(const float* __restrict__ x, const float* __restrict__ y,
+                                                   const float* __restrict__ xobs, const double* __restrict__ omf,
+                                                   double gamma2, float* __restrict__ yout,
                                                    const float* __restrict__ s, float* __restrict__ u32,
-                                                   float* __restrict__ w, const f2_t* __restrict__ wd_adj, int H, int W,
-                                                   int tiles_x, int tiles, float gamma1, int clamp_in) {
+                                                   float* __restrict__ w, const f2_t* __restrict__ wd_adj, int C, int H,
+                                                   int W, int tiles_x, int tiles, float gamma1, int clamp_in) {
   using G = TapGeom<T>;
   __shared__ float lds[G::N];
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
@@ -1030,7 +1111,8 @@ __global__ __launch_bounds__(256) void k1_blur_rb(const float* __restrict__ x, c
     }
   };
   if (LAT) load_epi(0);                               // LAT: issued before the halo fill
-  rb_fill_cols<G, LAT ? 32 : kRbFill>(lds, i0, j0, H, W, [&](int k) { return yp[k]; });
+  rb_fill_k1<G, LAT ? 32 : kRbFill, PEND>(lds, i0, j0, H, W, yp, PEND ? xobs + pb : nullptr,
+                                          PEND ? omf[bc / C] : 0.0, gamma2);
   __syncthreads();
   f2_t g[kRbRows];
   rb_stencil<T>(lds, wd_adj, g);
@@ -1053,6 +1135,7 @@ __global__ __launch_bounds__(256) void k1_blur_rb(const float* __restrict__ x, c
       const bool vec = al && rw.nv(r) == 2;
       st2g(u32, rw.ix(r), uo, rw.nv(r), vec);
       if (MB) st2g(w, rw.ix(r), wo, rw.nv(r), vec);
+      if (yout) st2g(yout, rw.ix(r), f2_t{yc[r * G::LW], yc[r * G::LW + 1]}, rw.nv(r), vec);
     }
   }
 }
@@ -1093,67 +1176,167 @@ __global__ __launch_bounds__(256) void k0_blur_rb(const float* __restrict__ x, f
 // K2 halo fill of 2 xn - xo (Phi's argument) that also accumulates the metric sums of the
 // tile's own pixels from the same loads: e2 = sum (xn - xo)^2, n2 = sum xo^2 (c_n,
 // iteration.py:187) and t2 = sum (xt - xn)^2 (PSNR, :188; x_true loaded for those pixels
-// only).  Each batch's <= kRbFill terms are summed in fp32, then added once into fp64.
-template <class G, int FB = kRbFill, int K0 = 0>
-__device__ __forceinline__ void rb_fill_k2(float* lds, int i0, int j0, int H, int W, const float* xnp,
-                                           const float* xop, const float* xtp, bool record, double& e2, double& n2,
-                                           double& t2, float& lo, float& hi) {
-  constexpr int K1 = K0 + FB < G::NF ? K0 + FB : G::NF;
+// only).  Column-wise (as rb_fill_cols): thread t < TPC LW owns LDS column t % LW and
+// rows t / LW + TPC i, so the column's wrap and its "inside the tile" test are resolved once
+// and a row step is an add, one conditional wrap and one row compare (the element-wise form
+// of round 2 re-derived and wrapped row and column and tested both per element: 1 240 of the kernel's
+// 2 555 VALU instructions per wave, against ~330 for K1's one-plane column fill).  The sums'
+// fp32 groups are flushed into fp64 every kRbFill rows of a thread, whatever the load batch
+// NB (the latency variant loads all rows at once), so both variants give the same bits.
+template <class G, int NB = kRbFill>
+__device__ __forceinline__ void rb_fill_k2_cols(float* lds, int i0, int j0, int H, int W, const float* xnp,
+                                                const float* xop, const float* xtp, bool record, double& e2,
+                                                double& n2, double& t2, float& lo, float& hi) {
+  constexpr int TPC = 256 / G::LW;                   // threads per column (row stride)
+  constexpr int NI = (G::LH + TPC - 1) / TPC;        // rows per thread (the last may be past LH)
   const int tid = threadIdx.x;
-  const int ly0 = tid / G::LW, lx0 = tid - ly0 * G::LW;
-  const int ci = i0 - G::R, cj = j0 - G::R + G::kOff;
-  const int ie = min(i0 + kRbH, H), je = min(j0 + kRbW, W);
-  float a[FB], bb[FB], t[FB];
-  bool in[FB];
-#pragma unroll
-  for (int k = K0; k < K1; ++k) {
-    const int dy = (256 * k) / G::LW, dx = (256 * k) % G::LW;
-    int lx = lx0 + dx, ly = ly0 + dy;
-    const bool carry = lx >= G::LW;
-    lx = carry ? lx - G::LW : lx;
-    ly = carry ? ly + 1 : ly;
-    const bool valid = G::N % 256 == 0 || tid + 256 * k < G::N;
-    ly = min(ly, G::LH - 1);
-    const int ui = ci + ly, uj = cj + lx;      // unwrapped image coordinates
-    int gi = ui, gj = uj;
-    gi += gi < 0 ? H : 0;
-    gi -= gi >= H ? H : 0;
-    gj += gj < 0 ? W : 0;
-    gj -= gj >= W ? W : 0;
-    gi = min(max(gi, 0), H - 1);
-    gj = min(max(gj, 0), W - 1);
-    const int idx = gi * W + gj;
-    a[k - K0] = xnp[idx];
-    bb[k - K0] = xop[idx];
-    in[k - K0] = record && valid && ui >= i0 && ui < ie && uj >= j0 && uj < je;
-    t[k - K0] = (in[k - K0] && xtp) ? xtp[idx] : 0.f;
-  }
-  // the fp32 partial sums are flushed into fp64 every kRbFill elements (of the absolute index k),
-  // so the sums are the same bits whatever the load batch FB
+  if (tid >= TPC * G::LW) return;
+  const int lx = tid % G::LW, ly0 = tid / G::LW;
+  int gj = j0 - G::R + G::kOff + lx;
+  const bool colin = record && gj >= j0 && gj < min(j0 + kRbW, W);   // a column of the tile's own pixels
+  gj += gj < 0 ? W : 0;
+  gj -= gj >= W ? W : 0;
+  gj = min(max(gj, 0), W - 1);
+  const int rhi = G::R + min(kRbH, H - i0);          // LDS rows R .. rhi-1: the tile's own rows
+  int gi = i0 - G::R + ly0;
+  gi += gi < 0 ? H : 0;
+  gi -= gi >= H ? H : 0;
   float be = 0.f, bn = 0.f, bt = 0.f;
 #pragma unroll
-  for (int k = K0; k < K1; ++k) {
-    if (k > K0 && k % kRbFill == 0) {
-      e2 += be;
-      n2 += bn;
-      t2 += bt;
-      be = bn = bt = 0.f;
+  for (int i0b = 0; i0b < NI; i0b += NB) {
+    float a[NB], bb[NB], t[NB];
+    bool in[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      if (i0b + i < NI) {
+        const int ly = ly0 + TPC * (i0b + i);
+        const int idx = min(max(gi, 0), H - 1) * W + gj;
+        a[i] = xnp[idx];
+        bb[i] = xop[idx];
+        in[i] = colin && ly >= G::R && ly < rhi;
+        t[i] = (in[i] && xtp) ? xtp[idx] : 0.f;
+        gi += TPC;
+        gi -= gi >= H ? H : 0;
+      }
     }
-    const int q = tid + 256 * k;
-    const float av = a[k - K0], bv = bb[k - K0];
-    if (G::N % 256 == 0 || q < G::N) lds[q] = 2.f * av - bv;
-    const float d = in[k - K0] ? av - bv : 0.f, o = in[k - K0] ? bv : 0.f;
-    const float tt = in[k - K0] ? t[k - K0] - av : 0.f;
-    be = fmaf(d, d, be);
-    bn = fmaf(o, o, bn);
-    bt = fmaf(tt, tt, bt);
-    lo = in[k - K0] ? fminf(lo, av) : lo;    // x+ range for SSIM's data_range (utils_eval.py:11)
-    hi = in[k - K0] ? fmaxf(hi, av) : hi;
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      if (i0b + i < NI) {
+        if ((i0b + i) % kRbFill == 0) {                // fp32 groups of kRbFill rows whatever NB: same bits
+          e2 += be;
+          n2 += bn;
+          t2 += bt;
+          be = bn = bt = 0.f;
+        }
+        const int ly = ly0 + TPC * (i0b + i);
+        if (G::LH % TPC == 0 || ly < G::LH) lds[ly * G::LW + lx] = 2.f * a[i] - bb[i];
+        const float d = in[i] ? a[i] - bb[i] : 0.f, o = in[i] ? bb[i] : 0.f;
+        const float tt = in[i] ? t[i] - a[i] : 0.f;
+        be = fmaf(d, d, be);
+        bn = fmaf(o, o, bn);
+        bt = fmaf(tt, tt, bt);
+        lo = in[i] ? fminf(lo, a[i]) : lo;            // x+ range for SSIM's data_range (utils_eval.py:11)
+        hi = in[i] ? fmaxf(hi, a[i]) : hi;
+      }
+    }
   }
   e2 += be;
   n2 += bn;
   t2 += bt;
-  if constexpr (K1 < G::NF) rb_fill_k2<G, FB, K1>(lds, i0, j0, H, W, xnp, xop, xtp, record, e2, n2, t2, lo, hi);
+}
+
+// K2's fill for tiles whose 64 rows lie inside the image (all but a ragged bottom row of
+// tiles, which takes rb_fill_k2_cols): the 2R halo rows above and below first (wrapped), then
+// the tile's own rows, which need no wrap or clamp (a row step is an index add) and no
+// per-element "inside" test: a thread's column is inside the tile or not, so the sums of a
+// batch are kept or dropped once per batch.
+template <class G, int NB = kRbFill>
+__device__ __forceinline__ void rb_fill_k2_fast(float* lds, int i0, int j0, int H, int W, const float* xnp,
+                                                const float* xop, const float* xtp, bool record, double& e2,
+                                                double& n2, double& t2, float& lo, float& hi) {
+  if (i0 + kRbH > H) {
+    rb_fill_k2_cols<G, NB>(lds, i0, j0, H, W, xnp, xop, xtp, record, e2, n2, t2, lo, hi);
+    return;
+  }
+  constexpr int R = G::R, TPC = 256 / G::LW;
+  constexpr int NH = (2 * R + TPC - 1) / TPC;        // halo rows per thread (the last may be past 2R)
+  constexpr int NT = (kRbH + TPC - 1) / TPC;         // tile rows per thread (the last may be past 64)
+  const int tid = threadIdx.x;
+  if (tid >= TPC * G::LW) return;
+  const int lx = tid % G::LW, ly0 = tid / G::LW;
+  int gj = j0 - R + G::kOff + lx;
+  const bool colin = record && gj >= j0 && gj < min(j0 + kRbW, W);
+  gj += gj < 0 ? W : 0;
+  gj -= gj >= W ? W : 0;
+  gj = min(max(gj, 0), W - 1);
+  const __amdgpu_buffer_rsrc_t rn = plane_rsrc(xnp, H, W), ro = plane_rsrc(xop, H, W);
+  const __amdgpu_buffer_rsrc_t rt = plane_rsrc(record ? xtp : nullptr, H, W);   // none: loads of 0
+  {
+    float a[NH], bb[NH];
+#pragma unroll
+    for (int k = 0; k < NH; ++k) {
+      const int q = ly0 + TPC * k;                     // halo row q: LDS row q (above) or q + 64 (below)
+      const int ly = q < R ? q : q + kRbH;
+      int gi = i0 - R + ly;
+      gi += gi < 0 ? H : 0;
+      gi -= gi >= H ? H : 0;
+      gi = min(max(gi, 0), H - 1);
+      const int idx = gi * W + gj;
+      a[k] = bld(rn, idx);
+      bb[k] = bld(ro, idx);
+    }
+#pragma unroll
+    for (int k = 0; k < NH; ++k) {
+      const int q = ly0 + TPC * k;
+      const int ly = q < R ? q : q + kRbH;
+      if ((2 * R) % TPC == 0 || q < 2 * R) lds[ly * G::LW + lx] = 2.f * a[k] - bb[k];
+    }
+  }
+  int idx = (i0 + ly0) * W + gj;
+  float be = 0.f, bn = 0.f, bt = 0.f, bl = lo, bh = hi;
+  auto flush = [&] {
+    if (colin) {
+      e2 += be;
+      n2 += bn;
+      t2 += bt;
+    }
+    be = bn = bt = 0.f;
+  };
+#pragma unroll
+  for (int k0 = 0; k0 < NT; k0 += NB) {
+    float a[NB], bb[NB], t[NB];
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+      if (k0 + k < NT) {
+        const int ii = (ly0 + TPC * (k0 + k) < kRbH) ? idx : idx - TPC * W;   // past row 63: any loaded row, not stored
+        a[k] = bld(rn, ii);
+        bb[k] = bld(ro, ii);
+        t[k] = bld(rt, ii);
+        idx += TPC * W;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+      if (k0 + k < NT) {
+        if ((k0 + k) % kRbFill == 0) flush();        // fp32 groups of kRbFill rows whatever NB: same bits
+        const int r = ly0 + TPC * (k0 + k);
+        const bool ok = kRbH % TPC == 0 || r < kRbH;
+        if (ok) lds[(R + r) * G::LW + lx] = 2.f * a[k] - bb[k];
+        const float d = a[k] - bb[k], tt = t[k] - a[k];
+        const float o = bb[k];
+        be = fmaf(ok ? d : 0.f, d, be);
+        bn = fmaf(ok ? o : 0.f, o, bn);
+        bt = fmaf(ok ? tt : 0.f, tt, bt);
+        bl = ok ? fminf(bl, a[k]) : bl;               // x+ range for SSIM's data_range (utils_eval.py:11)
+        bh = ok ? fmaxf(bh, a[k]) : bh;
+      }
+    }
+  }
+  flush();
+  if (colin) {
+    lo = bl;
+    hi = bh;
+  }
 }
 
 // K2: v = y + g2 (Phi(2x+ - x) [+ 2 s+ - s]), s+ = shrink(w, theta) (B), the GKL prox (C),
@@ -1207,8 +1390,9 @@ __global__ __launch_bounds__(256) void k2_blur_rb(const float* __restrict__ xn, 
   {
     double e2 = 0, n2 = 0, t2 = 0;
     float lo = __builtin_inff(), hi = -__builtin_inff();
-    rb_fill_k2<G, LAT ? G::NF : kRbFill>(lds, i0, j0, H, W, xn + (size_t)bc * plane, xo + (size_t)bc * plane,
-                  xtrue ? xtrue + (size_t)bc * plane : nullptr, record != 0, e2, n2, t2, lo, hi);
+    rb_fill_k2_fast<G, LAT ? 32 : kRbFill>(lds, i0, j0, H, W, xn + (size_t)bc * plane, xo + (size_t)bc * plane,
+                                          xtrue ? xtrue + (size_t)bc * plane : nullptr, record != 0, e2, n2, t2,
+                                          lo, hi);
     if (record) {                            // reduced here, so no fill value stays live past the fill
       e2 = wave_sum(e2);
       n2 = wave_sum(n2);
@@ -1566,7 +1750,7 @@ inline TileGrid tile_grid(int H, int W) {
   return g;
 }
 
-// The register-blocked kernels wrap the halo once (rb_gather): images at least Rd on a side.
+// The register-blocked kernels wrap the halo once (their fills): images at least Rd on a side.
 // Smaller ones (np.pad 'wrap' repeats the image) take the modulo-wrapped stencil4 kernels.
 static bool rb_ok(const OpDesc& op, int C, int H, int W) {
   return op.kind == OP_BLUR && op.dense_fwd && op.dense_adj && op.Rd > 0 && C >= 1 && H >= op.Rd && W >= op.Rd;
@@ -1574,15 +1758,42 @@ static bool rb_ok(const OpDesc& op, int C, int H, int W) {
 
 template <class T>
 static void launch_k1_rb(hipStream_t st, const float* x, const float* y, const float* s, float* u32, float* w,
-                         const OpDesc& op, int B, int C, int H, int W, float gamma1, int clamp_in, int method_b) {
+                         const OpDesc& op, int B, int C, int H, int W, float gamma1, int clamp_in, int method_b,
+                         const float* xobs = nullptr, const double* omf = nullptr, double gamma2 = 0.0,
+                         float* yout = nullptr, bool pend = false) {
   const int tx = (W + kRbW - 1) / kRbW, tiles = tx * ((H + kRbH - 1) / kRbH);
   const bool lat = B * C * tiles < op.num_cus;     // one block per CU at most: latency-bound
-#define K1RBL(MBV, L)                                                                                      \
-  hipLaunchKernelGGL((k1_blur_rb<T, MBV, L>), dim3(B * C * tiles), dim3(256), 0, st, x, y, s, u32, w,       \
-                     reinterpret_cast<const f2_t*>(op.dense_adj), H, W, tx, tiles, gamma1, clamp_in)
-  if (method_b) { if (lat) K1RBL(true, 1); else K1RBL(true, 0); }
-  else { if (lat) K1RBL(false, 1); else K1RBL(false, 0); }
+#define K1RBL(MBV, L, PD)                                                                                   \
+  hipLaunchKernelGGL((k1_blur_rb<T, MBV, L, PD>), dim3(B * C * tiles), dim3(256), 0, st, x, y, xobs, omf,   \
+                     gamma2, yout, s, u32, w, reinterpret_cast<const f2_t*>(op.dense_adj), C, H, W, tx, tiles, \
+                     gamma1, clamp_in)
+#define K1RBP(MBV, PD) if (lat) K1RBL(MBV, 1, PD); else K1RBL(MBV, 0, PD);
+  if (pend) { if (method_b) { K1RBP(true, true) } else { K1RBP(false, true) } }
+  else { if (method_b) { K1RBP(true, false) } else { K1RBP(false, false) } }
+#undef K1RBP
 #undef K1RBL
+}
+
+bool k1_fused_ok(const OpDesc& op, int C, int H, int W) { return op.kind == OP_BLUR && rb_ok(op, C, H, W); }
+
+void launch_k1_fused(const float* x, const float* y, const float* xobs, const double* omf, double gamma2, bool pend,
+                     float* yout, const float* s, float* u32, float* w, const OpDesc& op, int B, int C, int H, int W,
+                     float gamma1, int clamp_in, int method_b, hipStream_t st) {
+#define K1RB(TT) launch_k1_rb<TT>(st, x, y, s, u32, w, op, B, C, H, W, gamma1, clamp_in, method_b, xobs, omf, gamma2, \
+                                  yout, pend)
+  switch (op.taps_id) {
+    case TAPS_BLUR_1: K1RB(Taps_blur_1_Adj); break;
+    case TAPS_SQUARE_MINI: K1RB(Taps_square_mini_Adj); break;
+    default:
+      switch (op.Rd) { case 2: K1RB(DenseTaps<2>); break; case 4: K1RB(DenseTaps<4>); break; default: K1RB(DenseTaps<8>); }
+  }
+#undef K1RB
+}
+
+void launch_k3_norm(const double* partials, const OpDesc& op, int B, int C, int H, int W, double eps, double* omf,
+                    double* metrics, int it, int cap, int record, int has_true, hipStream_t st, const int* itp) {
+  hipLaunchKernelGGL(k3_norm, dim3(B), dim3(256), 0, st, partials, k2_partials(op, C, H, W), (size_t)C * H * W, eps,
+                     omf, metrics, it, cap, record, has_true, itp);
 }
 
 void launch_k1(int kind, const float* x, const float* y, const float* s, float* u32, float* w,

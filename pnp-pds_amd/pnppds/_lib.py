@@ -319,6 +319,13 @@ class Context:
         self._check(self.lib.pnp_solver_fetch(self.h, _fptr(x), _fptr(s), _dptr(c), _dptr(p), _dptr(m)))
         return x, s, c, p, m
 
+    def solver_state(self):
+        """Device pointers (x, y, s) of the solver's current state; y is the dual as the reference
+        holds it (a pending l2-ball step is applied first)."""
+        x, y, sv = _P(), _P(), _P()
+        self._check(self.lib.pnp_solver_state(self.h, C.byref(x), C.byref(y), C.byref(sv)))
+        return x.value, y.value, sv.value
+
     def profile_enable(self, on=True):
         self._check(self.lib.pnp_profile_enable(self.h, 1 if on else 0))
 

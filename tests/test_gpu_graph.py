@@ -143,3 +143,31 @@ def test_single_image_stack_equals_per_layer(case):
         got = ctx.run(m, prm, x0, xo, xt, 7)
         for a, b in zip(ref[:5], got[:5]):
             np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("case", ["A_blur", "B_blur"])
+def test_dual_state_between_iterates(case):
+    """ours-A / ours-B on the blur operator run K3 inside the next K1's halo fill, so between
+    iterations the dual buffer holds v and 1 - f.  Reading the state (pnp_solver_state) applies
+    the pending l2-ball step in place; the run then continues from the finalized dual, with
+    graph replay on and off (the captured pending-dual K1 is recaptured), to the same bits as an
+    uninterrupted run: the finalized y is the y the fused fill computes."""
+    import torch
+    ctx, m, prm, x0, xo, xt = _setup(case, 2)
+    B, Cc, H, W = x0.shape
+    ref = ctx.run(m, prm, x0, xo, xt, 9)
+    for graph in (0, 1):
+        ctx.set_graph(graph)
+        ctx.solver_setup(m, prm, B, Cc, H, W, 9)
+        ctx.solver_load(x0, xo, xt)
+        ctx.solver_iterate(4)
+        _, dy, _ = ctx.solver_state()
+        ctx.synchronize()
+        y4 = torch.empty(B * Cc * H * W, dtype=torch.float32, device="cuda")
+        ctx.device_copy(y4.data_ptr(), dy, y4.numel() * 4)
+        ctx.synchronize()
+        assert torch.isfinite(y4).all()
+        ctx.solver_iterate(5)
+        got = ctx.solver_fetch()
+        for a, b in zip(ref[:5], got[:5]):
+            np.testing.assert_array_equal(a, b)
