@@ -949,6 +949,21 @@ __device__ __forceinline__ void rb_fill_cols(float* lds, int i0, int j0, int H, 
   }
 }
 
+// XCD-aware block -> tile order for the register-blocked passes: blocks b and b + 8 share an
+// XCD (MI355X_MICROARCH.md, workgroup dispatch), so XCD x gets the contiguous tile range
+// [x n/8, (x+1) n/8) in order and a tile's halo rows and columns (41 % of its fill: the
+// neighbouring tiles' pixels) are read while those neighbours are in flight on the same
+// XCD's L2 instead of another XCD's.  (A tail of n % 8 blocks keeps the identity order.)
+#ifndef PNP_RB_XCD
+#define PNP_RB_XCD 1          // A/B builds only
+#endif
+__device__ __forceinline__ int rb_block_tile() {
+  const int b = blockIdx.x, n = gridDim.x;
+  if (!PNP_RB_XCD) return b;
+  const int full = n & ~7;
+  return b < full ? (b & 7) * (full >> 3) + (b >> 3) : b;
+}
+
 __device__ __forceinline__ void rb_tile_origin(int tile, int tiles_x, int& i0, int& j0) {
   const int ty = tile / tiles_x;
   i0 = ty * kRbH;
@@ -1092,9 +1107,10 @@ __global__ __launch_bounds__(256) void k1_blur_rb(const float* __restrict__ x, c
   using G = TapGeom<T>;
   __shared__ float lds[G::N];
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
-  const int bc = blockIdx.x / tiles;                    // plane (image, channel)
+  const int bt = rb_block_tile();
+  const int bc = bt / tiles;                            // plane (image, channel)
   int i0, j0;
-  rb_tile_origin(blockIdx.x - bc * tiles, tiles_x, i0, j0);
+  rb_tile_origin(bt - bc * tiles, tiles_x, i0, j0);
   const int j = j0 + 2 * tx;
   const size_t pb = (size_t)bc * H * W;
   const bool al = (W & 1) == 0;              // column pairs 8-B aligned
@@ -1150,9 +1166,10 @@ __global__ __launch_bounds__(256) void k0_blur_rb(const float* __restrict__ x, f
   using G = TapGeom<T>;
   __shared__ float lds[G::N];
   const int tx = threadIdx.x & 31;
-  const int bc = blockIdx.x / tiles;
+  const int bt = rb_block_tile();
+  const int bc = bt / tiles;
   int i0, j0;
-  rb_tile_origin(blockIdx.x - bc * tiles, tiles_x, i0, j0);
+  rb_tile_origin(bt - bc * tiles, tiles_x, i0, j0);
   const size_t pb = (size_t)bc * H * W;
   const bool al = (W & 1) == 0;
   RbRows rw;
@@ -1361,9 +1378,10 @@ __global__ __launch_bounds__(256) void k2_blur_rb(const float* __restrict__ xn, 
   __shared__ double redm[4][3];
   const int tx = threadIdx.x & 31;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int bc = blockIdx.x / tiles, b = bc / C, c = bc - b * C;
+  const int bt = rb_block_tile();
+  const int bc = bt / tiles, b = bc / C, c = bc - b * C;
   int i0, j0;
-  rb_tile_origin(blockIdx.x - bc * tiles, tiles_x, i0, j0);
+  rb_tile_origin(bt - bc * tiles, tiles_x, i0, j0);
   const size_t plane = (size_t)H * W;
   const int j = j0 + 2 * tx;
   const bool al = (W & 1) == 0;              // column pairs 8-B aligned
@@ -1410,7 +1428,7 @@ __global__ __launch_bounds__(256) void k2_blur_rb(const float* __restrict__ xn, 
   }
   __syncthreads();
   if (record && mm && threadIdx.x == 0) {    // per (image, channel, tile): [B][C * tiles][2]
-    const size_t chunk = (size_t)b * C * tiles + (size_t)c * tiles + (blockIdx.x - bc * tiles);
+    const size_t chunk = (size_t)b * C * tiles + (size_t)c * tiles + (bt - bc * tiles);
     mm[chunk * 2 + 0] = fminf(fminf(redr[0][0], redr[1][0]), fminf(redr[2][0], redr[3][0]));
     mm[chunk * 2 + 1] = fmaxf(fmaxf(redr[0][1], redr[1][1]), fmaxf(redr[2][1], redr[3][1]));
   }
