@@ -416,6 +416,9 @@ __device__ unsigned long long x8_clock[1024][2];   // per workgroup: shader-cloc
 #ifndef X8_HSPLIT
 #define X8_HSPLIT 1   // the strip-halo N-subtile's two A-subtiles on the two halves' waves: 306 MFMAs per SIMD-pair and step each instead of 324 / 288 (A/B builds: 0)
 #endif
+#ifndef X8_PRIO
+#define X8_PRIO 1     // static s_setprio 1 before the step loop: 1 = layer l+1's waves (4-7), 2 = layer l's, 0 none (A/B builds; 1: 2.182 -> 2.164 ms, two rounds, one box)
+#endif
 #ifndef X8_PADBR
 #define X8_PADBR 1    // layer l's zero-padding select skipped on interior steps by a uniform branch (A/B builds: 0)
 #endif
@@ -566,6 +569,7 @@ __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __re
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  if ((X8_PRIO == 1 && layer == 1) || (X8_PRIO == 2 && layer == 0)) __builtin_amdgcn_s_setprio(1);
 
   for (int J = 0; J <= K * sb; ++J) {
     auto side = [&](int ks) {                            // this wave's DMA row of the next step

@@ -808,7 +808,11 @@ __global__ __launch_bounds__(256) void pack_input_kernel(const float* __restrict
 // The LDS halo is only as wide as the taps' non-zero columns need (blur_1: columns -4..+4
 // of 19; rows -8..+8): 72 x 80 floats instead of 80 x 80.
 // =====================================================================================
-constexpr int kRbW = 64, kRbH = 64, kRbRows = 8;   // 8 thread rows x 8 rows; 32 threads x 2 columns
+#ifndef PNP_RB_H
+#define PNP_RB_H 64           // tile height (64 or 32; A/B builds)
+#endif
+constexpr int kRbW = 64, kRbH = PNP_RB_H, kRbRows = kRbH / 8;   // 8 thread rows x kRbRows rows; 32 threads x 2 columns
+static_assert(kRbH == 64 || kRbH == 32, "tiles of whole 32 x 32 metric cells");
 
 typedef float f2_t __attribute__((ext_vector_type(2)));
 
@@ -994,7 +998,7 @@ __device__ __forceinline__ void st2g(float* __restrict__ p, size_t idx, const f2
 #endif
 constexpr int kRbBatch = PNP_RB_BATCH;                   // K2 epilogue rows whose loads are in flight together (2: 0.351 ms K2, 4: 0.366, 1 per pixel before: 0.392)
 #ifndef PNP_RB1_BATCH
-#define PNP_RB1_BATCH 8      // A/B builds only
+#define PNP_RB1_BATCH kRbRows   // A/B builds only
 #endif
 constexpr int kRb1Batch = PNP_RB1_BATCH;                 // K1: all 8 rows' loads in flight (2: 0.173 ms, 4: 0.170, 8: 0.167)
 
@@ -1037,7 +1041,7 @@ __device__ __forceinline__ void rb_fill_k1(float* lds, int i0, int j0, int H, in
   }
   constexpr int R = G::R, TPC = 256 / G::LW;
   constexpr int NH = (2 * R + TPC - 1) / TPC;        // halo rows per thread (the last may be past 2R)
-  constexpr int NT = (kRbH + TPC - 1) / TPC;         // tile rows per thread (the last may be past 64)
+  constexpr int NT = (kRbH + TPC - 1) / TPC;         // tile rows per thread (the last may be past kRbH)
   const int tid = threadIdx.x;
   if (tid >= TPC * G::LW) return;
   const int lx = tid % G::LW, ly0 = tid / G::LW;
@@ -1075,7 +1079,7 @@ __device__ __forceinline__ void rb_fill_k1(float* lds, int i0, int j0, int H, in
 #pragma unroll
     for (int k = 0; k < NB; ++k) {
       if (k0 + k < NT) {
-        const int ii = (ly0 + TPC * (k0 + k) < kRbH) ? idx : idx - TPC * W;   // past row 63: any loaded row, not stored
+        const int ii = (ly0 + TPC * (k0 + k) < kRbH) ? idx : idx - TPC * W;   // past the last tile row: any loaded row, not stored
         a[k] = bld(ry, ii);
         bb[k] = PEND ? bld(ro, ii) : 0.f;
         idx += TPC * W;
@@ -1277,7 +1281,7 @@ __device__ __forceinline__ void rb_fill_k2_fast(float* lds, int i0, int j0, int 
   }
   constexpr int R = G::R, TPC = 256 / G::LW;
   constexpr int NH = (2 * R + TPC - 1) / TPC;        // halo rows per thread (the last may be past 2R)
-  constexpr int NT = (kRbH + TPC - 1) / TPC;         // tile rows per thread (the last may be past 64)
+  constexpr int NT = (kRbH + TPC - 1) / TPC;         // tile rows per thread (the last may be past kRbH)
   const int tid = threadIdx.x;
   if (tid >= TPC * G::LW) return;
   const int lx = tid % G::LW, ly0 = tid / G::LW;
@@ -1325,7 +1329,7 @@ __device__ __forceinline__ void rb_fill_k2_fast(float* lds, int i0, int j0, int 
 #pragma unroll
     for (int k = 0; k < NB; ++k) {
       if (k0 + k < NT) {
-        const int ii = (ly0 + TPC * (k0 + k) < kRbH) ? idx : idx - TPC * W;   // past row 63: any loaded row, not stored
+        const int ii = (ly0 + TPC * (k0 + k) < kRbH) ? idx : idx - TPC * W;   // past the last tile row: any loaded row, not stored
         a[k] = bld(rn, ii);
         bb[k] = bld(ro, ii);
         t[k] = bld(rt, ii);
@@ -1472,9 +1476,10 @@ __global__ __launch_bounds__(256) void k2_blur_rb(const float* __restrict__ xn, 
       }
     }
   }
-  // d2: 32 x 32 cell = 16 threads (tx) x 4 thread rows (ty) = two half-cells of two waves:
-  // reduce each half in its wave (lanes {c, c+32}: xor 32, then xor 8..1), then combine the
-  // two waves' halves through LDS in a fixed order.  e2 / n2 / t2: whole tile, fixed order.
+  // d2: a wave is two thread rows (2 kRbRows tile rows) x 32 threads; a 32 x 32 cell is 16
+  // threads (tx) of WPC = 32 / (2 kRbRows) waves: reduce each wave's two column halves in the
+  // wave (lanes {c, c+32}: xor 32, then xor 8..1), then combine the cell's waves through LDS
+  // in a fixed order.  e2 / n2 / t2: whole tile, fixed order.
   auto half_sum = [](double v) {
     v += __shfl_xor(v, 32, 64);
 #pragma unroll
@@ -1484,12 +1489,16 @@ __global__ __launch_bounds__(256) void k2_blur_rb(const float* __restrict__ xn, 
   d2 = half_sum(d2);
   if ((lane & 47) == 0) red[wave][lane >> 4] = d2;   // lanes 0 / 16: the wave's two half-cells
   __syncthreads();
-  if (threadIdx.x < 16) {                              // 2 x 2 cells x 4 sums
+  constexpr int CY = kRbH / 32, WPC = 4 / CY;          // cell rows per tile, waves per cell
+  if (threadIdx.x < 8 * CY) {                          // CY x 2 cells x 4 sums
     const int cell = threadIdx.x >> 2, k = threadIdx.x & 3, cy = cell >> 1, cx = cell & 1;
     const int gy = i0 / 32 + cy, gx = j0 / 32 + cx;
     double v = 0.0;
-    if (k == 0) v = red[2 * cy][cx] + red[2 * cy + 1][cx];
-    else if (record && cell == 0) v = ((redm[0][k - 1] + redm[1][k - 1]) + redm[2][k - 1]) + redm[3][k - 1];
+    if (k == 0) {
+      v = red[WPC * cy][cx];
+#pragma unroll
+      for (int q = 1; q < WPC; ++q) v += red[WPC * cy + q][cx];
+    } else if (record && cell == 0) v = ((redm[0][k - 1] + redm[1][k - 1]) + redm[2][k - 1]) + redm[3][k - 1];
     if (gy * 32 < H && gx < cells_x)
       partials[(((size_t)b * cells + (size_t)gy * cells_x + gx) * C + c) * 4 + k] = v;
   }
