@@ -180,7 +180,10 @@ int pnp_solver_iterate(pnp_ctx* ctx, int n_iter);   /* enqueue only (async) */
 int pnp_solver_fetch(pnp_ctx* ctx, float* x_out, float* s_out, double* c_out, double* psnr_out,
                      double* ssim_out);
 int pnp_solver_iterations_done(pnp_ctx* ctx, int* n);
-/* Device pointers of the solver's primal / dual state (read-only views, B*C*H*W). */
+/* Device pointers of the solver's primal / dual state (read-only views, B*C*H*W).  ours-A / ours-B
+ * on the blur operator keep the dual's l2-ball step pending between iterations (it runs inside
+ * the next iteration's first pass); this call applies it first (enqueued on the solver stream),
+ * so d_y is the dual as iteration.py holds it. */
 int pnp_solver_state(pnp_ctx* ctx, const float** d_x, const float** d_y, const float** d_s);
 
 /* Per-kernel timing of the last iterate() call: fills up to `cap` entries of
