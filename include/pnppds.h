@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define PNP_ABI_VERSION 4
+#define PNP_ABI_VERSION 5
 
 typedef struct pnp_ctx pnp_ctx;
 
@@ -203,6 +203,15 @@ int pnp_op_proj_l1_ball(pnp_ctx* ctx, const float* x, float* out, int B, int64_t
 int pnp_op_prox_gkl(pnp_ctx* ctx, const float* x, const float* x0, float* out, int64_t count,
                     double gamma, double alpha, void* stream);
 int pnp_op_denoise(pnp_ctx* ctx, const float* x, float* out, int B, int C, int H, int W, void* stream);
+/* (ABI 5) Synchronizes `stream` (NULL: the context's) and reports whether a single-op
+ * denoiser call's persistent small-batch launch failed (PNP_E_INTERNAL: its results are
+ * invalid).  The solver's own launches are checked by pnp_solver_fetch.               */
+int pnp_op_status(pnp_ctx* ctx, void* stream);
+/* (ABI 5, host only, no device) The fp16 values the fp16 operand precisions store for conv
+ * weights: n_filters 3x3 filters (9 floats each, [c_out][c_in][3][3] order) rounded to fp16
+ * so that each filter's rounding errors sum to ~0 (capi.hip fp16_filter_round).  out holds
+ * float32 copies of the fp16 values; w and out may alias.                              */
+int pnp_fp16_filter_round(const float* w, size_t n_filters, float* out);
 /* dst = src on the device (float4 streaming copy; 16-B aligned, bytes % 16 == 0).  The
  * measured copy ceiling bench.py reports the prox passes' HBM fraction against.        */
 int pnp_device_copy(pnp_ctx* ctx, void* dst, const void* src, size_t bytes, void* stream);

@@ -221,13 +221,46 @@ def make_observation(x_true, deg_op, h, r, gaussian_nl, sp_nl, poisson_noise, po
 # Denoiser (models/denoiser.py:34-46, models/basic_models.py:25-38,
 #           KAIR variant models/network_dncnn.py:42-77)
 # ---------------------------------------------------------------------------
+def fp16_filter_round(w):
+    """The fp16 values the device stores for conv weights w [c_out, c_in, 3, 3] (capi.hip
+    fp16_filter_round; device numerics, not a reference function): round to nearest, then per
+    3x3 filter move taps to their other fp16 neighbour, cheapest added error first (lowest tap
+    index on ties), while a move shrinks |sum of the filter's rounding errors|.  Returns float32
+    arrays of fp16-representable values."""
+    w = np.ascontiguousarray(w, np.float32)
+    f = w.reshape(-1, 9).astype(np.float64)
+    h = w.reshape(-1, 9).astype(np.float16)
+    r = h.astype(np.float64)
+    up = np.nextafter(h, np.float16(np.inf)).astype(np.float64)
+    dn = np.nextafter(h, np.float16(-np.inf)).astype(np.float64)
+    alt = np.where(r == f, r, np.where(r < f, up, dn))
+    cost = np.abs(alt - f) - np.abs(r - f)
+    S = (r - f).sum(1)                              # exact: a few dozen bits span
+    used = np.zeros(r.shape, bool)
+    rows = np.arange(r.shape[0])
+    for _ in range(9):
+        d = alt - r
+        cand = ~used & (np.abs(S[:, None] + d) < np.abs(S)[:, None])
+        any_c = cand.any(1)
+        if not any_c.any():
+            break
+        j = np.argmin(np.where(cand, cost, np.inf), 1)
+        sel = rows[any_c]
+        js = j[any_c]
+        S[sel] += d[sel, js]
+        r[sel, js] = alt[sel, js]
+        used[sel, js] = True
+    return r.astype(np.float32).reshape(w.shape)
+
+
 class OracleDenoiser:
     """Forward of the conv stack on torch-CPU in float32.
 
-    ``emulate_fp16=True`` rounds every conv's input activations and weights to fp16
-    (fp32 accumulation, fp16 storage of hidden activations) — the device numerics of
-    PNP_PREC_FP16.  ``emulate_fp16="w2"``: activations rounded to fp16, weights as the sum of
-    their fp16 high half and the fp16 rounding of the remainder (PNP_PREC_FP16W2).
+    ``emulate_fp16=True`` rounds every conv's input activations to fp16 and takes the weights'
+    fp16 values from ``fp16_filter_round`` (fp32 accumulation, fp16 storage of hidden
+    activations) — the device numerics of PNP_PREC_FP16.  ``emulate_fp16="w2"``: activations
+    rounded to fp16, weights as the sum of that fp16 high half and the fp16 rounding of the
+    remainder (PNP_PREC_FP16W2).
     """
 
     def __init__(self, weights, emulate_fp16=False):
@@ -235,10 +268,12 @@ class OracleDenoiser:
         self.emulate_fp16 = bool(emulate_fp16)
         self.tw = [torch.from_numpy(np.ascontiguousarray(a, np.float32)) for a in weights.weights]
         self.tb = [torch.from_numpy(np.ascontiguousarray(b, np.float32)) for b in weights.biases]
-        if emulate_fp16 == "w2":
-            self.tw = [t.half().float() + (t - t.half().float()).half().float() for t in self.tw]
-        elif emulate_fp16:
-            self.tw = [t.half().float() for t in self.tw]
+        if emulate_fp16:                     # the device's fp16 weights (fp16_filter_round)
+            hi = [torch.from_numpy(fp16_filter_round(t.numpy())) for t in self.tw]
+            if emulate_fp16 == "w2":          # + the fp16 rounding of the remainder
+                self.tw = [a + (t - a).half().float() for a, t in zip(hi, self.tw)]
+            else:
+                self.tw = hi
 
     @torch.no_grad()
     def forward_batch(self, x: np.ndarray) -> np.ndarray:

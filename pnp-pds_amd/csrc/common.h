@@ -68,6 +68,13 @@ __device__ __forceinline__ float act_fn(float v, int act) {
 // and per-CU L1s are not coherent with each other: MI355X_MICROARCH.md, inter-workgroup
 // visibility).  Every spin is bounded: a stuck wait sets *err and proceeds (results wrong,
 // no hang).
+// The contract is sc1-only, not a language-level release / acquire: the flag store and poll
+// are relaxed (agent-scope release / acquire fences measured slower: DESIGN.md §3, small
+// batches), and the ordering comes from (1) every access to handed-off data using the device-
+// scope cache policy kCpolDevice (sc1 stores, sc1 LDS-DMA loads), (2) the storing waves'
+// s_waitcnt vmcnt(0) and (3) the workgroup barrier before the flag store.  A new access to a
+// handed-off buffer must use kCpolDevice too.  tests/test_isa_handoff.py checks (1)-(3) on the
+// built code object of every stack kernel.
 constexpr int kTileSpinMax = 1 << 20;   // polls of ~0.1-1 us each: ~0.1-1 s before giving up
 
 __device__ __forceinline__ void tile_publish(int* flag, int value) {
@@ -85,6 +92,27 @@ __device__ __forceinline__ void tile_wait(const int* flags, int idx, bool want, 
     __builtin_amdgcn_s_sleep(1);
   }
   if ((threadIdx.x & 63) == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Cooperative launch of a persistent kernel whose workgroups wait on each other (the tile
+// hand-off above): the runtime either makes every workgroup of the grid resident at once or
+// fails the launch, so a concurrent launch (another stream, another process) can never leave a
+// waiting workgroup without its producer.  Arguments are converted to the kernel's parameter
+// types, as hipLaunchKernelGGL does.
+template <typename... KArgs>
+inline hipError_t coop_launch_impl(void (*kernel)(KArgs...), int grid, int block, unsigned lds, hipStream_t st,
+                                   KArgs... args) {
+  void* ptrs[] = {static_cast<void*>(&args)...};
+#ifdef PNP_AB_PLAIN_LAUNCH   // A/B build only (round 4): the cost of the cooperative launch
+  return hipLaunchKernel(reinterpret_cast<const void*>(kernel), dim3(grid), dim3(block), ptrs, lds, st);
+#endif
+  return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(kernel), dim3(grid), dim3(block), ptrs, lds, st);
+}
+template <typename... KArgs, typename... Args>
+inline hipError_t coop_launch(void (*kernel)(KArgs...), int grid, int block, unsigned lds, hipStream_t st,
+                              Args... args) {
+  static_assert(sizeof...(KArgs) == sizeof...(Args), "argument count");
+  return coop_launch_impl<KArgs...>(kernel, grid, block, lds, st, static_cast<KArgs>(args)...);
 }
 
 // Workgroup barrier for an LDS hand-off: this wave's LDS accesses complete (lgkmcnt(0)), then

@@ -367,13 +367,6 @@ PNP_V3_INST(6, 0)
 // twice, so the result is bit-identical to two one-layer launches.
 // LDS: input ring 18 x 36 px + intermediate ring 18 x 34 px, 128 B per pixel = 161280 B.
 // ------------------------------------------------------------------------------------
-#ifndef X8_SBAR
-#define X8_SBAR 1     // conv_body_x8's step barrier without the store drain (A/B builds: 0)
-#endif
-#ifndef HEAD_SBAR
-#define HEAD_SBAR 1   // conv_head's tile barriers without the store drain (A/B builds: 0)
-#endif
-
 constexpr int kF2Ring = 18;                                    // rows per ring
 struct SGeom { int b, x0; };
 constexpr int kF2InW = kTileW + 4, kF2MidW = kTileW + 2;       // 36, 34 pixels per ring row
@@ -407,22 +400,13 @@ constexpr bool kNtHead = true;
 __device__ unsigned long long x8_clock[1024][2];   // per workgroup: shader-clock cycles, 100 MHz ticks
 #endif
 
-#ifndef X8_OPQ
-#define X8_OPQ 1      // fragment addresses as opaque VGPRs (A/B builds: 0)
-#endif
-#ifndef X8_G3
-#define X8_G3 5       // groups of 3 N-subtiles in layer l (1) / layer l+1 (4): fewer group transitions; 2: prefetch depth 2 for them (A/B)
-#endif
-#ifndef X8_HSPLIT
-#define X8_HSPLIT 1   // the strip-halo N-subtile's two A-subtiles on the two halves' waves: 306 MFMAs per SIMD-pair and step each instead of 324 / 288 (A/B builds: 0)
-#endif
-#ifndef X8_PRIO
-#define X8_PRIO 1     // static s_setprio 1 before the step loop: 1 = layer l+1's waves (4-7), 2 = layer l's, 0 none (A/B builds; 1: 2.182 -> 2.164 ms, two rounds, one box)
-#endif
-#ifndef X8_PADBR
-#define X8_PADBR 1    // layer l's zero-padding select skipped on interior steps by a uniform branch (A/B builds: 0)
-#endif
-// QL: the A-subtiles (bit q) computed for the last N-subtile (the strip halo's split, X8_HSPLIT).
+// Schedule choices measured by A/B builds in round 3 (the alternatives are in git
+// history before round 4): fragment addresses as opaque VGPRs; groups of 3 N-subtiles with
+// fragment prefetch depth 1; the strip-halo N-subtile's two A-subtiles split over the two
+// halves' waves (306 MFMAs per SIMD and step each instead of 324 / 288); static s_setprio 1 for
+// layer l+1's waves (2.182 -> 2.164 ms); layer l's zero-padding select skipped on interior
+// steps; the step barrier without the store drain (lds_barrier).
+// QL: the A-subtiles (bit q) computed for the last N-subtile (the strip halo's split).
 template <int NT, int PLANE, class Side, int D = 2, int QL = 3>
 __device__ __forceinline__ void x8_kloop(const half8_t (&wA)[kX8KSteps][2], const unsigned char* ring,
                                          const int (&ad)[NT][3], floatx4 (&acc)[NT][2], Side&& side,
@@ -436,7 +420,7 @@ __device__ __forceinline__ void x8_kloop(const half8_t (&wA)[kX8KSteps][2], cons
 #pragma unroll
     for (int dy = 0; dy < 3; ++dy) {
       av[n][dy] = (int)(size_t)ring + ad[n][dy];          // LDS byte address
-      if (X8_OPQ) asm volatile("" : "+v"(av[n][dy]));
+      asm volatile("" : "+v"(av[n][dy]));
     }
   typedef const __attribute__((address_space(3))) half8_t* lds_h8p;
   auto ldB = [&](int ks, int n) {
@@ -569,7 +553,7 @@ __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __re
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if ((X8_PRIO == 1 && layer == 1) || (X8_PRIO == 2 && layer == 0)) __builtin_amdgcn_s_setprio(1);
+  if (layer == 1) __builtin_amdgcn_s_setprio(1);   // layer l+1's waves (4-7, the second-dispatched half)
 
   for (int J = 0; J <= K * sb; ++J) {
     auto side = [&](int ks) {                            // this wave's DMA row of the next step
@@ -590,11 +574,11 @@ __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __re
         const bool all_in = 8 * jb + 8 <= s.H && x0 + kTileW <= s.W;   // rows and columns of u < 16 inside
         // N-subtile u < 16: row u >> 1, columns 1 + 16 (u & 1) .. +15; u == 16: the strip halo
         // (columns 0 and 33 of the 8 rows: pixel px -> row px >> 1, column px & 1 ? 33 : 0)
-        // QL (qlc): the A-subtiles computed for the group's last N-subtile (X8_HSPLIT: the strip
-        // halo's q = 0 on half 0's wave, q = 1 on half 1's; each writes its 4 channels, 8 B)
+        // QL (qlc): the A-subtiles computed for the group's last N-subtile (the strip halo's
+        // q = 0 on half 0's wave, q = 1 on half 1's; each writes its 4 channels, 8 B)
         auto group = [&](auto ntc, auto qlc, int u0, int u1, int u2, bool first) {
           constexpr int NT = decltype(ntc)::value, QL = decltype(qlc)::value;
-          constexpr int DP = NT >= 3 && !(X8_G3 & 2) ? 1 : 2;   // fragment prefetch depth (registers)
+          constexpr int DP = NT >= 3 ? 1 : 2;   // fragment prefetch depth (registers)
           int ad[NT][3], prow[NT], pcol[NT], uu[NT];
 #pragma unroll
           for (int n = 0; n < NT; ++n) {
@@ -634,44 +618,20 @@ __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __re
                                           (f2_slot(8 * J + prow[n]) * kF2MidW + pcol[n]) * 16) = v;
             }
           };
-          if (!X8_PADBR) epi(true);
-          else if (__builtin_amdgcn_readfirstlane((int)all_in)) epi(false);
+          if (__builtin_amdgcn_readfirstlane((int)all_in)) epi(false);
           else epi(true);
         };
         using I1 = std::integral_constant<int, 1>;
         using I2 = std::integral_constant<int, 2>;
         using I3 = std::integral_constant<int, 3>;
-        if (X8_HSPLIT) {                                 // 8 N-subtiles + one A-subtile of the halo each
-          if (half == 0) {
-            group(I3{}, I3{}, 0, 1, 2, true);
-            group(I3{}, I3{}, 3, 4, 5, false);
-            group(I3{}, I1{}, 6, 7, 16, false);
-          } else {
-            group(I3{}, I3{}, 8, 9, 10, true);
-            group(I3{}, I3{}, 11, 12, 13, false);
-            group(I3{}, I2{}, 14, 15, 16, false);
-          }
-        } else if (X8_G3 & 1) {                          // groups of 3 N-subtiles: fewer group transitions
-          if (half == 0) {
-            group(I3{}, I3{}, 0, 1, 2, true);
-            group(I3{}, I3{}, 3, 4, 5, false);
-            group(I3{}, I3{}, 6, 7, 16, false);
-          } else {
-            group(I3{}, I3{}, 8, 9, 10, true);
-            group(I3{}, I3{}, 11, 12, 13, false);
-            group(I2{}, I3{}, 14, 15, 15, false);
-          }
-        } else if (half == 0) {                          // rows 0-3 + the halo: 9 N-subtiles
-          group(I2{}, I3{}, 0, 1, 1, true);
-          group(I2{}, I3{}, 2, 3, 3, false);
-          group(I2{}, I3{}, 4, 5, 5, false);
-          group(I2{}, I3{}, 6, 7, 7, false);
-          group(I1{}, I3{}, 16, 16, 16, false);
-        } else {                                         // rows 4-7: 8
-          group(I2{}, I3{}, 8, 9, 9, true);
-          group(I2{}, I3{}, 10, 11, 11, false);
-          group(I2{}, I3{}, 12, 13, 13, false);
-          group(I2{}, I3{}, 14, 15, 15, false);
+        if (half == 0) {                                 // 8 N-subtiles + one A-subtile of the halo each
+          group(I3{}, I3{}, 0, 1, 2, true);
+          group(I3{}, I3{}, 3, 4, 5, false);
+          group(I3{}, I1{}, 6, 7, 16, false);
+        } else {
+          group(I3{}, I3{}, 8, 9, 10, true);
+          group(I3{}, I3{}, 11, 12, 13, false);
+          group(I3{}, I2{}, 14, 15, 16, false);
         }
       } else {
 #pragma unroll 1
@@ -707,7 +667,7 @@ __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __re
         // N-subtile v = 0..7: output row t = v >> 1, columns 16 (v & 1) .. +15
         auto group = [&](auto ntc, int v0, int v1, int v2, bool first) {
           constexpr int NT = decltype(ntc)::value;
-          constexpr int DP = NT >= 3 && !(X8_G3 & 2) ? 1 : 2;
+          constexpr int DP = NT >= 3 ? 1 : 2;
           int ad[NT][3], vv[NT];
 #pragma unroll
           for (int n = 0; n < NT; ++n) {
@@ -728,16 +688,9 @@ __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __re
         };
         using I2 = std::integral_constant<int, 2>;
         using I3 = std::integral_constant<int, 3>;
-        if (X8_G3 & 4) {
-          group(I3{}, 0, 1, 2, true);
-          group(I3{}, 3, 4, 5, false);
-          group(I2{}, 6, 7, 7, false);
-        } else {
-          group(I2{}, 0, 1, 1, true);
-          group(I2{}, 2, 3, 3, false);
-          group(I2{}, 4, 5, 5, false);
-          group(I2{}, 6, 7, 7, false);
-        }
+        group(I3{}, 0, 1, 2, true);
+        group(I3{}, 3, 4, 5, false);
+        group(I2{}, 6, 7, 7, false);
         asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // the DMAs (older than the 8 stores) landed
       } else {
 #pragma unroll 1
@@ -745,8 +698,7 @@ __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __re
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
     }
-    if (X8_SBAR) lds_barrier();     // the layer-l+1 stores stay in flight (vmcnt above, per role)
-    else __syncthreads();
+    lds_barrier();     // the layer-l+1 stores stay in flight (vmcnt above, per role)
     if (++jb == sb) {
       jb = 0;
       ++kJ;
@@ -1349,16 +1301,14 @@ __global__ __launch_bounds__(256) void conv_head_kernel(const float* __restrict_
     decode_tile(t, s, b, ty0, tx0);
     // (lds_barrier: the previous tile's stores stay in flight; the halo registers' loads are
     // waited for where they are used)
-    if (HEAD_SBAR) lds_barrier();
-    else __syncthreads();
+    lds_barrier();
 #pragma unroll
     for (int k = 0; k < 2; ++k)
       if (tid + 256 * k < kHaloPix) {
         hl[tid + 256 * k] = quad(k, false);
         if (X3) hlo[tid + 256 * k] = quad(k, true);
       }
-    if (HEAD_SBAR) lds_barrier();
-    else __syncthreads();
+    lds_barrier();
     load_halo(t + gridDim.x);
     floatx16 acc00 = {}, acc01 = {}, acc10 = {}, acc11 = {};
 #pragma unroll
@@ -1799,22 +1749,15 @@ void launch_conv_body(const half_t* in, half_t* out, const void* w, const float*
 int launch_conv_stack16(half_t* a, half_t* b, const void* w, const float* bias, int nbody, const ConvShape& s,
                         int act, int num_cus, int* done, int epoch, int* err, bool pairs, hipStream_t st) {
   const int grid = s.tiles < num_cus ? s.tiles : num_cus;
+  const uint4* wp = (const uint4*)w;
   if (pairs && nbody >= 2 && (nbody & 1) == 0) {   // two layers per hand-off
     const int np = nbody / 2;
-    if (act == 0)
-      hipLaunchKernelGGL((conv_stack16x2_kernel<0>), dim3(grid), dim3(256), kX2Lds, st, a, b, (const uint4*)w, bias,
-                         np, s, done, epoch, err);
-    else
-      hipLaunchKernelGGL((conv_stack16x2_kernel<1>), dim3(grid), dim3(256), kX2Lds, st, a, b, (const uint4*)w, bias,
-                         np, s, done, epoch, err);
+    (void)coop_launch(act == 0 ? conv_stack16x2_kernel<0> : conv_stack16x2_kernel<1>, grid, 256, kX2Lds, st, a, b,
+                      wp, bias, np, s, done, epoch, err);
     return np & 1;
   }
-  if (act == 0)
-    hipLaunchKernelGGL((conv_stack16_kernel<0>), dim3(grid), dim3(256), kStkLds, st, a, b, (const uint4*)w, bias, nbody,
-                       s, done, epoch, err);
-  else
-    hipLaunchKernelGGL((conv_stack16_kernel<1>), dim3(grid), dim3(256), kStkLds, st, a, b, (const uint4*)w, bias, nbody,
-                       s, done, epoch, err);
+  (void)coop_launch(act == 0 ? conv_stack16_kernel<0> : conv_stack16_kernel<1>, grid, 256, kStkLds, st, a, b, wp,
+                    bias, nbody, s, done, epoch, err);
   return nbody & 1;
 }
 

@@ -559,12 +559,8 @@ void launch_conv_stack_s3(half_t* aH, half_t* aL, half_t* bH, half_t* bL, const 
                           int* err, hipStream_t st) {
   const S3Geom g = s3_geom(s);
   const int grid = g.tiles < num_cus ? g.tiles : num_cus;
-  if (act == 0)
-    hipLaunchKernelGGL((conv_stack_s3_kernel<0>), dim3(grid), dim3(256), kS3StkLds, st, aH, aL, bH, bL,
-                       (const uint4*)w_hi, (const uint4*)w_lo, bias, nbody, s, g, done, epoch, err);
-  else
-    hipLaunchKernelGGL((conv_stack_s3_kernel<1>), dim3(grid), dim3(256), kS3StkLds, st, aH, aL, bH, bL,
-                       (const uint4*)w_hi, (const uint4*)w_lo, bias, nbody, s, g, done, epoch, err);
+  (void)coop_launch(act == 0 ? conv_stack_s3_kernel<0> : conv_stack_s3_kernel<1>, grid, 256, kS3StkLds, st, aH, aL,
+                    bH, bL, (const uint4*)w_hi, (const uint4*)w_lo, bias, nbody, s, g, done, epoch, err);
 }
 
 }  // namespace pnp

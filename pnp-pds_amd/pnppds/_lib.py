@@ -46,7 +46,7 @@ class pnp_params(C.Structure):
                 ("record_ssim", C.c_int32)]
 
 
-ABI_VERSION = 4   # include/pnppds.h PNP_ABI_VERSION
+ABI_VERSION = 5   # include/pnppds.h PNP_ABI_VERSION
 class pnp_degrade_params(C.Structure):
     _fields_ = [("gaussian_nl", C.c_double), ("sp_nl", C.c_double), ("poisson_alpha", C.c_double),
                 ("poisson_noise", C.c_int32), ("seed", C.c_uint32)]
@@ -92,6 +92,8 @@ _SIGS = {
     "pnp_op_proj_l1_ball": ([_P, _P, _P, C.c_int, C.c_int64, C.c_double, C.c_double, C.c_double, _P], C.c_int),
     "pnp_op_prox_gkl": ([_P, _P, _P, _P, C.c_int64, C.c_double, C.c_double, _P], C.c_int),
     "pnp_op_denoise": ([_P, _P, _P, C.c_int, C.c_int, C.c_int, C.c_int, _P], C.c_int),
+    "pnp_op_status": ([_P, _P], C.c_int),
+    "pnp_fp16_filter_round": ([_F, C.c_size_t, _F], C.c_int),
     "pnp_op_psnr": ([_P, _P, _P, C.c_int, C.c_int64, _D, _P], C.c_int),
     "pnp_degrade": ([_P, C.POINTER(pnp_degrade_params), C.c_int, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P, _P],
                     C.c_int),
@@ -357,6 +359,10 @@ class Context:
 
     def op_denoise(self, x, out, B, Cc, H, W, stream=None):
         self._check(self.lib.pnp_op_denoise(self.h, _P(x), _P(out), B, Cc, H, W, _P(stream) if stream else None))
+
+    def op_status(self, stream=None):
+        """Synchronize the single ops' stream and raise if a persistent denoiser launch failed."""
+        self._check(self.lib.pnp_op_status(self.h, _P(stream) if stream else None))
 
     def device_copy(self, dst, src, nbytes, stream=None):
         """dst = src (device pointers): the float4 streaming copy bench.py measures."""

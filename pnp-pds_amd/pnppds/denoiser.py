@@ -39,6 +39,7 @@ class Denoiser:
             dx = to_device(x)
             dy = to_device(np.empty(x.shape, np.float32))
             ctx.op_denoise(dx.data_ptr(), dy.data_ptr(), B, Cc, H, W)
+            ctx.op_status()
             return from_device(dy, ctx)
         finally:
             if prev != ctx.precision:

@@ -69,7 +69,7 @@ BM3D_METHODS = ("A-PnPPDS-BM3D", "A-PnPFBS-BM3D", "comparisonB-1", "C-PnPPDS-BM3
 # restorations: gray Id 0.067 dB, A random sampling 0.05-0.11 dB over 3000) and for the Poisson
 # method (0.19 dB) they do not, and those run split fp16 (fp16x3: activations and weights as
 # fp16 hi + lo pairs, three MFMAs per product; <= 0.002 dB on every long golden).
-def resolve_precision(precision, method_code: int | None = None) -> str:
+def resolve_precision(precision) -> str:
     if precision not in _lib.PRECISIONS:
         raise ValueError(f"precision must be one of {sorted(_lib.PRECISIONS)}, not {precision!r}")
     return precision
@@ -120,7 +120,7 @@ def test_iter_batch(x_0, x_obsrv, x_true, phi, adj_phi, gamma1, gamma2, alpha_s,
     if Cc != ch:
         raise ValueError(f"ch={ch} but images have {Cc} channels")
     ctx = ctx or get_ctx()
-    ctx.set_precision(resolve_precision(precision, m))
+    ctx.set_precision(resolve_precision(precision))
     if m not in _lib.TV_METHODS:                       # the TV methods use no denoiser
         den = _resolve_denoiser(path_prox, ch)
         den.configure(ctx)

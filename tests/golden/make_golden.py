@@ -283,8 +283,15 @@ LONG_CASES = [
     ("A_rs_s0025_3000", "A-Proposed", "random_sampling", 3, 128, 0.0025, 0.0, False, 0.99, 0.99,      0.95, 1.0,  1.0, 0.8, 3000),
     # comparisonB-2 (BASELINE config 5's method) at its config's inner counts m1 = 35, m2 = 5
     ("ADMM_B2_30",   "comparisonB-2", "blur",         3, 128, 0.01, 0.1, False, 0.99,    0.99,        0.95, 0.95, 1.0, 0.8, 30),
+    # round 4: the fp16 regimes at the lengths they run
+    # ours-B blur + salt-and-pepper for the blur experiments' 1200 iterations (main.py:136-137)
+    ("B_blur_1200",  "B-Proposed", "blur",            3, 128, 0.01, 0.1, False, 1.0,     0.49,        0.95, 0.95, 1.0, 0.8, 1200),
+    # comparisonB-2 at m1 = 35, m2 = 5 for 200 outer iterations (7 000 denoiser calls)
+    ("ADMM_B2_200",  "comparisonB-2", "blur",         3, 128, 0.01, 0.1, False, 0.99,    0.99,        0.95, 0.95, 1.0, 0.8, 200),
+    # the grid's lowest noise level with its largest ball, alpha_n = 0.8 + 10 * 0.02 (main.py:130,143)
+    ("A_blur_s0025_a100_1200", "A-Proposed", "blur",  3, 128, 0.0025, 0.0, False, 0.99,  0.99,        1.0,  1.0,  1.0, 0.8, 1200),
 ]
-LONG_INNER = {"ADMM_B2_30": (35, 5)}     # (m1, m2) where not the default 15, 15
+LONG_INNER = {"ADMM_B2_30": (35, 5), "ADMM_B2_200": (35, 5)}     # (m1, m2) where not the default 15, 15
 
 
 def make_long_golden(ref_root="/root/reference", only=None):

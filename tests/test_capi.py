@@ -56,7 +56,7 @@ def test_exports_are_plain_c(lib):
 
 def test_abi_version_and_errors_without_gpu(lib):
     from pnppds import _lib
-    assert lib.pnp_abi_version() == _lib.ABI_VERSION == 4
+    assert lib.pnp_abi_version() == _lib.ABI_VERSION == 5
     lib.pnp_last_error.restype = ctypes.c_char_p
     h = ctypes.c_void_p()
     rc = lib.pnp_create(0, ctypes.byref(h))
@@ -87,3 +87,37 @@ def test_product_does_not_import_oracle():
             if f.endswith((".py", ".hip", ".h")):
                 txt = open(os.path.join(root, f)).read()
                 assert "pnp_oracle" not in txt and "import oracle" not in txt, f
+
+
+def test_fp16_filter_round_matches_oracle(lib):
+    """The fp16 weight values the device uses (capi.hip fp16_filter_round, host code) equal the
+    oracle's restatement bit for bit, for every layer of the shipped denoisers plus edge values
+    (exact fp16 weights, zeros, subnormals, ties); each filter's rounding-error sum is never
+    larger than round-to-nearest's and every value stays within one fp16 ulp."""
+    import numpy as np
+    from oracle.pnp_oracle import fp16_filter_round
+    from pnppds.weights import resolve_weights
+    fn = lib.pnp_fp16_filter_round
+    fn.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.c_size_t, ctypes.POINTER(ctypes.c_float)]
+    rng = np.random.default_rng(3)
+    edge = np.concatenate([np.zeros(9), np.full(9, 0.5), rng.standard_normal(9) * 1e-6,
+                           np.float16(0.1) + np.array([0.5, -0.5, 0.25, 0, 1, -1, 0.5, 0.5, -0.5]) *
+                           float(np.spacing(np.float16(0.1))),
+                           rng.standard_normal(9 * 64) * 0.05]).astype(np.float32).reshape(-1, 1, 3, 3)
+    layers = [edge]
+    for arch, ch in (("DnCNN_nobn_nch_3_nlev_0.01", 3), ("DnCNN_nobn_nch_1_nlev_0.01", 1), ("dncnn_15", 1)):
+        layers += list(resolve_weights(arch, ch).weights)
+    for w in layers:
+        w = np.ascontiguousarray(w, np.float32)
+        out = np.empty_like(w)
+        assert fn(w.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), w.size // 9,
+                  out.ctypes.data_as(ctypes.POINTER(ctypes.c_float))) == 0
+        ref = fp16_filter_round(w)
+        assert np.array_equal(out.view(np.uint32), ref.view(np.uint32)), w.shape
+        assert np.array_equal(out.astype(np.float16).astype(np.float32), out)          # fp16 values
+        f = w.reshape(-1, 9).astype(np.float64)
+        rn = w.astype(np.float16).astype(np.float64).reshape(-1, 9)
+        e = np.abs((out.reshape(-1, 9) - f).sum(1))
+        assert np.all(e <= np.abs((rn - f).sum(1)))
+        ulp = np.spacing(np.abs(w.reshape(-1, 9)).astype(np.float16)).astype(np.float64)
+        assert np.all(np.abs(out.reshape(-1, 9) - f) <= ulp * (1 + 1e-9) + 6e-8)

@@ -6,6 +6,7 @@ import numpy as np
 import pytest
 
 from conftest import load_golden
+from oracle import pnp_oracle as O
 
 pytestmark = pytest.mark.gpu
 
@@ -171,3 +172,76 @@ def test_dual_state_between_iterates(case):
         got = ctx.solver_fetch()
         for a, b in zip(ref[:5], got[:5]):
             np.testing.assert_array_equal(a, b)
+
+
+def _dev_array(ctx, ptr, shape):
+    import torch
+    n = int(np.prod(shape))
+    t = torch.empty(n, dtype=torch.float32, device="cuda")
+    ctx.device_copy(t.data_ptr(), ptr, n * 4)
+    ctx.synchronize()
+    return t.cpu().numpy().reshape(shape).astype(np.float64)
+
+
+@pytest.mark.parametrize("case", ["A_blur", "B_blur"])
+def test_dual_state_values_after_even_and_odd_counts(case):
+    """The dual pnp_solver_state returns is the reference's y (iteration.py:51-52 / 57-58),
+    recomputed on the host in fp64 from the device's own iterates: after 4 iterations (dual in
+    buffer y) and after 5 (dual in y2).  y_k = v - g2 P_l2(v / g2), v = y_{k-1} + g2 (Phi(2x_k -
+    x_{k-1}) [+ 2 s_k - s_{k-1}])."""
+    from pnppds.operators import load_blur_kernel
+    ctx, m, prm, x0, xo, xt = _setup(case, 2)
+    B, Cc, H, W = x0.shape
+    h = load_blur_kernel("blur_1")
+    ctx.solver_setup(m, prm, B, Cc, H, W, 9)
+    ctx.solver_load(x0, xo, xt)
+    ctx.solver_iterate(3)
+
+    def state():
+        dx, dy, ds = ctx.solver_state()
+        return _dev_array(ctx, dx, x0.shape), _dev_array(ctx, dy, x0.shape), _dev_array(ctx, ds, x0.shape)
+
+    xp, yp, sp_ = state()
+    for _ in (4, 5):
+        ctx.solver_iterate(1)
+        xn, yn, sn = state()
+        n = Cc * H * W
+        r = prm.r if case.startswith("B") else 1.0
+        eps = np.sqrt(n * (1 - prm.sp_nl)) * r * prm.alpha_n * prm.gaussian_nl
+        for b in range(B):
+            v = yp[b] + prm.gamma2 * (O.blur(2 * xn[b] - xp[b], h) + (2 * sn[b] - sp_[b] if case.startswith("B") else 0))
+            want = v - prm.gamma2 * O.proj_l2_ball(v / prm.gamma2, prm.alpha_n, prm.gaussian_nl, prm.sp_nl,
+                                                   xo[b].astype(np.float64), r)
+            assert np.isfinite(eps)
+            np.testing.assert_allclose(yn[b], want, atol=2e-5 * max(1.0, np.abs(want).max()))
+        xp, yp, sp_ = xn, yn, sn
+
+
+def test_destroy_releases_device_memory():
+    """pnp_destroy frees every buffer of the context (the fused-dual y2 / omf were
+    left out of the release list): three create / solve / destroy rounds of ours-A blur at
+    B = 64 RGB 256^2 (50 MB per state array) leave the device's free memory where it was."""
+    import torch
+    from pnppds import _lib
+    from pnppds.iteration import make_params, resolve_method
+    from pnppds.operators import load_blur_kernel
+    from pnppds.weights import resolve_weights
+    B, Cc, H, W = 64, 3, 256, 256
+    x0 = np.full((B, Cc, H, W), 0.5, np.float32)
+    prm = make_params(0.99, 0.99, 1.0, 0.95, 1.0, 15, 15, 0.1, 0.01, 0.0, 300, 0.8, True, True)
+    torch.cuda.synchronize()
+    free0 = None
+    for k in range(3):
+        ctx = _lib.Context(0)
+        ctx.set_denoiser(resolve_weights("DnCNN_nobn_nch_3_nlev_0.01", 3))
+        ctx.set_operator(_lib.OP_BLUR, h=load_blur_kernel("blur_1"))
+        ctx.solver_setup(resolve_method("ours-A"), prm, B, Cc, H, W, 2)
+        ctx.solver_load(x0, x0, x0)
+        ctx.solver_iterate(2)
+        ctx.solver_fetch()
+        ctx.close()
+        torch.cuda.synchronize()
+        free = torch.cuda.mem_get_info()[0]
+        if free0 is None:
+            free0 = free                     # after the first round: runtime / code objects loaded
+        assert free0 - free < 32 << 20, (k, (free0 - free) >> 20)

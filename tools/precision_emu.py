@@ -30,6 +30,34 @@ mode, n = sys.argv[1], int(sys.argv[2])
 torch.set_num_threads(int(sys.argv[3]) if len(sys.argv) > 3 else 4)
 
 
+def round_sum16(w):
+    """fp16 weights with each (cout, cin) 3x3 filter's rounding errors summed to ~0: taps are
+    moved to their other fp16 neighbour, cheapest first, while that shrinks |sum of errors|."""
+    w = w.numpy().astype(np.float32)
+    o, i = w.shape[:2]
+    f = w.reshape(o * i, -1).astype(np.float64)
+    r = f.astype(np.float16).astype(np.float64)
+    up = np.nextafter(r.astype(np.float16), np.float16(np.inf)).astype(np.float64)
+    dn = np.nextafter(r.astype(np.float16), np.float16(-np.inf)).astype(np.float64)
+    alt = np.where(r > f, dn, up)
+    alt = np.where(r == f, r, alt)
+    cost = np.abs(alt - f) - np.abs(r - f)
+    out = r.copy()
+    for k in range(f.shape[0]):
+        S = (out[k] - f[k]).sum()
+        used = np.zeros(f.shape[1], bool)
+        while True:
+            d = alt[k] - out[k]
+            cand = (~used) & (np.abs(S + d) < np.abs(S) - 1e-30)
+            if not cand.any():
+                break
+            j = np.argmin(np.where(cand, cost[k], np.inf))
+            S += d[j]
+            out[k, j] = alt[k, j]
+            used[j] = True
+    return torch.from_numpy(out.reshape(w.shape).astype(np.float32))
+
+
 def split(t, scale):
     hi = t.half().float()
     return hi, ((t - hi) * scale).half().float() / scale
@@ -49,6 +77,11 @@ class Emu(O.OracleDenoiser):
                 h = F.conv2d(h.half().float(), w, b, padding=1)
             elif mode == "w":
                 h = F.conv2d(h, w.half().float(), b, padding=1)
+            elif mode in ("ws", "fs"):
+                if not hasattr(self, "_ws"):
+                    self._ws = [round_sum16(t) for t in self.tw]
+                hin = h if mode == "ws" else h.half().float()
+                h = F.conv2d(hin, self._ws[i], b, padding=1)
             elif mode == "w2":
                 wh, wl = split(w, 1.0)
                 h = F.conv2d(h.half().float(), wh + wl, b, padding=1)
@@ -71,3 +104,5 @@ res = O.test_iter(x0.astype(np.float32).astype(np.float64), obs.astype(np.float3
                   0.99, 0.99, 1.0, 0.95, 1.0, 15, 15, 0.1, 0.01, 0.0, 300.0, den, n, "A-Proposed", 1, 0.8)
 idx = [i for i in (0, 1, 2, 5, 10, 22, n - 1) if i < n]
 print(mode, f"{time.time() - t:.0f}s", {i: round(float(res[3][i]), 5) for i in idx}, flush=True)
+if len(sys.argv) > 4:                      # save the PSNR track for max-over-iterations comparisons
+    np.save(sys.argv[4], np.asarray(res[3]))
