@@ -351,9 +351,11 @@ bool use_pair(pnp_ctx* ctx, int mb, int W) {
 // All body layers in one persistent launch (conv_stack16) for small batches: at most 2 tiles
 // of 8 x 32 per CU (B = 1 at 256^2: 256 tiles), where per-layer launches are fixed-cost-bound
 // (~11 us each for ~2 us of MFMA work).  Not while a graph is captured: the launch's epoch tag
-// is a kernel argument, which a replay would repeat.
-bool use_stack(pnp_ctx* ctx, int tiles) {
-  if (ctx->capturing) return false;
+// is a kernel argument, which a replay would repeat.  Only on the context's own stream (the
+// solver's, and single ops called without a stream), so two of the context's persistent grids
+// never compete for CUs (common.h persistent_launch).
+bool use_stack(pnp_ctx* ctx, int tiles, hipStream_t st) {
+  if (ctx->capturing || st != ctx->stream) return false;   // one persistent grid at a time per context
   if (ctx->body_layers) return ctx->body_layers >= 3;
   return tiles <= 2 * ctx->num_cus;
 }
@@ -473,7 +475,7 @@ void run_denoiser(pnp_ctx* ctx, const float* u32, float* xout, DevBuf (&act)[2],
       }
       int cur = 0;
       const int nbody = ctx->den_depth - 2;
-      if (nbody > 0 && use_stack(ctx, s3_tiles(s))) {   // every body layer in one launch
+      if (nbody > 0 && use_stack(ctx, s3_tiles(s), st)) {   // every body layer in one launch
         ProfScope ps(ctx, "conv_stack_s3", st);
         int epoch = 0;
         int* err = nullptr;
@@ -484,7 +486,7 @@ void run_denoiser(pnp_ctx* ctx, const float* u32, float* xout, DevBuf (&act)[2],
         check_launch(ctx, "conv_stack_s3");
         cur = nbody & 1;
       }
-      for (int l = (nbody > 0 && use_stack(ctx, s3_tiles(s))) ? nbody : 0; l < nbody; ++l, cur ^= 1) {
+      for (int l = (nbody > 0 && use_stack(ctx, s3_tiles(s), st)) ? nbody : 0; l < nbody; ++l, cur ^= 1) {
         ProfScope ps(ctx, "conv_body_s3", st);
         launch_conv_s3_body(P<half_t>(act[cur]), P<half_t>(alo[cur]), P<half_t>(act[cur ^ 1]), P<half_t>(alo[cur ^ 1]),
                             (const char*)ctx->body_s3h.p + (size_t)l * kBodyWBytes,
@@ -516,7 +518,7 @@ void run_denoiser(pnp_ctx* ctx, const float* u32, float* xout, DevBuf (&act)[2],
     int cur = 0;
     const int nbody = ctx->den_depth - 2;
     const bool pair = use_pair(ctx, mb, W);
-    const bool stack = !w2 && !ctx->ablate && nbody > 0 && use_stack(ctx, s.tiles);
+    const bool stack = !w2 && !ctx->ablate && nbody > 0 && use_stack(ctx, s.tiles, st);
     if (stack) {                                 // every body layer in one launch
       ProfScope ps(ctx, "conv_stack16", st);
       int epoch = 0;

@@ -94,25 +94,26 @@ __device__ __forceinline__ void tile_wait(const int* flags, int idx, bool want, 
   if ((threadIdx.x & 63) == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Cooperative launch of a persistent kernel whose workgroups wait on each other (the tile
-// hand-off above): the runtime either makes every workgroup of the grid resident at once or
-// fails the launch, so a concurrent launch (another stream, another process) can never leave a
-// waiting workgroup without its producer.  Arguments are converted to the kernel's parameter
-// types, as hipLaunchKernelGGL does.
+// Launch of a persistent kernel whose workgroups wait on each other (the tile hand-off above),
+// with the arguments converted to the kernel's parameter types as hipLaunchKernelGGL does.  The
+// grid is at most one workgroup per CU and each needs most of a CU's LDS, so all of it is
+// resident unless another persistent grid holds CUs at the same time: within a context only
+// the solver's stream launches these kernels (capi.hip use_stack), and a wait that still hits
+// its spin bound (another process's persistent grid) sets the error word, which
+// pnp_solver_fetch / pnp_op_status turn into PNP_E_INTERNAL.  hipLaunchCooperativeKernel
+// would guarantee co-residency but measured +30 us per launch at B = 1 (cfg2 0.184 -> 0.213
+// ms per iteration, round 4), a sixth of the iteration.
 template <typename... KArgs>
-inline hipError_t coop_launch_impl(void (*kernel)(KArgs...), int grid, int block, unsigned lds, hipStream_t st,
-                                   KArgs... args) {
+inline hipError_t persistent_launch_impl(void (*kernel)(KArgs...), int grid, int block, unsigned lds,
+                                         hipStream_t st, KArgs... args) {
   void* ptrs[] = {static_cast<void*>(&args)...};
-#ifdef PNP_AB_PLAIN_LAUNCH   // A/B build only (round 4): the cost of the cooperative launch
   return hipLaunchKernel(reinterpret_cast<const void*>(kernel), dim3(grid), dim3(block), ptrs, lds, st);
-#endif
-  return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(kernel), dim3(grid), dim3(block), ptrs, lds, st);
 }
 template <typename... KArgs, typename... Args>
-inline hipError_t coop_launch(void (*kernel)(KArgs...), int grid, int block, unsigned lds, hipStream_t st,
-                              Args... args) {
+inline hipError_t persistent_launch(void (*kernel)(KArgs...), int grid, int block, unsigned lds, hipStream_t st,
+                                    Args... args) {
   static_assert(sizeof...(KArgs) == sizeof...(Args), "argument count");
-  return coop_launch_impl<KArgs...>(kernel, grid, block, lds, st, static_cast<KArgs>(args)...);
+  return persistent_launch_impl<KArgs...>(kernel, grid, block, lds, st, static_cast<KArgs>(args)...);
 }
 
 // Workgroup barrier for an LDS hand-off: this wave's LDS accesses complete (lgkmcnt(0)), then

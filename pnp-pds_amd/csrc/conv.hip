@@ -847,8 +847,9 @@ template __global__ void conv_body_w2_kernel<1>(const half_t* __restrict__, half
 // conv_body_v3 (one 8 x 32 tile per CU at 256^2) spends ~11 us for ~2 us of MFMA work: wave
 // launch, weights into registers, halo DMA, drain.  Here a workgroup keeps its tiles for all
 // layers; layer l + 1 of a tile starts once the 3 x 3 neighbourhood of tiles has published
-// layer l (tile_wait / tile_publish, common.h: agent-scope release / acquire on a per-tile
-// progress word, epoch-tagged per launch so the words are never reset), and the next layer's
+// layer l (tile_wait / tile_publish, common.h: relaxed agent-scope stores and polls of a
+// per-tile progress word, epoch-tagged per launch so the words are never reset; ordering by
+// the sc1-only contract stated there), and the next layer's
 // weights load into the registers right after a layer's last tile is published, in flight
 // while the neighbourhood catches up.  The handed-off activations never sit stale in a cache:
 // the epilogue stores and the halo's LDS-DMA loads are device-scope (sc1), so neither side
@@ -1752,11 +1753,11 @@ int launch_conv_stack16(half_t* a, half_t* b, const void* w, const float* bias, 
   const uint4* wp = (const uint4*)w;
   if (pairs && nbody >= 2 && (nbody & 1) == 0) {   // two layers per hand-off
     const int np = nbody / 2;
-    (void)coop_launch(act == 0 ? conv_stack16x2_kernel<0> : conv_stack16x2_kernel<1>, grid, 256, kX2Lds, st, a, b,
+    (void)persistent_launch(act == 0 ? conv_stack16x2_kernel<0> : conv_stack16x2_kernel<1>, grid, 256, kX2Lds, st, a, b,
                       wp, bias, np, s, done, epoch, err);
     return np & 1;
   }
-  (void)coop_launch(act == 0 ? conv_stack16_kernel<0> : conv_stack16_kernel<1>, grid, 256, kStkLds, st, a, b, wp,
+  (void)persistent_launch(act == 0 ? conv_stack16_kernel<0> : conv_stack16_kernel<1>, grid, 256, kStkLds, st, a, b, wp,
                     bias, nbody, s, done, epoch, err);
   return nbody & 1;
 }

@@ -559,7 +559,7 @@ void launch_conv_stack_s3(half_t* aH, half_t* aL, half_t* bH, half_t* bL, const 
                           int* err, hipStream_t st) {
   const S3Geom g = s3_geom(s);
   const int grid = g.tiles < num_cus ? g.tiles : num_cus;
-  (void)coop_launch(act == 0 ? conv_stack_s3_kernel<0> : conv_stack_s3_kernel<1>, grid, 256, kS3StkLds, st, aH, aL,
+  (void)persistent_launch(act == 0 ? conv_stack_s3_kernel<0> : conv_stack_s3_kernel<1>, grid, 256, kS3StkLds, st, aH, aL,
                     bH, bL, (const uint4*)w_hi, (const uint4*)w_lo, bias, nbody, s, g, done, epoch, err);
 }
 

@@ -3,13 +3,14 @@
     python tools/traffic_from_pmc.py profiles/r01/bench/pmc_fetch.csv profiles/r01/bench/pmc_write.csv \
         --out profiles/r01/bench/traffic.json
 
-FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  On gfx950 FETCH_SIZE reports half the
-bytes of wide (16 B/lane) coalesced streaming reads (MI355X_MICROARCH.md, HBM section), the
-access pattern of the conv kernels' LDS-DMA halo loads, so it is doubled for them; the
-prox/operator kernels load 4 B per lane, for which FETCH_SIZE already matches their byte
-count (k2_dual: 1107 MB raw vs 1007 MB algorithmic + halo), so they are taken as reported.
-WRITE_SIZE is exact for 16-B-per-lane stores.  bench.py puts the conv_body entry in its
-roofline ``traffic`` field.
+FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  On gfx950 FETCH_SIZE reports half the bytes
+of a coalesced streaming read at every access width the kernels use: MI355X_MICROARCH.md gives
+it for 16 B per lane, and the round-4 calibration probe (tools/probes/fetch_probe.hip over a
+2 GiB buffer, 8x the Infinity Cache; profiles/r04/probe/) measured exactly 1/2 for 4, 8 and
+16 B per lane alike, and WRITE_SIZE exact for 4- and 16-B stores.  So every kernel's
+FETCH_SIZE is doubled (round 3 took the 4-B/lane prox passes as reported and read K2's
+0.51 GB as "half of its reads from the MALL": it is all of them from the fabric).  bench.py
+puts the conv_body entry in its roofline ``traffic`` field.
 """
 import argparse
 import collections
@@ -17,8 +18,7 @@ import csv
 import json
 import re
 
-WIDE_READ = ("conv_body_f2", "conv_body", "conv_tail", "conv_body_s3", "conv_tail_s3", "conv_stack")   # 16 B/lane
-# (conv_head reads fp32 u32 4 B per lane, r02)
+FETCH_CORRECTION = 2.0   # every access width (profiles/r04/probe/fetch_probe_summary.txt)
 
 
 def short(name):
@@ -55,10 +55,9 @@ def main():
     out = {"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes ({a.fetch_csv}, {a.write_csv})",
            "kernels": {}}
     for k in sorted(set(rd) | set(wr)):
-        r = rd.get(k, 0.0) * (2.0 if k in WIDE_READ else 1.0)
+        r = rd.get(k, 0.0) * FETCH_CORRECTION
         out["kernels"][k] = {"read_bytes": round(r), "write_bytes": round(wr.get(k, 0.0)),
-                             "bytes": round(r + wr.get(k, 0.0)),
-                             "fetch_correction": 2.0 if k in WIDE_READ else 1.0}
+                             "bytes": round(r + wr.get(k, 0.0)), "fetch_correction": FETCH_CORRECTION}
     json.dump(out, open(a.out, "w"), indent=1)
     print(json.dumps(out, indent=1))
 
