@@ -1000,6 +1000,10 @@ template __global__ void conv_stack16_kernel<1>(half_t* __restrict__, half_t* __
 #ifndef X2_WEARLY
 #define X2_WEARLY 0   // K-steps of layer 2p + 1's weights loaded during layer 2p's last epilogue (A/B; more spill)
 #endif
+#ifndef PNP_X2_PF
+#define PNP_X2_PF 1   // A/B builds only
+#endif
+constexpr int kX2Pf = PNP_X2_PF;   // B-fragment prefetch depth (K-steps) of both layers' K-loops
 constexpr int kX2InW = kTileW + 4, kX2InH = kTileH + 4;        // 36 x 12 input halo
 constexpr int kX2InPix = kX2InW * kX2InH;                      // 432 = 54 DMA slots of 8 pixels
 constexpr int kX2Slots = kX2InPix / 8;
@@ -1124,19 +1128,21 @@ __global__ __launch_bounds__(256, 1) void conv_stack16x2_kernel(half_t* __restri
           return *reinterpret_cast<const half8_t*>(hin + o);
         };
         floatx16 acc[NT];
-        half8_t fb[2][NT];
+        half8_t fb[kX2Pf + 1][NT];
 #pragma unroll
-        for (int n = 0; n < NT; ++n) fb[0][n] = ldB(0, n);
+        for (int d = 0; d < kX2Pf; ++d)
+#pragma unroll
+          for (int n = 0; n < NT; ++n) fb[d][n] = ldB(d, n);
 #pragma unroll
         for (int ks = 0; ks < kBodyKSteps; ++ks) {
-          const int r = ks & 1;
-          if (ks + 1 < kBodyKSteps) {
+          if (ks + kX2Pf < kBodyKSteps) {
 #pragma unroll
-            for (int n = 0; n < NT; ++n) fb[r ^ 1][n] = ldB(ks + 1, n);
+            for (int n = 0; n < NT; ++n) fb[(ks + kX2Pf) % (kX2Pf + 1)][n] = ldB(ks + kX2Pf, n);
           }
 #pragma unroll
           for (int n = 0; n < NT; ++n)
-            acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(w[ks], fb[r][n], ks == 0 ? bias16(bl) : acc[n], 0, 0, 0);
+            acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(w[ks], fb[ks % (kX2Pf + 1)][n], ks == 0 ? bias16(bl) : acc[n],
+                                                             0, 0, 0);
         }
         if (last && X2_WEARLY) {           // part of layer 2p + 1's weights, in flight during this epilogue;
           __builtin_amdgcn_sched_barrier(0);   // the barrier keeps the loads below the MFMAs
@@ -1181,19 +1187,21 @@ __global__ __launch_bounds__(256, 1) void conv_stack16x2_kernel(half_t* __restri
           return *reinterpret_cast<const half8_t*>(mid + com[dx][sub] + (n + dy) * (kHaloW * 128));
         };
         floatx16 acc[4];
-        half8_t fb[2][4];
+        half8_t fb[kX2Pf + 1][4];
 #pragma unroll
-        for (int n = 0; n < 4; ++n) fb[0][n] = ldB(0, n);
+        for (int d = 0; d < kX2Pf; ++d)
+#pragma unroll
+          for (int n = 0; n < 4; ++n) fb[d][n] = ldB(d, n);
 #pragma unroll
         for (int ks = 0; ks < kBodyKSteps; ++ks) {
-          const int r = ks & 1;
-          if (ks + 1 < kBodyKSteps) {
+          if (ks + kX2Pf < kBodyKSteps) {
 #pragma unroll
-            for (int n = 0; n < 4; ++n) fb[r ^ 1][n] = ldB(ks + 1, n);
+            for (int n = 0; n < 4; ++n) fb[(ks + kX2Pf) % (kX2Pf + 1)][n] = ldB(ks + kX2Pf, n);
           }
 #pragma unroll
           for (int n = 0; n < 4; ++n)
-            acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(w[ks], fb[r][n], ks == 0 ? bias16(bl) : acc[n], 0, 0, 0);
+            acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(w[ks], fb[ks % (kX2Pf + 1)][n], ks == 0 ? bias16(bl) : acc[n],
+                                                             0, 0, 0);
         }
         STK_STAMP(p, 4);
 #pragma unroll
