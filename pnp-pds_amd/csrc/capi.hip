@@ -118,11 +118,6 @@ struct pnp_ctx {
   DevBuf stack_done, scr_stack_done, stack_err, scr_stack_err;
   int stack_epoch = 0, scr_stack_epoch = 0;
 
-  // small batches: SSIM on a side stream beside the next iteration's K1 / head (ssim_side)
-  hipStream_t side = nullptr;
-  hipEvent_t ev_k2 = nullptr, ev_ssim = nullptr;
-  bool ssim_pending = false;
-
   // profiling
   bool prof = false;
   std::vector<ProfEntry> prof_log;
@@ -605,21 +600,6 @@ void record_ssim(pnp_ctx* ctx, const float* xn, hipStream_t st, int mm_chunks = 
   check_launch(ctx, "ssim");
 }
 
-// Small batches (the stack's criterion: at most 2 conv tiles per CU) run the iteration's SSIM on
-// a side stream: it depends on K2 (x+'s range) and feeds nothing but its metrics row, so it runs
-// beside k3_norm and the next iteration's K1 / head, whose grids leave most CUs idle at B = 1.
-// The solver stream waits for it before the next K2 (which rewrites the range partials; the
-// next-but-one tail rewrites its x+) and at the end of every run, so a sync of the solver
-// stream covers it.  Same kernels, same bits.  Not while a graph is captured.
-bool ssim_side(pnp_ctx* ctx) {
-  return !ctx->capturing && make_conv_shape(ctx->B, ctx->H, ctx->W).tiles <= 2 * ctx->num_cus;
-}
-void ssim_join(pnp_ctx* ctx) {
-  if (!ctx->ssim_pending) return;
-  HIPCHK(ctx, hipStreamWaitEvent(ctx->stream, ctx->ev_ssim, 0));
-  ctx->ssim_pending = false;
-}
-
 // K3 fused into the next K1 (ours-A / ours-B on the register-blocked blur path)
 bool dual_fused(pnp_ctx* ctx, const OpDesc& od) {
   return (ctx->method == PNP_METHOD_A || ctx->method == PNP_METHOD_B) && k1_fused_ok(od, ctx->C, ctx->H, ctx->W);
@@ -670,7 +650,6 @@ void solver_iteration(pnp_ctx* ctx) {
   }
   run_denoiser(ctx, P<float>(ctx->u32), xn, ctx->act, B, H, W, st);
   int mm_chunks = 0;
-  ssim_join(ctx);                              // the previous iteration's SSIM (side stream) is done
   {
     ProfScope ps(ctx, "k2_dual", st);
     const double gkl_gamma = p.my_lambda / p.gamma2;   // iteration.py:63
@@ -692,20 +671,7 @@ void solver_iteration(pnp_ctx* ctx) {
               l2_eps(ctx, n), P<double>(ctx->metrics), ctx->it, ctx->cap, record, ctx->has_true, st, ctx->itp);
     check_launch(ctx, "k3");
   }
-  if (want_ssim(ctx) && ssim_side(ctx)) {
-    if (!ctx->side) {
-      HIPCHK(ctx, hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
-      HIPCHK(ctx, hipEventCreateWithFlags(&ctx->ev_k2, hipEventDisableTiming));
-      HIPCHK(ctx, hipEventCreateWithFlags(&ctx->ev_ssim, hipEventDisableTiming));
-    }
-    HIPCHK(ctx, hipEventRecord(ctx->ev_k2, st));
-    HIPCHK(ctx, hipStreamWaitEvent(ctx->side, ctx->ev_k2, 0));
-    record_ssim(ctx, xn, ctx->side, mm_chunks);
-    HIPCHK(ctx, hipEventRecord(ctx->ev_ssim, ctx->side));
-    ctx->ssim_pending = true;
-  } else {
-    record_ssim(ctx, xn, st, mm_chunks);
-  }
+  record_ssim(ctx, xn, st, mm_chunks);
   if (ctx->capturing) launch_it_advance(P<int>(ctx->it_dev), st);
   ctx->cur ^= 1;
   ctx->it += 1;
@@ -1007,14 +973,12 @@ void solver_run(pnp_ctx* ctx, int n) {
   };
   if (!graph_enabled(ctx)) {
     for (int i = 0; i < n; ++i) plain();
-    ssim_join(ctx);                            // a sync of the solver stream covers the side stream
     return;
   }
   while (n > 0 && (ctx->cur != 0 || ctx->warm_gen != ctx->gen)) {
     plain();
     --n;
   }
-  ssim_join(ctx);                              // before a capture: no wait on an uncaptured event inside
   if (n >= 2) {
     if (!ctx->gexec || ctx->gexec_gen != ctx->gen) graph_build(ctx);
     HIPCHK(ctx, hipMemsetD32Async((hipDeviceptr_t)ctx->it_dev.p, ctx->it, 1, ctx->stream));
@@ -1023,7 +987,6 @@ void solver_run(pnp_ctx* ctx, int n) {
     n &= 1;
   }
   if (n) plain();
-  ssim_join(ctx);
 }
 
 void solver_setup(pnp_ctx* ctx, int method, const pnp_params* params, int B, int C, int H, int W, int cap) {
@@ -1214,11 +1177,7 @@ int pnp_destroy(pnp_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   graph_release(ctx);
-  if (ctx->side) (void)hipStreamSynchronize(ctx->side);
   for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
-  if (ctx->ev_k2) (void)hipEventDestroy(ctx->ev_k2);
-  if (ctx->ev_ssim) (void)hipEventDestroy(ctx->ev_ssim);
-  if (ctx->side) (void)hipStreamDestroy(ctx->side);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;   // every DevBuf member frees its allocation (device ctx->device is current)
   return PNP_OK;

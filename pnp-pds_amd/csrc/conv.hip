@@ -997,13 +997,6 @@ template __global__ void conv_stack16_kernel<1>(half_t* __restrict__, half_t* __
 // so the results are bit-identical (tests/test_gpu_graph.py).  The pairs ping-pong A -> B -> A:
 // after an odd number of pairs the output is in actB (launch_conv_stack16x2 returns which).
 // ------------------------------------------------------------------------------------
-#ifndef X2_WEARLY
-#define X2_WEARLY 0   // K-steps of layer 2p + 1's weights loaded during layer 2p's last epilogue (A/B; more spill)
-#endif
-#ifndef PNP_X2_PF
-#define PNP_X2_PF 1   // A/B builds only
-#endif
-constexpr int kX2Pf = PNP_X2_PF;   // B-fragment prefetch depth (K-steps) of both layers' K-loops
 constexpr int kX2InW = kTileW + 4, kX2InH = kTileH + 4;        // 36 x 12 input halo
 constexpr int kX2InPix = kX2InW * kX2InH;                      // 432 = 54 DMA slots of 8 pixels
 constexpr int kX2Slots = kX2InPix / 8;
@@ -1128,25 +1121,19 @@ __global__ __launch_bounds__(256, 1) void conv_stack16x2_kernel(half_t* __restri
           return *reinterpret_cast<const half8_t*>(hin + o);
         };
         floatx16 acc[NT];
-        half8_t fb[kX2Pf + 1][NT];
+        half8_t fb[2][NT];
 #pragma unroll
-        for (int d = 0; d < kX2Pf; ++d)
-#pragma unroll
-          for (int n = 0; n < NT; ++n) fb[d][n] = ldB(d, n);
+        for (int n = 0; n < NT; ++n) fb[0][n] = ldB(0, n);
 #pragma unroll
         for (int ks = 0; ks < kBodyKSteps; ++ks) {
-          if (ks + kX2Pf < kBodyKSteps) {
+          const int r = ks & 1;
+          if (ks + 1 < kBodyKSteps) {
 #pragma unroll
-            for (int n = 0; n < NT; ++n) fb[(ks + kX2Pf) % (kX2Pf + 1)][n] = ldB(ks + kX2Pf, n);
+            for (int n = 0; n < NT; ++n) fb[r ^ 1][n] = ldB(ks + 1, n);
           }
 #pragma unroll
           for (int n = 0; n < NT; ++n)
-            acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(w[ks], fb[ks % (kX2Pf + 1)][n], ks == 0 ? bias16(bl) : acc[n],
-                                                             0, 0, 0);
-        }
-        if (last && X2_WEARLY) {           // part of layer 2p + 1's weights, in flight during this epilogue;
-          __builtin_amdgcn_sched_barrier(0);   // the barrier keeps the loads below the MFMAs
-          load_w(2 * p + 1, 0, X2_WEARLY);
+            acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(w[ks], fb[r][n], ks == 0 ? bias16(bl) : acc[n], 0, 0, 0);
         }
 #pragma unroll
         for (int n = 0; n < NT; ++n) {
@@ -1171,7 +1158,7 @@ __global__ __launch_bounds__(256, 1) void conv_stack16x2_kernel(half_t* __restri
       }
       __syncthreads();
       STK_STAMP(p, 3);
-      load_w(2 * p + 1, X2_WEARLY, kBodyKSteps);
+      load_w(2 * p + 1, 0, kBodyKSteps);   // (part of it during layer 2p's last epilogue spilled, r03)
       // ---- layer 2p + 1: the 8 x 32 tile from the intermediate (conv_stack16's K-loop) ----
       {
         int com[3][4];
@@ -1187,21 +1174,19 @@ __global__ __launch_bounds__(256, 1) void conv_stack16x2_kernel(half_t* __restri
           return *reinterpret_cast<const half8_t*>(mid + com[dx][sub] + (n + dy) * (kHaloW * 128));
         };
         floatx16 acc[4];
-        half8_t fb[kX2Pf + 1][4];
+        half8_t fb[2][4];
 #pragma unroll
-        for (int d = 0; d < kX2Pf; ++d)
-#pragma unroll
-          for (int n = 0; n < 4; ++n) fb[d][n] = ldB(d, n);
+        for (int n = 0; n < 4; ++n) fb[0][n] = ldB(0, n);
 #pragma unroll
         for (int ks = 0; ks < kBodyKSteps; ++ks) {
-          if (ks + kX2Pf < kBodyKSteps) {
+          const int r = ks & 1;
+          if (ks + 1 < kBodyKSteps) {
 #pragma unroll
-            for (int n = 0; n < 4; ++n) fb[(ks + kX2Pf) % (kX2Pf + 1)][n] = ldB(ks + kX2Pf, n);
+            for (int n = 0; n < 4; ++n) fb[r ^ 1][n] = ldB(ks + 1, n);
           }
 #pragma unroll
           for (int n = 0; n < 4; ++n)
-            acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(w[ks], fb[ks % (kX2Pf + 1)][n], ks == 0 ? bias16(bl) : acc[n],
-                                                             0, 0, 0);
+            acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(w[ks], fb[r][n], ks == 0 ? bias16(bl) : acc[n], 0, 0, 0);
         }
         STK_STAMP(p, 4);
 #pragma unroll

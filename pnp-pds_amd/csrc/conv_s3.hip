@@ -104,22 +104,21 @@ __device__ __forceinline__ int xcd_block_s3(int b, int G) {   // as conv.hip xcd
 }
 
 // MODE 0: body 64 -> 64 (hi/lo out).  MODE 1: tail 64 -> C + residual + clamp (fp32 NCHW out).
-#ifndef S3_EPI
-#define S3_EPI 3      // body epilogue: 1 = bias as the first MFMA's C operand, 2 = activation max without
-#endif                // the compiler's canonicalizing v_max (A/B builds: 0)
-// C operand of a tile's first MFMA: the bias (body, S3_EPI & 1) or zero (the tail adds its own)
+// Body epilogue (round 3, A/B: cfg4 body 1.650 -> 1.639 ms): the bias is the first MFMA's C
+// operand, and the activation's max is one v_max_f32 without the compiler's canonicalizing one.
+// C operand of a tile's first MFMA: the bias (body) or zero (the tail adds its own)
 template <int MODE>
 __device__ __forceinline__ floatx4 s3_c0(const float* bl) {
-  if (MODE == 0 && (S3_EPI & 1)) return floatx4{bl[0], bl[1], bl[2], bl[3]};
+  if (MODE == 0) return floatx4{bl[0], bl[1], bl[2], bl[3]};
   return floatx4{};
 }
 // bias (unless already in the accumulator) + activation in fp32, then the hi / lo fp16 halves
 template <int ACT>
 __device__ __forceinline__ void s3_split(float a, float b, h4_t& hi, h4_t& lo, int i) {
-  float v = (S3_EPI & 1) ? a : a + b;
+  (void)b;                                         // the bias is already in the accumulator
+  float v = a;
   const float t = ACT == 0 ? v * 0.01f : 0.f;
-  if (S3_EPI & 2) asm("v_max_f32 %0, %1, %2" : "=v"(v) : "v"(v), "v"(t));
-  else v = fmaxf(v, t);
+  asm("v_max_f32 %0, %1, %2" : "=v"(v) : "v"(v), "v"(t));
   const half_t h = (half_t)v;
   hi[i] = h;
   lo[i] = (half_t)(v - (float)h);

@@ -808,10 +808,8 @@ __global__ __launch_bounds__(256) void pack_input_kernel(const float* __restrict
 // The LDS halo is only as wide as the taps' non-zero columns need (blur_1: columns -4..+4
 // of 19; rows -8..+8): 72 x 80 floats instead of 80 x 80.
 // =====================================================================================
-#ifndef PNP_RB_H
-#define PNP_RB_H 64           // tile height (64 or 32; A/B builds)
-#endif
-constexpr int kRbW = 64, kRbH = PNP_RB_H, kRbRows = kRbH / 8;   // 8 thread rows x kRbRows rows; 32 threads x 2 columns
+constexpr int kRbW = 64, kRbH = 64, kRbRows = kRbH / 8;   // 8 thread rows x kRbRows rows; 32 threads x 2 columns
+// (64 x 32 tiles measured slower, r03: K1 0.206 -> 0.222, K2 0.269 -> 0.276 ms)
 static_assert(kRbH == 64 || kRbH == 32, "tiles of whole 32 x 32 metric cells");
 
 typedef float f2_t __attribute__((ext_vector_type(2)));
@@ -911,10 +909,7 @@ __device__ __forceinline__ void rb_stencil(const float* lds, const f2_t* __restr
 
 // Halo fills: batches of kRbFill elements per thread (the loads of a batch in flight
 // together, then their LDS stores), so few registers are live and 6 blocks fit per CU.
-#ifndef PNP_RB_FILL
-#define PNP_RB_FILL 8        // A/B builds only
-#endif
-constexpr int kRbFill = PNP_RB_FILL;
+constexpr int kRbFill = 8;      // (batches of 14 / 16 / 27 / 32 measured equal or slower)
 
 // Column-wise halo fill (K1): thread t < TPC LW owns LDS column t % LW and rows t / LW +
 // TPC i, so the column's wrap is resolved once and each row step is an add and one
@@ -958,12 +953,8 @@ __device__ __forceinline__ void rb_fill_cols(float* lds, int i0, int j0, int H, 
 // [x n/8, (x+1) n/8) in order and a tile's halo rows and columns (41 % of its fill: the
 // neighbouring tiles' pixels) are read while those neighbours are in flight on the same
 // XCD's L2 instead of another XCD's.  (A tail of n % 8 blocks keeps the identity order.)
-#ifndef PNP_RB_XCD
-#define PNP_RB_XCD 1          // A/B builds only
-#endif
 __device__ __forceinline__ int rb_block_tile() {
   const int b = blockIdx.x, n = gridDim.x;
-  if (!PNP_RB_XCD) return b;
   const int full = n & ~7;
   return b < full ? (b & 7) * (full >> 3) + (b >> 3) : b;
 }
@@ -993,14 +984,8 @@ __device__ __forceinline__ void st2g(float* __restrict__ p, size_t idx, const f2
   if (nv > 0) p[idx] = v.x;
   if (nv > 1) p[idx + 1] = v.y;
 }
-#ifndef PNP_RB_BATCH
-#define PNP_RB_BATCH 2       // A/B builds only
-#endif
-constexpr int kRbBatch = PNP_RB_BATCH;                   // K2 epilogue rows whose loads are in flight together (2: 0.351 ms K2, 4: 0.366, 1 per pixel before: 0.392)
-#ifndef PNP_RB1_BATCH
-#define PNP_RB1_BATCH kRbRows   // A/B builds only
-#endif
-constexpr int kRb1Batch = PNP_RB1_BATCH;                 // K1: all 8 rows' loads in flight (2: 0.173 ms, 4: 0.170, 8: 0.167)
+constexpr int kRbBatch = 2;                   // K2 epilogue rows whose loads are in flight together (2: 0.351 ms K2, 4: 0.366, 1 per pixel before: 0.392)
+constexpr int kRb1Batch = kRbRows;                 // K1: all 8 rows' loads in flight (2: 0.173 ms, 4: 0.170, 8: 0.167)
 
 // Epilogue rows of a thread: rows i0 + 8ty + r, columns j, j + 1 (nv(r) valid of 2); the
 // per-row index and count are recomputed (two registers live instead of sixteen).
@@ -1504,310 +1489,6 @@ __global__ __launch_bounds__(256) void k2_blur_rb(const float* __restrict__ xn, 
   }
 }
 
-// -------------------------------------------------------------------------------------
-// K2, strip-walking form (round 4): a block walks a 64-column strip of one plane down a run of
-// TB 64 x 64 tiles.  K2 is bound by the latency of its memory phases, not by bytes or issue
-// (r03 PMC: waves waiting on memory 60 % of their cycles, TA busy 7.5 %), and in
-// k2_blur_rb each block's halo fill, stencil and epilogue run one after the other.  Here the
-// next tile's fill rows (x+ and x, own rows + bottom halo: 64 + R rows of LW columns) stream
-// into an LDS staging area by LDS-DMA (buffer_load ... lds, 16 B per lane, no registers) and
-// the current tile's epilogue operands (y, x_obs [s, w]) and the next tile's x_true into
-// registers, all issued before the current tile's stencil, so every memory phase overlaps
-// compute; the top R halo rows are the previous window's rows 64 .. 64+R-1 (an LDS copy), so
-// only the own rows and the bottom halo are read per step.  Two barriers per tile:
-//   loads (y, x_obs of tile k; DMA + x_true of tile k+1) -> stencil(k) -> wait -> barrier ->
-//   copy + combine(k+1) (2 x+ - x into the window; the metric sums from the staged raw rows) ->
-//   barrier -> epilogue(k) (v, s; d2 per 32 x 32 cell).
-// Every sum uses k2_blur_rb's thread mapping and fp32 grouping (the fill's column-wise loop
-// over the tile's own rows, groups of kRbFill rows; the epilogue's per-cell d2), so the two
-// kernels give the same bits: the small-grid latency variant and ragged shapes keep
-// k2_blur_rb, and a single image equals the batch (tests).
-// LDS: window LH x LW + staging 2 x (LH + 1) x LW floats (blur_1: 69.6 KiB: 2 blocks per CU).
-// Needs W % 64 == 0, H % 64 == 0, 16-B aligned halo columns (k2_sw_ok).
-// -------------------------------------------------------------------------------------
-#ifndef PNP_K2_SW
-#define PNP_K2_SW 0          // experiment (1: the strip-walking K2; measured slower, round 4)
-#endif
-template <class G>
-struct SwGeom {
-  static constexpr int CPR = G::LW / 4;                 // 16-B chunks per staged row
-  static constexpr int RPI = 64 / CPR;                  // staged rows per DMA instruction
-  static constexpr int SROWS = (G::LH + RPI - 1) / RPI * RPI;   // staging rows (the last group may pass LH)
-  static constexpr int kStg = SROWS * G::LW;            // floats per staged plane
-  static constexpr bool ok = G::LW % 4 == 0 && (G::kOff - G::R) % 4 == 0 && RPI >= 1 && G::R <= kRbH;
-  static constexpr int kLds = (G::N + 2 * kStg) * 4;
-};
-
-// Staged rows [r0, r0 + n) <- global rows sbase + r (mod H), columns c0 .. c0 + LW - 1 (mod W,
-// chunk-wise), both planes; DMA instructions spread over the 4 waves.
-template <class G>
-__device__ __forceinline__ void sw_issue_dma(float* stg, __amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rsrc_t rb, int sbase,
-                                            int n, int c0, int H, int W) {
-  using S = SwGeom<G>;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int groups = (n + S::RPI - 1) / S::RPI;
-  const int rl = lane / S::CPR, q = lane - rl * S::CPR;
-  int col = c0 + 4 * q;
-  col += col < 0 ? W : 0;
-  col -= col >= W ? W : 0;
-  for (int gq = wave; gq < 2 * groups; gq += 4) {
-    const int pl = gq >= groups, g = gq - pl * groups;
-    int gi = sbase + g * S::RPI + rl;
-    gi %= H;
-    gi += gi < 0 ? H : 0;
-    float* dst = stg + pl * S::kStg + g * S::RPI * G::LW;
-    if (lane < S::RPI * S::CPR)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(pl ? rb : ra, (__attribute__((address_space(3))) void*)dst, 16,
-                                               (unsigned)((gi * W + col) * 4), 0, 0, 0);
-  }
-}
-
-template <class T, int METHOD>
-__global__ __launch_bounds__(256, 2) void k2_blur_sw(const float* __restrict__ xn, const float* __restrict__ xo,
-                                                      float* __restrict__ y, const float* __restrict__ xobs,
-                                                      const float* __restrict__ xtrue, float* __restrict__ s,
-                                                      const float* __restrict__ w, const float* __restrict__ theta,
-                                                      double* __restrict__ partials, const f2_t* __restrict__ wd_fwd,
-                                                      int C, int H, int W, int tiles_x, int tiles, int TB, int cells_x,
-                                                      int cells, double gamma2, double inv_g2, double gkl_gamma,
-                                                      double gkl_alpha, int record, float* __restrict__ mm) {
-  using G = TapGeom<T>;
-  using S = SwGeom<G>;
-  constexpr int R = G::R, TPC = 256 / G::LW;
-  constexpr int NT = (kRbH + TPC - 1) / TPC;            // own rows per fill thread (as rb_fill_k2_fast)
-  extern __shared__ __attribute__((aligned(16))) float sw_lds[];
-  float* win = sw_lds;
-  float* stg = sw_lds + G::N;
-  __shared__ double red[4][2];
-  __shared__ double redm[4][3];
-  __shared__ float redr[4][2];
-  const int tid = threadIdx.x, tx = tid & 31, lane = tid & 63, wave = tid >> 6;
-  // block -> (plane, strip, run of TB tiles), XCD-aware like rb_block_tile
-  const int strips = tiles_x, ty_n = tiles / tiles_x, runs = (ty_n + TB - 1) / TB;
-  const int unit = rb_block_tile();
-  const int bc = unit / (strips * runs), rem = unit - bc * strips * runs;
-  const int strip = rem / runs, run = rem - strip * runs;
-  const int b = bc / C, c = bc - b * C;
-  const int j0 = strip * kRbW, t0 = run * TB, t1 = min(ty_n, t0 + TB);
-  const size_t plane = (size_t)H * W, pb = (size_t)bc * plane;
-  const int c0 = j0 - R + G::kOff;                      // the window's first global column
-  const __amdgpu_buffer_rsrc_t ra = plane_rsrc(xn + pb, H, W), rb = plane_rsrc(xo + pb, H, W);
-  const __amdgpu_buffer_rsrc_t rt = plane_rsrc(record ? (xtrue ? xtrue + pb : nullptr) : nullptr, H, W);
-  const bool want_m = record != 0;
-  // fill-thread geometry (rb_fill_k2_fast): column lx, rows ly0 + TPC k
-  const bool filler = tid < TPC * G::LW;
-  const int lx = tid % G::LW, ly0 = tid / G::LW;
-  const int gjc = c0 + lx;
-  const bool colin = want_m && filler && gjc >= j0 && gjc < j0 + kRbW;
-  int gj = gjc;
-  gj += gj < 0 ? W : 0;
-  gj -= gj >= W ? W : 0;
-  const float th = METHOD == M_B ? theta[b] : 0.f;
-
-  float xt[NT];                                         // x_true of the next combine's own rows
-  auto load_xt = [&](int i0) {
-#pragma unroll
-    for (int k = 0; k < NT; ++k) {
-      const int r = ly0 + TPC * k;
-      xt[k] = bld(rt, (i0 + (r < kRbH ? r : 0)) * W + gj);
-    }
-  };
-  // window rows wr0 .. wr0 + n - 1 <- 2 a - b of staged rows sr0 .., and (own = true) the
-  // metric sums over the tile's own rows (window rows R .. R + 63 = staged rows so ..)
-  float lo = __builtin_inff(), hi = -__builtin_inff();
-  double e2 = 0, n2 = 0, t2 = 0;
-  auto combine = [&](int so, bool top) {                // top: the window's top R rows are staged too (first tile)
-    const float* sa = stg;
-    const float* sb = stg + S::kStg;
-    // halo rows (no sums): the top R (first tile) and the bottom R
-    for (int e = tid; e < (top ? 2 : 1) * R * G::LW; e += 256) {
-      const int hr = e / G::LW, hc = e - hr * G::LW;
-      const int wr = (top && hr < R) ? hr : R + kRbH + (top ? hr - R : hr);   // window row
-      const int sr = wr - R + so;                                             // staged row
-      win[wr * G::LW + hc] = 2.f * sa[sr * G::LW + hc] - sb[sr * G::LW + hc];
-    }
-    if (!filler) return;
-    float be = 0.f, bn = 0.f, bt = 0.f, bl = lo, bh = hi;
-    auto flush = [&] {
-      if (colin) {
-        e2 += be;
-        n2 += bn;
-        t2 += bt;
-      }
-      be = bn = bt = 0.f;
-    };
-#pragma unroll
-    for (int k = 0; k < NT; ++k) {
-      if (k % kRbFill == 0) flush();
-      const int r = ly0 + TPC * k;
-      const bool okr = kRbH % TPC == 0 || r < kRbH;
-      const int sr = (okr ? r : 0) + so;
-      const float a = sa[sr * G::LW + lx], bb = sb[sr * G::LW + lx];
-      if (okr) win[(R + r) * G::LW + lx] = 2.f * a - bb;
-      const float d = a - bb, tt = xt[k] - a;
-      be = fmaf(okr ? d : 0.f, d, be);
-      bn = fmaf(okr ? bb : 0.f, bb, bn);
-      bt = fmaf(okr ? tt : 0.f, tt, bt);
-      bl = okr ? fminf(bl, a) : bl;
-      bh = okr ? fmaxf(bh, a) : bh;
-    }
-    flush();
-    if (colin) {
-      lo = bl;
-      hi = bh;
-    }
-  };
-  auto reduce_metrics = [&] {                           // after combine: per-wave sums (k2_blur_rb order)
-    if (want_m) {
-      e2 = wave_sum(e2);
-      n2 = wave_sum(n2);
-      t2 = wave_sum(t2);
-      if (lane == 0) { redm[wave][0] = e2; redm[wave][1] = n2; redm[wave][2] = t2; }
-      if (mm) {
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-          lo = fminf(lo, __shfl_xor(lo, o, 64));
-          hi = fmaxf(hi, __shfl_xor(hi, o, 64));
-        }
-        if (lane == 0) { redr[wave][0] = lo; redr[wave][1] = hi; }
-      }
-    }
-    e2 = n2 = t2 = 0;
-    lo = __builtin_inff();
-    hi = -__builtin_inff();
-  };
-  constexpr int CY = kRbH / 32, WPC = 4 / CY;
-  // the tile's metric partials (cell 0, k = 1..3) and x+ range (after a barrier that follows
-  // reduce_metrics) / its d2 partials (k = 0, after a barrier that follows the epilogue)
-  auto write_metrics = [&](int ty) {
-    const int i0 = ty * kRbH, tile = ty * tiles_x + strip;
-    if (want_m && tid < 3) {
-      const double v = ((redm[0][tid] + redm[1][tid]) + redm[2][tid]) + redm[3][tid];
-      partials[(((size_t)b * cells + (size_t)(i0 / 32) * cells_x + j0 / 32) * C + c) * 4 + 1 + tid] = v;
-    }
-    if (want_m && mm && tid == 0) {
-      const size_t chunk = (size_t)b * C * tiles + (size_t)c * tiles + tile;
-      mm[chunk * 2 + 0] = fminf(fminf(redr[0][0], redr[1][0]), fminf(redr[2][0], redr[3][0]));
-      mm[chunk * 2 + 1] = fmaxf(fmaxf(redr[0][1], redr[1][1]), fmaxf(redr[2][1], redr[3][1]));
-    }
-  };
-  auto write_d2 = [&](int ty) {
-    const int i0 = ty * kRbH;
-    if (tid < 8 * CY && (tid & 3) == 0) {
-      const int cell = tid >> 2, cy = cell >> 1, cx = cell & 1;
-      double v = red[WPC * cy][cx];
-#pragma unroll
-      for (int q = 1; q < WPC; ++q) v += red[WPC * cy + q][cx];
-      partials[(((size_t)b * cells + (size_t)(i0 / 32 + cy) * cells_x + j0 / 32 + cx) * C + c) * 4] = v;
-    }
-    if (tid < 8 * CY && (tid & 3) != 0 && !want_m) {   // no metrics recorded: zeros, as k2_blur_rb
-      const int cell = tid >> 2, cy = cell >> 1, cx = cell & 1;
-      partials[(((size_t)b * cells + (size_t)(i0 / 32 + cy) * cells_x + j0 / 32 + cx) * C + c) * 4 + (tid & 3)] = 0.0;
-    }
-    if (want_m && tid >= 4 && tid < 8 * CY && (tid & 3) != 0) {   // the other cells' metric slots: zeros
-      const int cell = tid >> 2, cy = cell >> 1, cx = cell & 1;
-      partials[(((size_t)b * cells + (size_t)(i0 / 32 + cy) * cells_x + j0 / 32 + cx) * C + c) * 4 + (tid & 3)] = 0.0;
-    }
-  };
-
-  // ---- prologue: the first tile's whole window ----
-  {
-    const int i0 = t0 * kRbH;
-    sw_issue_dma<G>(stg, ra, rb, i0 - R, G::LH, c0, H, W);
-    if (want_m) load_xt(i0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    combine(R, true);
-    reduce_metrics();
-    __syncthreads();
-    write_metrics(t0);
-  }
-  const bool al = true;                                  // W % 64 == 0: column pairs 8-B aligned
-  for (int ty = t0; ty < t1; ++ty) {
-    const int i0 = ty * kRbH;
-    const bool more = ty + 1 < t1;
-    RbRows rw;
-    rw.init(pb, i0, j0 + 2 * tx, H, W);
-    // 1. this tile's epilogue operands (the oldest loads: ready first)
-    f2_t yv[kRbRows], bv[kRbRows], sv[kRbRows], wv[kRbRows];
-#pragma unroll
-    for (int k = 0; k < kRbRows; ++k) {
-      yv[k] = ld2g(y, rw.ix(k), rw.nv(k), al);
-      bv[k] = ld2g(xobs, rw.ix(k), rw.nv(k), al);
-      if (METHOD == M_B) {
-        sv[k] = ld2g(s, rw.ix(k), rw.nv(k), al);
-        wv[k] = ld2g(w, rw.ix(k), rw.nv(k), al);
-      }
-    }
-    // 2. the next tile's rows (own + bottom halo) into the staging area, its x_true
-    if (more) {
-      sw_issue_dma<G>(stg, ra, rb, i0 + kRbH, kRbH + R, c0, H, W);
-      if (want_m) load_xt(i0 + kRbH);
-    }
-    // 3. the stencil of this tile
-    f2_t g[kRbRows];
-    rb_stencil<T>(win, wd_fwd, g);
-    // the window's rows 64 .. 64+R-1: the next window's top halo
-    constexpr int NCP = (R * G::LW + 255) / 256;
-    float cp[NCP];
-#pragma unroll
-    for (int q = 0; q < NCP; ++q) {
-      const int e = tid + 256 * q;
-      cp[q] = e < R * G::LW ? win[kRbH * G::LW + e] : 0.f;
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // the staging DMA, x_true and the operands
-    __syncthreads();                                     // the window is free, the staging complete
-    if (ty > t0) write_d2(ty - 1);                       // the previous tile's d2 (red[] of its epilogue)
-    if (more) {
-#pragma unroll
-      for (int q = 0; q < NCP; ++q) {
-        const int e = tid + 256 * q;
-        if (e < R * G::LW) win[e] = cp[q];
-      }
-      combine(0, false);
-      reduce_metrics();
-    }
-    __syncthreads();                                     // the next window and its metric sums are in
-    if (more) write_metrics(ty + 1);
-    // 4. this tile's epilogue (as k2_blur_rb)
-    double d2 = 0;
-#pragma unroll
-    for (int r = 0; r < kRbRows; ++r) {
-      f2_t yo = yv[r], so = {0.f, 0.f};
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        if (q >= rw.nv(r)) break;
-        double gv = g[r][q];
-        if (METHOD == M_B) {
-          const float wq = wv[r][q];
-          const float sp = copysignf(fmaxf(fabsf(wq) - th, 0.f), wq);   // operators.py:98
-          gv += 2.0 * (double)sp - (double)sv[r][q];
-          so[q] = sp;
-        }
-        const double v = (double)yv[r][q] + gamma2 * gv;
-        const double ob = bv[r][q];
-        if (METHOD == M_C) {
-          const double tt = v * inv_g2 - gkl_gamma * gkl_alpha;
-          const double p = 0.5 * (tt + sqrt(tt * tt + 4.0 * gkl_gamma * ob));
-          yo[q] = (float)(v - gamma2 * p);
-        } else {
-          yo[q] = (float)v;
-          const double dd = v * inv_g2 - ob;
-          d2 += dd * dd;
-        }
-      }
-      st2g(y, rw.ix(r), yo, rw.nv(r), al);
-      if (METHOD == M_B) st2g(s, rw.ix(r), so, rw.nv(r), al);
-    }
-    d2 += __shfl_xor(d2, 32, 64);
-#pragma unroll
-    for (int o = 8; o > 0; o >>= 1) d2 += __shfl_xor(d2, o, 64);
-    if ((lane & 47) == 0) red[wave][lane >> 4] = d2;     // read after the next step's first barrier
-  }
-  __syncthreads();
-  write_d2(t1 - 1);
-}
-
 // =====================================================================================
 // SSIM (utils/utils_eval.py:9-12): skimage.metrics.structural_similarity(x_true, x,
 // data_range = x.max() - x.min(), channel_axis = 0), scikit-image 0.22.0 defaults:
@@ -2192,33 +1873,6 @@ static void launch_k2_rb(int method, hipStream_t st, const float* xn, const floa
   const int tx = (W + kRbW - 1) / kRbW, tiles = tx * ((H + kRbH - 1) / kRbH);
   const dim3 grid(B * C * tiles);
   const bool lat = B * C * tiles < op.num_cus;     // one block per CU at most: latency-bound
-  using S = SwGeom<TapGeom<T>>;
-  if (PNP_K2_SW && !lat && S::ok && W % kRbW == 0 && H % kRbH == 0) {
-    // strip-walking K2: runs of TB tiles per block, halved until there are >= 3 rounds of blocks
-    // at 2 per CU (the metric: whole 256-row strips, 3072 blocks)
-    const int ty_n = H / kRbH, planes_strips = B * C * tx;
-    int TB = ty_n;
-    while (TB > 1 && (long long)planes_strips * ((ty_n + TB - 1) / TB) < 6LL * op.num_cus) TB = (TB + 1) / 2;
-    const dim3 gsw((unsigned)(planes_strips * ((ty_n + TB - 1) / TB)));
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    static bool attr_set[3][64];                   // per method and device: LDS above 64 KiB
-#define K2SW(M)                                                                                                   \
-  {                                                                                                               \
-    if (dev < 64 && !attr_set[M][dev]) {                                                                          \
-      (void)hipFuncSetAttribute((const void*)k2_blur_sw<T, M>, hipFuncAttributeMaxDynamicSharedMemorySize, S::kLds); \
-      attr_set[M][dev] = true;                                                                                    \
-    }                                                                                                             \
-    hipLaunchKernelGGL((k2_blur_sw<T, M>), gsw, dim3(256), S::kLds, st, xn, xo, y, xobs, xtrue, s, w, theta,      \
-                       partials, reinterpret_cast<const f2_t*>(op.dense_fwd), C, H, W, tx, tiles, TB, cells_x,    \
-                       cells, gamma2, 1.0 / gamma2, gkl_gamma, gkl_alpha, record, mm);                            \
-  }
-    if (method == M_A) K2SW(M_A)
-    else if (method == M_B) K2SW(M_B)
-    else K2SW(M_C)
-#undef K2SW
-    return;
-  }
 #define K2RB_ARGS xn, xo, y, xobs, xtrue, s, w, theta, partials, reinterpret_cast<const f2_t*>(op.dense_fwd), C, H, W, \
                   tx, tiles, cells_x, cells, gamma2, 1.0 / gamma2, gkl_gamma, gkl_alpha, record, mm
 #define K2RBL(M)                                                                                              \
