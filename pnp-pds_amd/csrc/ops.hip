@@ -1087,7 +1087,10 @@ __device__ __forceinline__ void rb_fill_k1(float* lds, int i0, int j0, int H, in
 // (nullable) receives the tile's y, the next K2's input (a separate buffer: other blocks
 // still read v's halo).
 template <class T, bool MB, int LAT = 0, bool PEND = false>
-__global__ __launch_bounds__(256) void k1_blur_rb(const float* __restrict__ x, const float* __restrict__ y,
+// (The batched variants at 7 waves per SIMD, 70-72 VGPRs: the LDS holds 7 blocks per CU; 0.207 -> 0.205 ms at
+// the metric, 0.0815 -> 0.079 at cfg3, round 4.  K2 at 7 spilled 10 VGPRs and was no faster.)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LAT ? 1 : (TapGeom<T>::N * 4 * 7 <= 163840 ? 7 : 1))))
+void k1_blur_rb(const float* __restrict__ x, const float* __restrict__ y,
                                                    const float* __restrict__ xobs, const double* __restrict__ omf,
                                                    double gamma2, float* __restrict__ yout,
                                                    const float* __restrict__ s, float* __restrict__ u32,
