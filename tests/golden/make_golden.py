@@ -290,6 +290,17 @@ LONG_CASES = [
     ("ADMM_B2_200",  "comparisonB-2", "blur",         3, 128, 0.01, 0.1, False, 0.99,    0.99,        0.95, 0.95, 1.0, 0.8, 200),
     # the grid's lowest noise level with its largest ball, alpha_n = 0.8 + 10 * 0.02 (main.py:130,143)
     ("A_blur_s0025_a100_1200", "A-Proposed", "blur",  3, 128, 0.0025, 0.0, False, 0.99,  0.99,        1.0,  1.0,  1.0, 0.8, 1200),
+    # the rest of main.py's blur grid for the fp16 policy: the other noise levels (:130), the
+    # smallest ball alpha_n = 0.82 (:143), and the two DnCNN comparison methods the grid runs
+    # (:133,148-152: gamma1 = 1, myLambda in 0.2 .. 1.99)
+    ("A_blur_s0005_1200", "A-Proposed", "blur",       3, 128, 0.005, 0.0, False, 0.99,   0.99,        0.95, 1.0,  1.0, 0.8, 1200),
+    ("A_blur_s002_1200", "A-Proposed", "blur",        3, 128, 0.02,  0.0, False, 0.99,   0.99,        0.95, 1.0,  1.0, 0.8, 1200),
+    ("A_blur_s004_1200", "A-Proposed", "blur",        3, 128, 0.04,  0.0, False, 0.99,   0.99,        0.95, 1.0,  1.0, 0.8, 1200),
+    ("A_blur_s0025_a082_1200", "A-Proposed", "blur",  3, 128, 0.0025, 0.0, False, 0.99,  0.99,        0.82, 1.0,  1.0, 0.8, 1200),
+    ("FBS_blur_1200", "A-PnPFBS-DnCNN", "blur",       3, 128, 0.01,  0.0, False, 1.0,    0.99,        0.95, 1.0,  1.0, 0.8, 1200),
+    ("FBS_blur_s0025_1200", "A-PnPFBS-DnCNN", "blur", 3, 128, 0.0025, 0.0, False, 1.0,   0.99,        0.95, 1.0,  1.0, 0.8, 1200),
+    ("RED_blur_1200", "A-RED-DnCNN", "blur",          3, 128, 0.01,  0.0, False, 1.0,    0.99,        0.95, 1.0,  1.0, 0.8, 1200),
+    ("RED_blur_s0025_1200", "A-RED-DnCNN", "blur",    3, 128, 0.0025, 0.0, False, 1.0,   0.99,        0.95, 1.0,  1.0, 0.8, 1200),
 ]
 LONG_INNER = {"ADMM_B2_30": (35, 5), "ADMM_B2_200": (35, 5)}     # (m1, m2) where not the default 15, 15
 
