@@ -263,3 +263,31 @@ def test_fp16x3_all_layers_one_launch_bit_identical(gpu_ctx, name, B, C, H, W):
         gpu_ctx.set_precision("fp16")
     np.testing.assert_array_equal(stack, single)
     np.testing.assert_array_equal(stack2, single)
+
+
+@pytest.mark.parametrize("prec", ["fp16", "fp16x3"])
+def test_op_denoise_side_stream_equals_context_stream(gpu_ctx, prec):
+    """A single denoise on the context's stream (NULL) may take the persistent all-layers
+    kernel at a small batch; on a caller's stream it takes the per-layer launches (only the
+    context's stream runs persistent grids, so two of them never compete for CUs).  Both give
+    the same bits, and pnp_op_status reports success on both streams."""
+    import torch
+    w = DenoiserWeights.load_npz(os.path.join(WEIGHTS_DIR, "DnCNN_nobn_nch_3_nlev_0.01.npz"))
+    rng = np.random.default_rng(11)
+    x = rng.uniform(0, 1, (1, 3, 64, 96)).astype(np.float32)
+    gpu_ctx.set_denoiser(w)
+    prev = gpu_ctx.precision
+    gpu_ctx.set_precision(prec)
+    try:
+        dx = torch.from_numpy(x).cuda()
+        d0, d1 = torch.empty_like(dx), torch.empty_like(dx)
+        gpu_ctx.op_denoise(dx.data_ptr(), d0.data_ptr(), 1, 3, 64, 96)        # the context's stream
+        gpu_ctx.op_status()
+        s = torch.cuda.Stream()
+        torch.cuda.synchronize()
+        gpu_ctx.op_denoise(dx.data_ptr(), d1.data_ptr(), 1, 3, 64, 96, stream=s.cuda_stream)
+        gpu_ctx.op_status(stream=s.cuda_stream)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(d0.cpu().numpy(), d1.cpu().numpy())
+    finally:
+        gpu_ctx.set_precision(prev)

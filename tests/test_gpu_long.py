@@ -58,7 +58,14 @@ def run_long(g, precision=None):
                                             # ours-A blur sigma 0.0025 at the grid's alpha_n = 1.00
                                             ("B_blur_1200", "auto"), ("ADMM_B2_200", "auto"),
                                             ("A_blur_s0025_a100_1200", "auto"),
-                                            ("B_blur_1200", "fp16x3"), ("A_blur_s0025_a100_1200", "fp16x3")])
+                                            ("B_blur_1200", "fp16x3"), ("A_blur_s0025_a100_1200", "fp16x3"),
+                                            # the rest of main.py's blur grid (:130,143): sigma 0.005 / 0.02 /
+                                            # 0.04 and the smallest ball alpha_n = 0.82 at sigma 0.0025
+                                            ("A_blur_s0005_1200", "auto"), ("A_blur_s002_1200", "auto"),
+                                            ("A_blur_s004_1200", "auto"), ("A_blur_s0025_a082_1200", "auto"),
+                                            # the grid's DnCNN comparison methods on blur (:133,148-152)
+                                            ("FBS_blur_1200", "auto"), ("FBS_blur_s0025_1200", "auto"),
+                                            ("RED_blur_1200", "auto"), ("RED_blur_s0025_1200", "auto")])
 def test_long_trajectory_psnr(case, precision):
     """Every iteration's PSNR within 0.01 dB of the reference's trajectory.  'auto' is the
     default precision policy (PNP_PREC_AUTO: fp16 operands for ours-A/B and comparisonB-2 on blur, split fp16
