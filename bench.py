@@ -332,8 +332,9 @@ def main():
     ap.add_argument("--op", default="", choices=["", "blur", "Id", "random_sampling"],
                     help="override the config's degradation operator (profiling the elementwise K1/K2)")
     ap.add_argument("--precision", default="auto", choices=["auto", "fp16", "fp16w2", "fp16x3", "fp32"],
-                    help="denoiser operands: auto = the library's per-solve policy (PNP_PREC_AUTO: fp16 for "
-                         "ours-A/B and comparisonB-2 on blur, split fp16 'fp16x3' otherwise)")
+                    help="denoiser operands: auto = the library's per-solve policy (PNP_PREC_AUTO: on blur, fp16 "
+                         "up to sigma 0.01 for ours-A/B, comparisonB-2, PnP-FBS, RED, and fp16w2 above it "
+                         "for ours-A and comparisonB-2; split fp16 'fp16x3' otherwise)")
     ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU-baseline work")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile", type=int, default=1, help="HIP-event per-kernel timing in the timed region")

@@ -90,10 +90,12 @@ enum pnp_precision {
                         three fp16 MFMAs per product (hi*hi + hi*lo + lo*hi), fp32
                         accumulation: near-fp32 results at 1/3 of the fp16 MFMA rate
                         (ABI 4)                                                      */
-  PNP_PREC_AUTO = 4   /* default (ABI 4): per solve, FP16 for A/B-Proposed and comparisonB-2 on the blur
-                        operator (measured within 0.01 dB of the reference over its
-                        experiments' lengths), FP16X3 otherwise; single denoiser calls
-                        (pnp_op_denoise) run FP16X3                                  */
+  PNP_PREC_AUTO = 4   /* default (ABI 4): per solve, on the blur operator: FP16 for
+                        A/B-Proposed, comparisonB-2, A-PnPFBS-DnCNN and A-RED-DnCNN up
+                        to gaussian_nl = 0.01; above it FP16W2 for A-Proposed and
+                        comparisonB-2 (each measured within 0.005 dB of the reference
+                        over its experiments' lengths); FP16X3 otherwise; single
+                        denoiser calls (pnp_op_denoise) run FP16X3                   */
 };
 
 /* Scalar parameters of iteration.test_iter (iteration.py:10), same names/meaning. */

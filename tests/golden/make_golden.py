@@ -301,8 +301,15 @@ LONG_CASES = [
     ("FBS_blur_s0025_1200", "A-PnPFBS-DnCNN", "blur", 3, 128, 0.0025, 0.0, False, 1.0,   0.99,        0.95, 1.0,  1.0, 0.8, 1200),
     ("RED_blur_1200", "A-RED-DnCNN", "blur",          3, 128, 0.01,  0.0, False, 1.0,    0.99,        0.95, 1.0,  1.0, 0.8, 1200),
     ("RED_blur_s0025_1200", "A-RED-DnCNN", "blur",    3, 128, 0.0025, 0.0, False, 1.0,   0.99,        0.95, 1.0,  1.0, 0.8, 1200),
+    # the grid's higher noise levels (main.py:130) for the other fp16-candidate methods: ours-A's
+    # fp16 error grows with sigma (0.0055 / 0.0068 dB at 0.02 / 0.04), so the policy needs them too
+    ("B_blur_s002_1200", "B-Proposed", "blur",        3, 128, 0.02, 0.1, False, 1.0,     0.49,        0.95, 0.95, 1.0, 0.8, 1200),
+    ("B_blur_s004_1200", "B-Proposed", "blur",        3, 128, 0.04, 0.1, False, 1.0,     0.49,        0.95, 0.95, 1.0, 0.8, 1200),
+    ("FBS_blur_s004_1200", "A-PnPFBS-DnCNN", "blur",  3, 128, 0.04,  0.0, False, 1.0,    0.99,        0.95, 1.0,  1.0, 0.8, 1200),
+    ("RED_blur_s004_1200", "A-RED-DnCNN", "blur",     3, 128, 0.04,  0.0, False, 1.0,    0.99,        0.95, 1.0,  1.0, 0.8, 1200),
+    ("ADMM_B2_s004_30", "comparisonB-2", "blur",      3, 128, 0.04, 0.1, False, 0.99,    0.99,        0.95, 0.95, 1.0, 0.8, 30),
 ]
-LONG_INNER = {"ADMM_B2_30": (35, 5), "ADMM_B2_200": (35, 5)}     # (m1, m2) where not the default 15, 15
+LONG_INNER = {"ADMM_B2_30": (35, 5), "ADMM_B2_200": (35, 5), "ADMM_B2_s004_30": (35, 5)}   # (m1, m2) if not 15, 15
 
 
 def make_long_golden(ref_root="/root/reference", only=None):

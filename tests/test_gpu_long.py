@@ -28,6 +28,28 @@ AUTO_FP16_MARGIN_DB = 0.005  # where PNP_PREC_AUTO picks plain fp16 operands: ha
 C_FLOOR = {"fp16": 1e-3, "fp16w2": 1e-3, "fp16x3": 2e-5, "fp32": 2e-6}
 
 
+# Ill-conditioned trajectories (tools/chaos_probe.py on the fp32 test oracle): ours-B
+# at sigma 0.04 moves 0.19 % of its pixels by more than 5e-3 (max 0.025) when x_0 moves by one
+# float32 ulp; PnP-FBS at sigma 0.04 is stable against x_0 but its final pixels differ by up to
+# 0.0022 between two fp32 convolutions (the oracle's vs the reference's) and by 0.012 under split
+# fp16.  Their final iterate is checked by the share of pixels more than 5e-3 off the reference's
+# (bounded here), not pixel by pixel; the PSNR trajectory is the criterion.
+CHAOTIC = {"B_blur_s004_1200": 0.005, "FBS_blur_s004_1200": 0.001}
+FP16_BLUR = ("A-Proposed", "B-Proposed", "comparisonB-2", "A-PnPFBS-DnCNN", "A-RED-DnCNN")
+FP16W2_BLUR = ("A-Proposed", "comparisonB-2")
+
+
+def expected_auto(g):
+    """PNP_PREC_AUTO restated (capi.hip auto_precision): the operands a solve of this golden runs."""
+    sigma, method = float(g["params"][8]), str(g["method"])
+    if str(g["deg_op"]) == "blur":
+        if method in FP16_BLUR and sigma <= 0.01 * (1 + 1e-9):
+            return "fp16"
+        if method in FP16W2_BLUR:
+            return "fp16w2"
+    return "fp16x3"
+
+
 def run_long(g, precision=None):
     from pnppds import operators as ops
     from pnppds.iteration import test_iter
@@ -65,12 +87,18 @@ def run_long(g, precision=None):
                                             ("A_blur_s004_1200", "auto"), ("A_blur_s0025_a082_1200", "auto"),
                                             # the grid's DnCNN comparison methods on blur (:133,148-152)
                                             ("FBS_blur_1200", "auto"), ("FBS_blur_s0025_1200", "auto"),
-                                            ("RED_blur_1200", "auto"), ("RED_blur_s0025_1200", "auto")])
+                                            ("RED_blur_1200", "auto"), ("RED_blur_s0025_1200", "auto"),
+                                            # the grid's higher noise levels for the other methods of the
+                                            # blur family (auto: fp16w2 above sigma 0.01)
+                                            ("B_blur_s002_1200", "auto"), ("B_blur_s004_1200", "auto"),
+                                            ("FBS_blur_s004_1200", "auto"), ("RED_blur_s004_1200", "auto"),
+                                            ("ADMM_B2_s004_30", "auto"),
+                                            ("A_blur_s004_1200", "fp16x3")])
 def test_long_trajectory_psnr(case, precision):
     """Every iteration's PSNR within 0.01 dB of the reference's trajectory.  'auto' is the
-    default precision policy (PNP_PREC_AUTO: fp16 operands for ours-A/B and comparisonB-2 on blur, split fp16
-    elsewhere; with fp16 ones ours-C drifts 0.19 dB over 3000 iterations and ours-A on random
-    sampling 0.05-0.11 dB)."""
+    default precision policy (PNP_PREC_AUTO, restated in expected_auto: on blur, fp16 operands up
+    to sigma 0.01, fp16w2 above it for ours-A and comparisonB-2; split fp16 elsewhere, where fp16
+    ones drift 0.19 dB (ours-C over 3000 iterations) and 0.05-0.11 dB (ours-A random sampling))."""
     g = load_golden(f"long_{case}.npz")
     x, s, c, psnr, ssim, t = run_long(g, precision)
     d = np.abs(psnr - g["psnr"])
@@ -78,12 +106,19 @@ def test_long_trajectory_psnr(case, precision):
     print(f"{case} {precision} ({get_ctx().get_precision()[1]}): max|dPSNR| = {d.max():.5f} dB at iteration {int(d.argmax())}, "
           f"final {psnr[-1]:.4f} vs {g['psnr'][-1]:.4f} dB")
     assert d.max() < PSNR_TOL_DB, (d.max(), int(d.argmax()))
-    np.testing.assert_allclose(x, g["x_out"].astype(np.float32), atol=5e-3)
+    if case in CHAOTIC:   # a share of pixels may move; the PSNR above is the criterion
+        off = np.mean(np.abs(x - g["x_out"].astype(np.float32)) > 5e-3)
+        print(f"  pixels off by > 5e-3: {off:.5f}")
+        assert off <= CHAOTIC[case], (case, off)
+    else:
+        np.testing.assert_allclose(x, g["x_out"].astype(np.float32), atol=5e-3)
     from pnppds._device import get_ctx
     prec = get_ctx().get_precision()[1]          # what 'auto' resolved to for this solve
-    if precision == "auto" and prec == "fp16":
-        # the policy runs plain fp16 operands only with half the bound to spare
-        assert d.max() <= AUTO_FP16_MARGIN_DB, (case, d.max())
+    if precision == "auto":
+        assert prec == expected_auto(g), (case, prec)
+        if prec in ("fp16", "fp16w2"):
+            # the policy runs fp16 activations only with half the bound to spare
+            assert d.max() <= AUTO_FP16_MARGIN_DB, (case, d.max())
     np.testing.assert_allclose(c, g["c"], rtol=0.05, atol=C_FLOOR[prec])
     print(f"  c_n final {c[-1]:.3e} vs {g['c'][-1]:.3e}")
 
