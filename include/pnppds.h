@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define PNP_ABI_VERSION 5
+#define PNP_ABI_VERSION 6
 
 typedef struct pnp_ctx pnp_ctx;
 
@@ -214,6 +214,10 @@ int pnp_op_status(pnp_ctx* ctx, void* stream);
  * so that each filter's rounding errors sum to ~0 (capi.hip fp16_filter_round).  out holds
  * float32 copies of the fp16 values; w and out may alias.                              */
 int pnp_fp16_filter_round(const float* w, size_t n_filters, float* out);
+/* (ABI 6, host only, no device) What PNP_PREC_AUTO resolves to for a solve of `method` on
+ * operator `op_kind` at Gaussian noise level `gaussian_nl` (pnp_params.gaussian_nl): a
+ * pnp_precision value, or PNP_E_ARG for an unknown method / operator.                    */
+int pnp_auto_precision(int method, int op_kind, double gaussian_nl);
 /* dst = src on the device (float4 streaming copy; 16-B aligned, bytes % 16 == 0).  The
  * measured copy ceiling bench.py reports the prox passes' HBM fraction against.        */
 int pnp_device_copy(pnp_ctx* ctx, void* dst, const void* src, size_t bytes, void* stream);

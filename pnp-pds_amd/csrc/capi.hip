@@ -1668,6 +1668,12 @@ int pnp_fp16_filter_round(const float* w, size_t n_filters, float* out) {
   return PNP_OK;
 }
 
+int pnp_auto_precision(int method, int op_kind, double gaussian_nl) {
+  if (method < PNP_METHOD_A || method > PNP_METHOD_C_RED || op_kind < PNP_OP_ID || op_kind > PNP_OP_RANDOM_SAMPLING)
+    return PNP_E_ARG;
+  return auto_precision(method, op_kind, gaussian_nl);
+}
+
 int pnp_op_status(pnp_ctx* ctx, void* stream) {
   if (!ctx) return PNP_E_ARG;
   return guarded(ctx, [&] {

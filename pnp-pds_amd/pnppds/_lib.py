@@ -46,7 +46,7 @@ class pnp_params(C.Structure):
                 ("record_ssim", C.c_int32)]
 
 
-ABI_VERSION = 5   # include/pnppds.h PNP_ABI_VERSION
+ABI_VERSION = 6   # include/pnppds.h PNP_ABI_VERSION
 class pnp_degrade_params(C.Structure):
     _fields_ = [("gaussian_nl", C.c_double), ("sp_nl", C.c_double), ("poisson_alpha", C.c_double),
                 ("poisson_noise", C.c_int32), ("seed", C.c_uint32)]
@@ -94,6 +94,7 @@ _SIGS = {
     "pnp_op_denoise": ([_P, _P, _P, C.c_int, C.c_int, C.c_int, C.c_int, _P], C.c_int),
     "pnp_op_status": ([_P, _P], C.c_int),
     "pnp_fp16_filter_round": ([_F, C.c_size_t, _F], C.c_int),
+    "pnp_auto_precision": ([C.c_int, C.c_int, C.c_double], C.c_int),
     "pnp_op_psnr": ([_P, _P, _P, C.c_int, C.c_int64, _D, _P], C.c_int),
     "pnp_degrade": ([_P, C.POINTER(pnp_degrade_params), C.c_int, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P, _P],
                     C.c_int),
@@ -178,6 +179,20 @@ def device_count() -> int:
     return n.value
 
 
+OP_KINDS = {"Id": OP_ID, "blur": OP_BLUR, "random_sampling": OP_RANDOM_SAMPLING}
+
+
+def auto_precision(method: int, op_kind, gaussian_nl: float) -> str:
+    """What precision='auto' (PNP_PREC_AUTO) resolves to for a solve of ``method`` (a METHOD_*
+    code) on ``op_kind`` (OP_* code or 'Id' / 'blur' / 'random_sampling') at noise level
+    ``gaussian_nl``: 'fp16', 'fp16w2' or 'fp16x3' (pnp_auto_precision; no device needed)."""
+    op = OP_KINDS[op_kind] if isinstance(op_kind, str) else int(op_kind)
+    rc = load_library().pnp_auto_precision(int(method), op, float(gaussian_nl))
+    if rc < 0:
+        raise PnpError(rc, f"unknown method {method} or operator {op_kind}")
+    return PRECISION_NAMES[rc]
+
+
 def as_f32(a):
     return np.ascontiguousarray(a, dtype=np.float32)
 
@@ -228,8 +243,8 @@ class Context:
         self._denoiser_key = key
 
     def set_precision(self, precision):
-        """Denoiser operands: 'auto' (default: the library's per-solve policy, fp16 for ours-A/B
-        on blur and fp16x3 otherwise; include/pnppds.h PNP_PREC_AUTO), 'fp16' (fp32
+        """Denoiser operands: 'auto' (default: the library's per-solve policy, auto_precision()
+        below; include/pnppds.h PNP_PREC_AUTO), 'fp16' (fp32
         accumulation), 'fp16w2' (fp16 activations, weights as fp16 hi + lo pairs: two MFMAs per
         product), 'fp16x3' (activations and weights as hi + lo pairs: three MFMAs per product,
         near-fp32) or 'fp32' (the reference's own precision, models/denoiser.py:37; about a

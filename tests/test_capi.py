@@ -56,7 +56,7 @@ def test_exports_are_plain_c(lib):
 
 def test_abi_version_and_errors_without_gpu(lib):
     from pnppds import _lib
-    assert lib.pnp_abi_version() == _lib.ABI_VERSION == 5
+    assert lib.pnp_abi_version() == _lib.ABI_VERSION == 6
     lib.pnp_last_error.restype = ctypes.c_char_p
     h = ctypes.c_void_p()
     rc = lib.pnp_create(0, ctypes.byref(h))
@@ -121,3 +121,35 @@ def test_fp16_filter_round_matches_oracle(lib):
         assert np.all(e <= np.abs((rn - f).sum(1)))
         ulp = np.spacing(np.abs(w.reshape(-1, 9)).astype(np.float16)).astype(np.float64)
         assert np.all(np.abs(out.reshape(-1, 9) - f) <= ulp * (1 + 1e-9) + 6e-8)
+
+
+def test_auto_precision_policy(lib):
+    """PNP_PREC_AUTO (capi.hip auto_precision, exported as pnp_auto_precision) against the
+    policy test_gpu_long.py asserts on the device: every long golden's method, operator and
+    sigma, plus the sigma threshold's edges, the non-denoiser operators and bad arguments."""
+    from conftest import load_golden
+    from pnppds import _lib
+    from pnppds.iteration import resolve_method
+    from test_gpu_long import expected_auto
+    golden_dir = os.path.join(REPO, "tests", "golden")
+    names = sorted(f[len("long_"):-len(".npz")] for f in os.listdir(golden_dir) if f.startswith("long_"))
+    checked = 0
+    for name in names:
+        g = load_golden(f"long_{name}.npz")
+        if "method" not in g:                # long_A_blur_256: the trajectory-only fixture
+            continue
+        checked += 1
+        got = _lib.auto_precision(resolve_method(str(g["method"])), str(g["deg_op"]), float(g["params"][8]))
+        assert got == expected_auto(g), (name, got)
+    assert checked >= 25
+    A, B, C = _lib.METHOD_A, _lib.METHOD_B, _lib.METHOD_C
+    for m, op, sig, want in [(A, "blur", 0.01, "fp16"), (A, "blur", 0.0100001, "fp16w2"), (A, "blur", 0.0, "fp16"),
+                             (B, "blur", 0.01, "fp16"), (B, "blur", 0.02, "fp16x3"),
+                             (_lib.METHOD_ADMM_B2, "blur", 0.04, "fp16w2"), (_lib.METHOD_A_RED, "blur", 0.04, "fp16x3"),
+                             (_lib.METHOD_A_PNPFBS, "blur", 0.005, "fp16"), (C, "blur", 0.0, "fp16x3"),
+                             (A, "Id", 0.01, "fp16x3"), (A, "random_sampling", 0.01, "fp16x3"),
+                             (_lib.METHOD_B_RED, "blur", 0.01, "fp16x3"), (_lib.METHOD_C_RED, "blur", 0.0, "fp16x3")]:
+        assert _lib.auto_precision(m, op, sig) == want, (m, op, sig)
+    fn = lib.pnp_auto_precision
+    fn.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_double]
+    assert fn(13, 1, 0.01) == -1 and fn(-1, 1, 0.01) == -1 and fn(0, 3, 0.01) == -1
