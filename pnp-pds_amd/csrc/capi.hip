@@ -509,23 +509,27 @@ void run_denoiser(pnp_ctx* ctx, const float* u32, float* xout, DevBuf (&act)[2],
     const float* xin = u32 + (size_t)b0 * C * H * W;
     float* xo = xout + (size_t)b0 * C * H * W;
     const bool w2 = ctx->prec == PNP_PREC_FP16W2;
-    {
+    int cur = 0;
+    const int nbody = ctx->den_depth - 2;
+    const bool pair = use_pair(ctx, mb, W);
+    const bool stack = !w2 && !ctx->ablate && nbody > 0 && use_stack(ctx, s.tiles, st);
+    const bool stack_pairs = ctx->body_layers != 4;
+    // the two-layer stack computes the head itself (its first pair's input halo)
+    const bool head_in_stack = stack && stack16_takes_head(nbody, stack_pairs);
+    if (!head_in_stack) {
       ProfScope ps(ctx, "conv_head", st);
       launch_conv_head(xin, C, P<half_t>(act[0]), ctx->head_w.p, w2 ? ctx->head_wlo.p : nullptr, P<float>(ctx->head_b),
                        s, ctx->den_act, ctx->num_cus, 4, st);
       check_launch(ctx, "conv_head");
     }
-    int cur = 0;
-    const int nbody = ctx->den_depth - 2;
-    const bool pair = use_pair(ctx, mb, W);
-    const bool stack = !w2 && !ctx->ablate && nbody > 0 && use_stack(ctx, s.tiles, st);
     if (stack) {                                 // every body layer in one launch
       ProfScope ps(ctx, "conv_stack16", st);
       int epoch = 0;
       int* err = nullptr;
       int* done = stack_flags(ctx, &act[0] == &ctx->act[0], s.tiles, nbody, st, epoch, err);
       cur = launch_conv_stack16(P<half_t>(act[0]), P<half_t>(act[1]), ctx->body_w.p, P<float>(ctx->body_b), nbody,
-                                s, ctx->den_act, ctx->num_cus, done, epoch, err, ctx->body_layers != 4, st);
+                                s, ctx->den_act, ctx->num_cus, done, epoch, err, stack_pairs, st,
+                                head_in_stack ? xin : nullptr, C, ctx->head_w.p, P<float>(ctx->head_b));
       check_launch(ctx, "conv_stack16");
     }
     for (int l = stack ? nbody : 0; l < nbody;) {

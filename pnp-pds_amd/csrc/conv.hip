@@ -1005,17 +1005,29 @@ constexpr int kX2In = 4 * kX2SlotsW * 1024;                    // 57344 B per in
 constexpr int kX2Mid = 2 * kX2In;                              // intermediate (10 x 34, halo_off layout)
 constexpr int kX2Lds = kX2Mid + kV3Halo;                       // 158208 B
 static_assert(kX2Lds <= 163840, "conv_stack16x2 LDS");
+// HEAD: the head layer (C -> 64) computed into the first pair's input halo (round 4, VERDICT r03
+// item 6): its 12 x 36 outputs need the fp32 input on 14 x 38 pixels, staged as 4 fp16 channels
+constexpr int kX2HeadW = kX2InW + 2, kX2HeadPix = kX2HeadW * (kX2InH + 2);   // 38 x 14 = 532
+constexpr int kX2LdsHead = kX2Lds + kX2HeadPix * 8;            // 162464 B
+static_assert(kX2LdsHead <= 163840, "conv_stack16x2 LDS with the head stage");
 
 __device__ __forceinline__ int x2_in_off(int pr, int pc, int chunk) {          // 12 x 36 input halo
   return (pr * kX2InW + pc) * 128 + 16 * (chunk ^ ((pc >> 1) & 7));
 }
 
-template <int ACT>
+// HEAD: pair 0's input halo is the head layer of conv_head_kernel (PREC 0) computed in place from
+// the fp32 NCHW input u32 (C channels): the same packed weights hw, the same three
+// v_mfma_f32_32x32x16_f16 per output in the same K order from a zero accumulator, the same fp16
+// input rounding and bias_act8 epilogue, zero outside the image (the activation images' border),
+// so the bits are those of the head launch plus the DMA it replaces.
+template <int ACT, bool HEAD>
 __global__ __launch_bounds__(256, 1) void conv_stack16x2_kernel(half_t* __restrict__ actA, half_t* __restrict__ actB,
                                                                  const uint4* __restrict__ wpk,
                                                                  const float* __restrict__ bias, int npairs,
                                                                  ConvShape s, int* __restrict__ done, int epoch,
-                                                                 int* __restrict__ err) {
+                                                                 int* __restrict__ err, const float* __restrict__ u32,
+                                                                 int C, const uint4* __restrict__ hw,
+                                                                 const float* __restrict__ hb) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1084,9 +1096,71 @@ __global__ __launch_bounds__(256, 1) void conv_stack16x2_kernel(half_t* __restri
       }
       STK_STAMP(p, 1);
       unsigned char* hin = smem + (k & 1) * kX2In;
-      issue_dma(hin, src, b, ty0, tx0);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
+      if (HEAD && p == 0) {
+        // fp32 input rows ty0-3 .. ty0+10, columns tx0-3 .. tx0+34 -> 4 fp16 channels per pixel
+        // (channels >= C and pixels outside the image 0, as conv_head_kernel's quad())
+        // (buffer loads of the image's C planes: no plain global load besides the progress polls,
+        // which tests/test_isa_handoff.py requires to be sc1)
+        uint2* hst = reinterpret_cast<uint2*>(smem + kX2Lds);
+        const unsigned plane = (unsigned)(s.H * s.W);
+        const __amdgpu_buffer_rsrc_t ru = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(u32 + (size_t)b * C * plane), (short)0, (int)(C * plane * 4u), 0x00020000);
+        for (int q = tid; q < kX2HeadPix; q += 256) {
+          const int r = q / kX2HeadW, c = q - r * kX2HeadW;
+          const int gy = ty0 - 3 + r, gx = tx0 - 3 + c;
+          const bool in = gy >= 0 && gy < s.H && gx >= 0 && gx < s.W;
+          const unsigned o = in ? (unsigned)(gy * s.W + gx) : 0u;
+          _Float16 h4[4];
+#pragma unroll
+          for (int ch = 0; ch < 4; ++ch) {
+            const float v = __builtin_bit_cast(
+                float, __builtin_amdgcn_raw_buffer_load_b32(ru, ((unsigned)min(ch, C - 1) * plane + o) * 4u, 0, 0));
+            h4[ch] = (ch < C && in) ? (_Float16)v : (_Float16)0;
+          }
+          hst[q] = make_uint2((uint32_t)__builtin_bit_cast(uint16_t, h4[0]) |
+                                  ((uint32_t)__builtin_bit_cast(uint16_t, h4[1]) << 16),
+                              (uint32_t)__builtin_bit_cast(uint16_t, h4[2]) |
+                                  ((uint32_t)__builtin_bit_cast(uint16_t, h4[3]) << 16));
+        }
+        half8_t ha[kHeadKSteps];
+#pragma unroll
+        for (int ks = 0; ks < kHeadKSteps; ++ks)
+          ha[ks] = *reinterpret_cast<const half8_t*>(reinterpret_cast<const unsigned char*>(hw) +
+                                                     ((ks * 2 + m) * 64 + lane) * 16);
+        float hbl[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) hbl[r] = hb[32 * m + 16 * h + r];
+        __syncthreads();
+        // the 12 x 36 halo = 432 pixels, N-tiles of 32 (pixel 32 n + col, the last one half used);
+        // wave (m, rq): M-tile m of N-tiles rq, rq + 2, ..
+        for (int n = rq; n < (kX2InPix + 31) / 32; n += 2) {
+          const int pix = 32 * n + col, pl = min(pix, kX2InPix - 1);
+          const int pr = pl / kX2InW, pc = pl - pr * kX2InW;
+          floatx16 acc = {};
+#pragma unroll
+          for (int ks = 0; ks < kHeadKSteps; ++ks) {
+            const int t0 = 4 * ks + 2 * h;               // this lane's two taps (k = 8h .. 8h+7)
+            uint2 q0 = make_uint2(0, 0), q1 = make_uint2(0, 0);
+            if (t0 < 9) q0 = hst[(pr + t0 / 3) * kX2HeadW + pc + t0 % 3];
+            if (t0 + 1 < 9) q1 = hst[(pr + (t0 + 1) / 3) * kX2HeadW + pc + (t0 + 1) % 3];
+            const uint4 q = make_uint4(q0.x, q0.y, q1.x, q1.y);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ha[ks], *reinterpret_cast<const half8_t*>(&q), acc, 0, 0, 0);
+          }
+          const int gy = ty0 - 2 + pr, gx = tx0 - 2 + pc;
+          const bool inside = gy >= 0 && gy < s.H && gx >= 0 && gx < s.W;
+          half8_t v0 = bias_act8<ACT>(acc, 0, hbl), v1 = bias_act8<ACT>(acc, 8, hbl + 8);
+          if (!inside) v0 = v1 = half8_t{};
+          if (pix < kX2InPix) {
+            *reinterpret_cast<half8_t*>(hin + x2_in_off(pr, pc, 4 * m + 2 * h)) = v0;
+            *reinterpret_cast<half8_t*>(hin + x2_in_off(pr, pc, 4 * m + 2 * h + 1)) = v1;
+          }
+        }
+        __syncthreads();
+      } else {
+        issue_dma(hin, src, b, ty0, tx0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+      }
       STK_STAMP(p, 2);
       // ---- layer 2p: the 10 x 34 intermediate into LDS ----
       // N-tile u < 10: intermediate row u, columns 1 .. 32 (lane col -> column col + 1);
@@ -1211,12 +1285,17 @@ __global__ __launch_bounds__(256, 1) void conv_stack16x2_kernel(half_t* __restri
   }
 }
 
-template __global__ void conv_stack16x2_kernel<0>(half_t* __restrict__, half_t* __restrict__,
-                                                  const uint4* __restrict__, const float* __restrict__, int, ConvShape,
-                                                  int* __restrict__, int, int* __restrict__);
-template __global__ void conv_stack16x2_kernel<1>(half_t* __restrict__, half_t* __restrict__,
-                                                  const uint4* __restrict__, const float* __restrict__, int, ConvShape,
-                                                  int* __restrict__, int, int* __restrict__);
+#define PNP_X2_INST(A, HD)                                                                                   \
+  template __global__ void conv_stack16x2_kernel<A, HD>(half_t* __restrict__, half_t* __restrict__,             \
+                                                        const uint4* __restrict__, const float* __restrict__, int, \
+                                                        ConvShape, int* __restrict__, int, int* __restrict__,    \
+                                                        const float* __restrict__, int, const uint4* __restrict__, \
+                                                        const float* __restrict__);
+PNP_X2_INST(0, false)
+PNP_X2_INST(1, false)
+PNP_X2_INST(0, true)
+PNP_X2_INST(1, true)
+#undef PNP_X2_INST
 
 // ------------------------------------------------------------------------------------
 // Head layer C -> 64 (basic_models.py:16,27-28).  Input: the fp32 NCHW denoiser input u32
@@ -1661,8 +1740,12 @@ hipError_t conv_kernels_init() {
     e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kStkLds);
     if (e != hipSuccess) return e;
   }
-  for (const void* k : {(const void*)conv_stack16x2_kernel<0>, (const void*)conv_stack16x2_kernel<1>}) {
+  for (const void* k : {(const void*)conv_stack16x2_kernel<0, false>, (const void*)conv_stack16x2_kernel<1, false>}) {
     e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kX2Lds);
+    if (e != hipSuccess) return e;
+  }
+  for (const void* k : {(const void*)conv_stack16x2_kernel<0, true>, (const void*)conv_stack16x2_kernel<1, true>}) {
+    e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kX2LdsHead);
     if (e != hipSuccess) return e;
   }
   for (const void* k : {(const void*)conv_tail_kernel<false>, (const void*)conv_tail_kernel<true>}) {
@@ -1740,14 +1823,22 @@ void launch_conv_body(const half_t* in, half_t* out, const void* w, const float*
 #undef V3
 }
 
+bool stack16_takes_head(int nbody, bool pairs) { return pairs && nbody >= 2 && (nbody & 1) == 0; }
+
 int launch_conv_stack16(half_t* a, half_t* b, const void* w, const float* bias, int nbody, const ConvShape& s,
-                        int act, int num_cus, int* done, int epoch, int* err, bool pairs, hipStream_t st) {
+                        int act, int num_cus, int* done, int epoch, int* err, bool pairs, hipStream_t st,
+                        const float* u32, int C, const void* head_w, const float* head_b) {
   const int grid = s.tiles < num_cus ? s.tiles : num_cus;
   const uint4* wp = (const uint4*)w;
-  if (pairs && nbody >= 2 && (nbody & 1) == 0) {   // two layers per hand-off
+  if (stack16_takes_head(nbody, pairs)) {           // two layers per hand-off
     const int np = nbody / 2;
-    (void)persistent_launch(act == 0 ? conv_stack16x2_kernel<0> : conv_stack16x2_kernel<1>, grid, 256, kX2Lds, st, a, b,
-                      wp, bias, np, s, done, epoch, err);
+    const uint4* hw = (const uint4*)head_w;
+    if (u32)                                         // the head computed in pair 0
+      (void)persistent_launch(act == 0 ? conv_stack16x2_kernel<0, true> : conv_stack16x2_kernel<1, true>, grid, 256,
+                              kX2LdsHead, st, a, b, wp, bias, np, s, done, epoch, err, u32, C, hw, head_b);
+    else
+      (void)persistent_launch(act == 0 ? conv_stack16x2_kernel<0, false> : conv_stack16x2_kernel<1, false>, grid, 256,
+                              kX2Lds, st, a, b, wp, bias, np, s, done, epoch, err, u32, C, hw, head_b);
     return np & 1;
   }
   (void)persistent_launch(act == 0 ? conv_stack16_kernel<0> : conv_stack16_kernel<1>, grid, 256, kStkLds, st, a, b, wp,

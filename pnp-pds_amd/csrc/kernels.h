@@ -41,9 +41,14 @@ void launch_conv_body_f2(const half_t* in, half_t* out, const void* w16_1, const
 // all nbody 64 -> 64 layers in one launch for small batches (grid = min(tiles, CUs)); returns
 // where the result is (0: a, 1: b).  pairs: two layers per hand-off (conv_stack16x2, even
 // nbody), else one.  done: s.tiles progress words (zeroed once), epoch: this launch's tag
-// (advance by >= nbody + 1 per launch); err: set on a stuck wait.
+// (advance by >= nbody + 1 per launch); err: set on a stuck wait.  u32 != nullptr (only where
+// stack16_takes_head): the head layer (fp32 NCHW u32 with C channels, head_w / head_b as for
+// launch_conv_head) is computed inside the launch and a is not read.
+bool stack16_takes_head(int nbody, bool pairs);
 int launch_conv_stack16(half_t* a, half_t* b, const void* w, const float* bias, int nbody, const ConvShape& s,
-                        int act, int num_cus, int* done, int epoch, int* err, bool pairs, hipStream_t st);
+                        int act, int num_cus, int* done, int epoch, int* err, bool pairs, hipStream_t st,
+                        const float* u32 = nullptr, int C = 0, const void* head_w = nullptr,
+                        const float* head_b = nullptr);
 // one 64 -> 64 layer with split weights W_hi + W_lo (PNP_PREC_FP16W2)
 void launch_conv_body_w2(const half_t* in, half_t* out, const void* w, const void* w_lo, const float* bias,
                          const ConvShape& s, int act, int num_cus, hipStream_t st);
