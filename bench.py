@@ -218,6 +218,19 @@ def host_cpu_info():
             "threads_used": usable}
 
 
+def cgroup_throttled_s():
+    """Seconds this cgroup has been throttled by its CPU quota (cgroup v2 cpu.stat), or None."""
+    try:
+        with open("/sys/fs/cgroup/cpu.stat") as f:
+            for line in f:
+                k, v = line.split()
+                if k == "throttled_usec":
+                    return int(v) / 1e6
+    except (OSError, ValueError):
+        pass
+    return None
+
+
 def cpu_baseline(cfg, x_true, x_obs, x_0, h, budget_s, max_iter):
     """Oracle restatement of test_iter (numpy FFT / mask, sort-based l1, torch-CPU conv) on
     image 0, with every CPU this process may use.  Returns (image-iters/s,
@@ -233,11 +246,15 @@ def cpu_baseline(cfg, x_true, x_obs, x_0, h, budget_s, max_iter):
     sq = (lambda a: a[0]) if C == 1 else (lambda a: a)          # gray: the reference's (H, W) arrays
     xo, x0, xt = sq(x_obs.astype(np.float64)), sq(x_0.astype(np.float64)), sq(x_true)
 
+    cpu_use = []                  # per run: process CPU seconds / (wall seconds x threads)
+
     def run(n, m1=cfg["m1"], m2=cfg["m2"]):
-        t = time.perf_counter()
+        t, c = time.perf_counter(), time.process_time()
         res = O.test_iter(x0, xo, xt, phi, adj, cfg["g1"], cfg["g2"], cfg["a_s"], cfg["a_n"], cfg["lam"], m1, m2,
                           0.1, cfg["sigma"], cfg["sp"], POISSON_ALPHA, den, n, cfg["method"], C, cfg["r"])
-        return time.perf_counter() - t, res
+        el = time.perf_counter() - t
+        cpu_use.append((time.process_time() - c) / max(el * torch.get_num_threads(), 1e-9))
+        return el, res
 
     if cfg["method"] == "comparisonB-2":
         # one outer iteration costs a + m1 tx + m2 ts; at 1024^2 (about 2 s per CPU denoiser pass)
@@ -259,12 +276,19 @@ def cpu_baseline(cfg, x_true, x_obs, x_0, h, budget_s, max_iter):
     run(1)                                                        # warm-up
     t1, _ = run(2)
     # three repeats of n iterations (the median is the value, the spread is reported): a
-    # 16-CPU cgroup on a shared host measured 4.1-9.5 image-iterations/s for one sample in r03
+    # 16-CPU cgroup on a shared host measured 4.1-9.5 image-iterations/s for one sample in r03,
+    # and 3.95 vs 12.9 for the same workload minutes apart on one box in r04 (cfg2 vs the metric
+    # line): the cgroup's quota throttling, recorded here with the process's CPU use
     n = int(min(max_iter, max(2, budget_s / 3 / (t1 / 2))))
     rates, res = [], None
+    thr0 = cgroup_throttled_s()
+    del cpu_use[:]
     for _ in range(3):
         el, res = run(n)
         rates.append(n / el)
+    thr1 = cgroup_throttled_s()
+    info["cpu_use_of_threads"] = [round(u, 3) for u in cpu_use]
+    info["cgroup_throttled_s"] = round(thr1 - thr0, 3) if thr0 is not None and thr1 is not None else None
     info["repeat_rates"] = [round(r_, 4) for r_ in rates]
     info["torch_threads"] = torch.get_num_threads()
     med = float(np.median(rates))
@@ -534,6 +558,10 @@ def main():
             line["cpu_baseline"] = {"value": round(rate, 4), "unit": "image-iterations/s",
                                     "cores": info["threads_used"], "kind": "port", "sample": sample,
                                     "repeat_rates": info.get("repeat_rates"), "spread": info.get("spread"),
+                                    # process CPU seconds / (wall x threads) per run, and the cgroup's
+                                    # quota-throttled seconds over the three repeats (CPU contention)
+                                    "cpu_use_of_threads": info.get("cpu_use_of_threads"),
+                                    "cgroup_throttled_s": info.get("cgroup_throttled_s"),
                                     "torch_threads": info.get("torch_threads", info["threads_used"]),
                                     "host": f"{info['threads_used']}-CPU share (cgroup quota "
                                             f"{info['cgroup_quota_cpus']}) of a {info['logical_cpus']}-CPU host",
