@@ -34,12 +34,18 @@ import argparse
 import json
 import os
 import platform
-import socket
 import subprocess
 import sys
 import time
 
-import numpy as np
+# The CPU baseline's torch-CPU convolutions run on an OpenMP pool: with the default (active)
+# wait policy its idle threads spin between parallel regions, which on the GPU box's 16-CPU
+# cgroup quota competes with the oracle's serial numpy phases and gets the process throttled
+# (r05: 1-4 s of throttling per 16-thread run, rates 3.7-6.3 at 4 threads).  Set before numpy /
+# torch load their OpenMP runtimes; an explicit setting in the environment wins.
+os.environ.setdefault("OMP_WAIT_POLICY", "PASSIVE")
+
+import numpy as np  # noqa: E402
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "pnp-pds_amd"))
@@ -231,117 +237,205 @@ def cgroup_throttled_s():
     return None
 
 
+def proc_threads():
+    """Threads of this process right now (/proc/self/status), or None."""
+    try:
+        with open("/proc/self/status") as f:
+            for line in f:
+                if line.startswith("Threads:"):
+                    return int(line.split()[1])
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def thread_sweep(usable):
+    """torch thread counts of the CPU leg's sweep: 4, 8, 12, 16 capped at the usable CPUs."""
+    ts = sorted({t for t in (4, 8, 12, 16) if t <= usable} | {usable})
+    return [t for t in ts if t >= 1]
+
+
 def cpu_baseline(cfg, x_true, x_obs, x_0, h, budget_s, max_iter):
     """Oracle restatement of test_iter (numpy FFT / mask, sort-based l1, torch-CPU conv) on
-    image 0, with every CPU this process may use.  Returns (image-iters/s,
-    sample description, PSNR track, threads)."""
+    image 0, on this host's CPUs, after the GPU work has drained (the timed
+    region is over and the device is idle, so the GPU process's runtime threads are asleep).
+    A thread sweep (4 / 8 / 12 / 16 torch threads, capped at the CPUs this process may use) with
+    two repeats each records, per repeat, the rate, the process's CPU use and the cgroup's
+    quota-throttled seconds.  Returns (best image-iters/s, sample description, PSNR track, info):
+    the best rate is the CPU's fair best case (r04 measured 4.05 to 12.9 for one workload on
+    16 threads in a 16-CPU quota, the throttled runs contending with the process's own runtime
+    threads); info carries the median, the sweep and the thread count at the best rate."""
     import torch
     from oracle import pnp_oracle as O
     from pnppds.weights import resolve_weights
     info = host_cpu_info()
-    torch.set_num_threads(info["threads_used"])
     C = cfg["C"]
     den = O.OracleDenoiser(resolve_weights(f"DnCNN_nobn_nch_{C}_nlev_0.01", C))
     phi, adj = O.observation_operators(cfg["op"], h, cfg["r"])
     sq = (lambda a: a[0]) if C == 1 else (lambda a: a)          # gray: the reference's (H, W) arrays
     xo, x0, xt = sq(x_obs.astype(np.float64)), sq(x_0.astype(np.float64)), sq(x_true)
+    scale = 1.0
+    if cfg["method"] == "comparisonB-2" and xo.shape[-1] > 256:
+        # one outer iteration at 1024^2 is 35 CPU denoiser passes of ~2 s each: timed instead on
+        # the 256^2 top-left crop at the config's m1 / m2 and scaled by pixels (the conv stack is
+        # linear in pixels; the FFT blur's N log N makes the scaled figure slightly optimistic)
+        scale = (xo.shape[-1] * xo.shape[-2]) / (256.0 * 256.0)
+        xo, x0, xt = xo[..., :256, :256], x0[..., :256, :256], xt[..., :256, :256]
 
-    cpu_use = []                  # per run: process CPU seconds / (wall seconds x threads)
-
-    def run(n, m1=cfg["m1"], m2=cfg["m2"]):
+    def run(n, threads):
+        torch.set_num_threads(threads)
+        thr0 = cgroup_throttled_s()
         t, c = time.perf_counter(), time.process_time()
-        res = O.test_iter(x0, xo, xt, phi, adj, cfg["g1"], cfg["g2"], cfg["a_s"], cfg["a_n"], cfg["lam"], m1, m2,
-                          0.1, cfg["sigma"], cfg["sp"], POISSON_ALPHA, den, n, cfg["method"], C, cfg["r"])
+        res = O.test_iter(x0, xo, xt, phi, adj, cfg["g1"], cfg["g2"], cfg["a_s"], cfg["a_n"], cfg["lam"], cfg["m1"],
+                          cfg["m2"], 0.1, cfg["sigma"], cfg["sp"], POISSON_ALPHA, den, n, cfg["method"], C, cfg["r"])
         el = time.perf_counter() - t
-        cpu_use.append((time.process_time() - c) / max(el * torch.get_num_threads(), 1e-9))
-        return el, res
+        thr1 = cgroup_throttled_s()
+        rec = {"threads": threads, "iters": n, "rate": round(n / (el * scale), 5),
+               "cpu_use_of_threads": round((time.process_time() - c) / max(el * threads, 1e-9), 3),
+               "throttled_s": round(thr1 - thr0, 3) if thr0 is not None and thr1 is not None else None}
+        return rec, res
 
-    if cfg["method"] == "comparisonB-2":
-        # one outer iteration costs a + m1 tx + m2 ts; at 1024^2 (about 2 s per CPU denoiser pass)
-        # m1 = 35 does not fit the budget, so tx / ts / a are timed at small m1, m2 and scaled.
-        t11, res = run(1, 1, 1)
-        t21, _ = run(1, 2, 1)
-        t12, _ = run(1, 1, 2)
-        tx, ts = max(t21 - t11, 0.0), max(t12 - t11, 0.0)
-        a_raw = t11 - tx - ts
-        a = max(a_raw, 0.0)
-        per = a + cfg["m1"] * tx + cfg["m2"] * ts
-        sample = (f"oracle comparisonB-2 on image 0: one outer iteration timed at (m1, m2) = (1, 1), (2, 1), (1, 2) "
-                  f"-> fixed {a:.2f} s (raw t11 - tx - ts = {a_raw:+.2f} s, clamped at 0: timing noise) + {tx:.2f} s "
-                  f"per x-step + {ts:.3f} s per s-step, scaled to m1={cfg['m1']}, m2={cfg['m2']}: {per:.1f} s per "
-                  f"outer iteration.  The reference itself is slower than this port: it builds a new Denoiser, "
-                  f"reloading the checkpoint, on every inner x-step (operators.py:81-83 via admm.py:35), which "
-                  f"the oracle does not")
-        return 1.0 / per, sample, None, info
-    run(1)                                                        # warm-up
-    t1, _ = run(2)
-    # three repeats of n iterations (the median is the value, the spread is reported): a
-    # 16-CPU cgroup on a shared host measured 4.1-9.5 image-iterations/s for one sample in r03,
-    # and 3.95 vs 12.9 for the same workload minutes apart on one box in r04 (cfg2 vs the metric
-    # line): the cgroup's quota throttling, recorded here with the process's CPU use
-    n = int(min(max_iter, max(2, budget_s / 3 / (t1 / 2))))
-    rates, res = [], None
-    thr0 = cgroup_throttled_s()
-    del cpu_use[:]
-    for _ in range(3):
-        el, res = run(n)
-        rates.append(n / el)
-    thr1 = cgroup_throttled_s()
-    info["cpu_use_of_threads"] = [round(u, 3) for u in cpu_use]
-    info["cgroup_throttled_s"] = round(thr1 - thr0, 3) if thr0 is not None and thr1 is not None else None
-    info["repeat_rates"] = [round(r_, 4) for r_ in rates]
-    info["torch_threads"] = torch.get_num_threads()
-    med = float(np.median(rates))
-    info["spread"] = round((max(rates) - min(rates)) / med, 3)
-    sample = (f"oracle test_iter ({cfg['method']}, {cfg['op']}) on image 0: 3 repeats of {n} iterations after a "
-              f"warm-up, wall clock, median (rates {info['repeat_rates']}, spread {info['spread']:.0%}); "
-              f"{info['torch_threads']} torch threads")
-    return med, sample, res[3], info
+    sweep = thread_sweep(info["threads_used"])
+    t_cal, _ = run(1, sweep[-1])                                   # warm-up and calibration
+    per_iter = max(t_cal["iters"] / (t_cal["rate"] * scale), 1e-3)
+    n = int(min(max_iter, max(1, budget_s / (2 * len(sweep)) / per_iter)))
+    recs, res = [], None
+    for threads in sweep:
+        for _ in range(2):
+            rec, res = run(n, threads)
+            recs.append(rec)
+    best = max(recs, key=lambda r_: r_["rate"])
+    at_best = [r_["rate"] for r_ in recs if r_["threads"] == best["threads"]]
+    rates = [r_["rate"] for r_ in recs]
+    info.update({"sweep": recs, "best_threads": best["threads"], "median": round(float(np.median(rates)), 5),
+                 "median_at_best_threads": round(float(np.median(at_best)), 5),
+                 "spread": round((max(rates) - min(rates)) / max(best["rate"], 1e-12), 3),
+                 "cgroup_throttled_s": round(sum(r_["throttled_s"] or 0.0 for r_ in recs), 3)
+                 if recs[0]["throttled_s"] is not None else None,
+                 "process_threads": proc_threads(), "torch_threads": best["threads"]})
+    what = (f"oracle {cfg['method']} ({cfg['op']}) on image 0" if scale == 1.0 else
+            f"oracle comparisonB-2 on the 256x256 crop of image 0 at m1={cfg['m1']}, m2={cfg['m2']}, scaled "
+            f"by pixels x{scale:g} to the config's image (one step = one outer iteration)")
+    sample = (f"{what}: {n} iterations per run, 2 runs at each of {sweep} torch threads after a warm-up, wall "
+              f"clock; value = the best run ({best['threads']} threads), median of all runs {info['median']:.4g}")
+    return best["rate"], sample, (res[3] if scale == 1.0 else None), info
 
 
 def launch_ranks(n, argv):
     """Start n ranks of this script (one per GPU, device = rank) and wait for them: the
     torch.distributed.run contract without the launcher.  Fresh processes, started before this
-    one touches the GPU (never an exec from a GPU process).  Returns the first non-zero exit
-    code (the other ranks are then terminated) or 0."""
-    with socket.socket() as sk:
-        sk.bind(("127.0.0.1", 0))
-        port = sk.getsockname()[1]
-    procs = []
-    for r in range(n):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
-    rc = 0
-    while procs:
-        for p in list(procs):
-            code = p.poll()
-            if code is None:
-                continue
-            procs.remove(p)
-            if code != 0 and rc == 0:
-                rc = code
-                log(f"rank pid {p.pid} exited with {code}; stopping the others")
-                for q in procs:
-                    q.terminate()
-        time.sleep(0.05)
+    one touches the GPU (never an exec from a GPU process).  The rendezvous store is created
+    here on an ephemeral port (TCPStore port 0: no probe-then-release race) and the ranks join
+    it as clients (init_dist).  Returns the first non-zero exit code (the other ranks are then
+    terminated) or 0; if this process is interrupted or fails while waiting, the ranks are
+    terminated and reaped before it exits."""
+    import datetime
+    import torch.distributed as dist
+    store = dist.TCPStore("127.0.0.1", 0, n + 1, True, timeout=datetime.timedelta(seconds=600),
+                          wait_for_workers=False)
+    procs, rc = [], 0
+    try:
+        for r in range(n):
+            env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                       GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(store.port),
+                       PNP_BENCH_STORE_PORT=str(store.port))
+            procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+        live = list(procs)
+        while live:
+            for p in list(live):
+                code = p.poll()
+                if code is None:
+                    continue
+                live.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code
+                    log(f"rank pid {p.pid} exited with {code}; stopping the others")
+                    for q in live:
+                        q.terminate()
+            time.sleep(0.05)
+    finally:
+        for p in procs:                  # interrupted or failed while waiting: no rank outlives us
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
     return rc
 
 
-def selftest_ranks():
+def init_dist(backend):
+    """Join the job's process group: through the store launch_ranks created (PNP_BENCH_STORE_PORT),
+    or env:// under torch.distributed.run."""
+    import datetime
+    import torch.distributed as dist
+    world, rank = int(os.environ["WORLD_SIZE"]), int(os.environ["RANK"])
+    port = os.environ.get("PNP_BENCH_STORE_PORT")
+    if port:
+        store = dist.TCPStore("127.0.0.1", int(port), world + 1, False, timeout=datetime.timedelta(seconds=600))
+        dist.init_process_group(backend, store=store, rank=rank, world_size=world)
+    else:
+        dist.init_process_group(backend, init_method="env://")
+
+
+DTYPES = {"fp16": "fp16-mfma/fp32-acc+state", "fp16w2": "fp16-mfma(split fp16 hi+lo weights)/fp32-acc+state",
+          "fp16x3": "fp16-mfma(split fp16 hi+lo activations and weights, 3 MFMAs)/fp32-acc+state",
+          "fp16a2": "fp16-mfma(split fp16 hi+lo activations, fp16 weights, 2 MFMAs)/fp32-acc+state",
+          "fp32": "fp32-mfma/fp32-state",
+          "converge": "fp16-mfma (auto's fp16 operands, then split fp16 hi+lo activations with fp16 weights, "
+                      "fp16a2, once c_n < 3e-3)/fp32-acc+state"}
+DTYPES_SHORT = {"fp16": "fp16", "fp16w2": "fp16w2"}
+
+
+def base_line(cfg, config_name, world, K, Wm, t_el, precision, prec_req):
+    """The contract fields of the JSON line: ``value`` = image-iterations/s of the whole job
+    (cfg['B'] images per rank x world ranks x K steps / the slowest rank's time), weak scaling."""
+    B, C, H, W = cfg["B"], cfg["C"], cfg["S"], cfg["S"]
+    is_metric = cfg["op"] == "blur" and cfg["method"] == "A-Proposed" and B == 256 and C == 3 and H == 256
+    metric = METRIC if is_metric else \
+        f"PDS iters/sec ({config_name}: {cfg['method']} {cfg['op']}, {B} x {C}x{H}x{W} per GPU); PSNR Δ vs ref"
+    arch = f"DnCNN_nobn_nch_{C}_nlev_0.01"
+    return {
+        "metric": metric, "value": round(B * world * K / t_el, 2), "unit": "image-iterations/s",
+        "n_gpus": world, "steps": K, "warmup": Wm,
+        "ms_per_step": round(1e3 * t_el / K, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": DTYPES[precision],
+        "data": f"synthetic structured images, x_obs from the device observation pipeline (main.py:49-64: "
+                f"{cfg['op']}, sigma={cfg['sigma']}, sp={cfg['sp']}, poisson={cfg['poisson']}, "
+                f"np.random.seed(1234) streams); real {arch} weights",
+        "config": {"workload": cfg["desc"].format(B=B, S=H), "config": config_name, "global_batch": B * world,
+                   "image": f"{C}x{H}x{W}", "deg_op": "blur_1" if cfg["op"] == "blur" else cfg["op"],
+                   "method": cfg["method"], "precision": precision, "precision_requested": prec_req,
+                   "parallelism": f"dp{world} (independent image shards, no collective)"},
+        "batch_iters_per_s": round(K / t_el, 3),
+    }
+
+
+def selftest_ranks(args):
     """CPU rehearsal of the rank plumbing (tests/test_bench_launch.py): gloo barrier and
-    max-over-ranks on the ranks launch_ranks started; rank 0 prints one JSON line."""
+    max-over-ranks on the ranks launch_ranks started, rank r taking 0.01 (r + 1) s per "step";
+    rank 0 prints the contract line (base_line) built as the GPU path builds it.  With
+    --selftest-fail-rank R, rank R exits with status 3 before the first barrier (the others
+    then wait there until launch_ranks stops them)."""
     import torch.distributed as dist
     sys.path.insert(0, os.path.join(REPO, "pnp-pds_amd"))
     from pnppds.shard import max_over_ranks
     world, rank = int(os.environ["WORLD_SIZE"]), int(os.environ["RANK"])
-    dist.init_process_group("gloo", init_method="env://")
+    if rank == args.selftest_fail_rank:
+        log(f"[rank {rank}] selftest: failing on purpose")
+        return 3
+    init_dist("gloo")
     dist.barrier()
-    t = max_over_ranks(0.01 * (rank + 1))
+    t = max_over_ranks(0.01 * (rank + 1) * args.steps)
     dist.barrier()
     if rank == 0:
-        print(json.dumps({"n_gpus": world, "ranks_local": [int(os.environ["LOCAL_RANK"])], "max_t": t,
-                          "value": 256 * world / t}), flush=True)
+        cfg = dict(CONFIGS[args.config])
+        line = base_line(cfg, args.config, world, args.steps, args.warmup, t, "fp16", "auto")
+        line.update({"ranks_local": [int(os.environ["LOCAL_RANK"])], "max_t": t})
+        print(json.dumps(line), flush=True)
     dist.destroy_process_group()
 
 
@@ -355,11 +449,15 @@ def main():
     ap.add_argument("--size", type=int, default=0, help="image side (0 = the config's)")
     ap.add_argument("--op", default="", choices=["", "blur", "Id", "random_sampling"],
                     help="override the config's degradation operator (profiling the elementwise K1/K2)")
-    ap.add_argument("--precision", default="auto", choices=["auto", "fp16", "fp16w2", "fp16x3", "fp32"],
+    ap.add_argument("--precision", default="auto",
+                    choices=["auto", "fp16", "fp16w2", "fp16x3", "fp16a2", "fp32", "converge"],
                     help="denoiser operands: auto = the library's per-solve policy (PNP_PREC_AUTO: on blur, fp16 "
                          "up to sigma 0.01 for ours-A/B, comparisonB-2, PnP-FBS, RED, and fp16w2 above it "
                          "for ours-A and comparisonB-2; split fp16 'fp16x3' otherwise)")
-    ap.add_argument("--cpu-budget", type=float, default=15.0, help="seconds of CPU-baseline work")
+    ap.add_argument("--full-run", action="store_true",
+                    help="time one whole solve of --steps iterations from iteration 0 (state reloaded after the "
+                         "warm-up): with --precision converge, the experiments' 1200-iteration run")
+    ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of CPU-baseline work")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile", type=int, default=1, help="HIP-event per-kernel timing in the timed region")
     ap.add_argument("--chunk", type=int, default=0, help="images per denoiser pass (0 = auto)")
@@ -369,7 +467,11 @@ def main():
                     help="body layers per launch on the fp16 path (0 = the library default)")
     ap.add_argument("--ablate", type=int, default=0,
                     help="profiling build only (PNP_LIB_PATH=lib_prof/...; results wrong): 1 DMA, 2 stores, 4 MFMA")
+    ap.add_argument("--ablate-k2", type=int, default=0,
+                    help="profiling build only (results wrong): blur K2 phases removed (1 stencil, 2 fp64 partials, "
+                         "4 stores, 8 fill, 16 epilogue loads)")
     ap.add_argument("--selftest-ranks", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--selftest-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.gpus < 1:
         raise SystemExit("--gpus must be >= 1")
@@ -379,7 +481,7 @@ def main():
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={os.environ.get('WORLD_SIZE')} "
                          f"(one rank per GPU: they must agree)")
     if args.selftest_ranks:
-        return selftest_ranks()
+        return selftest_ranks(args)
 
     cfg = dict(CONFIGS[args.config])
     if args.batch:
@@ -401,7 +503,7 @@ def main():
     backend = "gloo" if rehearsal else "nccl"
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group(backend, init_method="env://")
+        init_dist(backend)
     from pnppds import _lib
     from pnppds.iteration import make_params, resolve_method, resolve_precision
     from pnppds.operators import load_blur_kernel, sampling_keep_mask
@@ -437,16 +539,24 @@ def main():
     torch.cuda.synchronize()
     log(f"[rank {rank}] inputs ready in {time.perf_counter() - t0:.1f}s")
 
-    cap = Wm + K
+    # --full-run: the timed K steps are a whole solve from iteration 0 (state reloaded after the
+    # warm-up, which only allocates and warms the buffers), e.g. precision='converge' over the
+    # experiments' 1200 iterations: its fp16 opening and split-fp16 rest, as a solve runs them
+    cap = max(Wm, K) if args.full_run else Wm + K
     prm = make_params(cfg["g1"], cfg["g2"], cfg["a_s"], cfg["a_n"], cfg["lam"], cfg["m1"], cfg["m2"], 0.1,
                       cfg["sigma"], cfg["sp"], POISSON_ALPHA, cfg["r"], True)
     ctx.set_denoise_chunk(args.chunk)
     ctx.solver_setup(resolve_method(cfg["method"]), prm, B, C, H, W, cap)
     prec_req, args.precision = ctx.get_precision()      # what 'auto' resolves to for this solve
+    prec_fast = args.precision
     ctx.solver_load_device(d_x0.data_ptr(), d_obs.data_ptr(), d_true.data_ptr())   # x_0 (main.py:62-64)
     if args.ablate:
         ctx.set_ablate(args.ablate)
+    if args.ablate_k2:
+        ctx.set_ablate_k2(args.ablate_k2)
     ctx.solver_iterate(Wm)
+    if args.full_run:
+        ctx.solver_load_device(d_x0.data_ptr(), d_obs.data_ptr(), d_true.data_ptr())
     ctx.synchronize()
     torch.cuda.synchronize()
 
@@ -466,43 +576,35 @@ def main():
         t_el = max_over_ranks(t_el, device=None if rehearsal else f"cuda:{local}")   # job time = slowest rank
     prof = ctx.profile_read() if args.profile else {}
     x_out, s_out, c_hist, psnr_hist, ssim_hist = ctx.solver_fetch()
+    switch_it = ctx.get_precision_switch()
+    if prec_req == "converge":       # the line names the mode; the roofline the body kernel it ended on
+        body_prec = ctx.get_precision()[1]
+        args.precision = "converge"
+    else:
+        body_prec = args.precision
+    last = (K if args.full_run else Wm + K) - 1
 
-    value = B * world * K / t_el
     if rank == 0:
-        is_metric = (cfg["op"] == "blur" and cfg["method"] == "A-Proposed" and B == 256 and C == 3 and H == 256
-                     and W == 256)
-        metric = METRIC if is_metric else \
-            f"PDS iters/sec ({args.config}: {cfg['method']} {cfg['op']}, {B} x {C}x{H}x{W} per GPU); PSNR Δ vs ref"
-        line = {
-            "metric": metric, "value": round(value, 2), "unit": "image-iterations/s",
-            "n_gpus": world, "steps": K, "warmup": Wm,
-            "ms_per_step": round(1e3 * t_el / K, 3), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": {"fp16": "fp16-mfma/fp32-acc+state", "fp16w2": "fp16-mfma(split fp16 hi+lo weights)/fp32-acc+state",
-                      "fp16x3": "fp16-mfma(split fp16 hi+lo activations and weights, 3 MFMAs)/fp32-acc+state",
-                      "fp32": "fp32-mfma/fp32-state"}[args.precision],
-            "data": f"synthetic structured images, x_obs from the device observation pipeline (main.py:49-64: "
-                    f"{cfg['op']}, sigma={cfg['sigma']}, sp={cfg['sp']}, poisson={cfg['poisson']}, "
-                    f"np.random.seed(1234) streams); real {arch} weights",
-            "config": {"workload": cfg["desc"].format(B=B, S=H), "config": args.config, "global_batch": B * world,
-                       "image": f"{C}x{H}x{W}", "deg_op": "blur_1" if cfg["op"] == "blur" else cfg["op"],
-                       "method": cfg["method"], "precision": args.precision, "precision_requested": prec_req,
-                       "parallelism": f"dp{world} (independent image shards, no collective)"},
-            "batch_iters_per_s": round(K / t_el, 3),
-            "build_id": _lib.build_id(),
-        }
+        line = base_line(cfg, args.config, world, K, Wm, t_el, args.precision, prec_req)
+        line["build_id"] = _lib.build_id()
+        if args.full_run:
+            line["full_run"] = f"the {K} timed steps are one solve from iteration 0 (state reloaded after the warm-up)"
+        if prec_req == "converge":
+            line["precision_switch_iteration"] = switch_it
+            line["config"]["precision"] = (f"converge: {DTYPES_SHORT.get(prec_fast, prec_fast)} until iteration "
+                                           f"{switch_it}, then {body_prec}")
         if prof:
             kt = {k: round(v[0], 4) for k, v in prof.items()}
             line["kernel_ms"] = kt
             line["kernel_calls_per_step"] = {k: round(v[1] / K, 2) for k, v in prof.items()}
-            fp32 = args.precision == "fp32"
-            kname = {"fp32": "conv32_body", "fp16w2": "conv_body_w2", "fp16x3": "conv_body_s3"}.get(args.precision,
-                                                                                                  "conv_body")
+            fp32 = body_prec == "fp32"
+            kname = {"fp32": "conv32_body", "fp16w2": "conv_body_w2", "fp16x3": "conv_body_s3",
+                     "fp16a2": "conv_body_a2"}.get(body_prec, "conv_body")
             if kname == "conv_body" and "conv_body_f2" in prof:
                 kname = "conv_body_f2"
             if kname in prof:
                 body_ms = prof[kname][0]
-                m = images_per_launch(B, H, W, args.chunk, fp32, args.precision == "fp16x3")
+                m = images_per_launch(B, H, W, args.chunk, fp32, body_prec in ("fp16x3", "fp16a2"))
                 fl = conv_flops_per_launch(m, H, W)
                 by = conv_bytes_per_launch(m, H, W, 4 if fp32 else 2)
                 gbs = by / (body_ms * 1e-3) / 1e9
@@ -513,16 +615,19 @@ def main():
                                         "achieved": round(tfl, 2), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                                         "frac": round(tfl / FP32_PEAK_TFLOPS, 4), "traffic": None,
                                         "bytes_per_launch": by, "flops_per_launch": fl, "hbm_gbs": round(gbs, 1)}
-                elif args.precision == "fp16x3":   # 3 MFMAs per product on hi + lo activations: MFMA roof
+                elif body_prec in ("fp16x3", "fp16a2"):   # 3 (2) MFMAs per product on hi + lo activations
+                    nm = 3 if body_prec == "fp16x3" else 2
                     by = 2 * by                    # hi + lo images read and written
                     gbs = by / (body_ms * 1e-3) / 1e9
-                    line["roofline"] = {"kernel": "conv_body_s3 (64->64 3x3, split fp16: 3 fp16 MFMAs per product)",
-                                        "bound": "mfma", "achieved": round(3 * tfl, 1), "peak": FP16_PEAK_TFLOPS,
-                                        "unit": "TFLOP/s (MFMA work, 3x algorithmic)",
-                                        "frac": round(3 * tfl / FP16_PEAK_TFLOPS, 4), "traffic": None,
+                    what = ("split fp16: 3 fp16 MFMAs per product" if nm == 3 else
+                            "split fp16 activations, fp16 weights: 2 fp16 MFMAs per product")
+                    line["roofline"] = {"kernel": f"{kname} (64->64 3x3, {what})",
+                                        "bound": "mfma", "achieved": round(nm * tfl, 1), "peak": FP16_PEAK_TFLOPS,
+                                        "unit": f"TFLOP/s (MFMA work, {nm}x algorithmic)",
+                                        "frac": round(nm * tfl / FP16_PEAK_TFLOPS, 4), "traffic": None,
                                         "bytes_per_launch": by, "flops_per_launch": fl, "hbm_gbs": round(gbs, 1),
                                         "algorithmic_tflops": round(tfl, 1)}
-                elif args.precision == "fp16w2":   # 2 MFMAs per product: 576 MFMA-FLOP/B, MFMA roof
+                elif body_prec == "fp16w2":   # 2 MFMAs per product: 576 MFMA-FLOP/B, MFMA roof
                     line["roofline"] = {"kernel": "conv_body_w2 (64->64 3x3, fp16 MFMA, split hi+lo weights)",
                                         "bound": "mfma", "achieved": round(2 * tfl, 1), "peak": FP16_PEAK_TFLOPS,
                                         "unit": "TFLOP/s (MFMA work, 2x algorithmic)",
@@ -550,19 +655,21 @@ def main():
                                     "frac": round(pb[k] / (prof[k][0] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                                     "frac_of_copy": round(pb[k] / (prof[k][0] * 1e-3) / 1e9 / copy_gbs, 4)}
                                 for k in pb if k in prof}
-        line["psnr_img0_db"] = [round(float(psnr_hist[0, 0]), 4), round(float(psnr_hist[0, cap - 1]), 4)]
-        line["ssim_img0"] = [round(float(ssim_hist[0, 0]), 5), round(float(ssim_hist[0, cap - 1]), 5)]
+        line["psnr_img0_db"] = [round(float(psnr_hist[0, 0]), 4), round(float(psnr_hist[0, last]), 4)]
+        line["ssim_img0"] = [round(float(ssim_hist[0, 0]), 5), round(float(ssim_hist[0, last]), 5)]
+        if prec_req == "converge" or args.full_run:
+            line["c_img0"] = [float(c_hist[0, 0]), float(c_hist[0, last])]
         if world == 1 and not args.no_cpu_baseline:
             rate, sample, ps_cpu, info = cpu_baseline(cfg, x_true[0:1][0], d_obs[0].cpu().numpy(),
                                                       d_x0[0].cpu().numpy(), h, args.cpu_budget, cap)
             line["cpu_baseline"] = {"value": round(rate, 4), "unit": "image-iterations/s",
-                                    "cores": info["threads_used"], "kind": "port", "sample": sample,
-                                    "repeat_rates": info.get("repeat_rates"), "spread": info.get("spread"),
-                                    # process CPU seconds / (wall x threads) per run, and the cgroup's
-                                    # quota-throttled seconds over the three repeats (CPU contention)
-                                    "cpu_use_of_threads": info.get("cpu_use_of_threads"),
-                                    "cgroup_throttled_s": info.get("cgroup_throttled_s"),
-                                    "torch_threads": info.get("torch_threads", info["threads_used"]),
+                                    "cores": info["best_threads"], "kind": "port", "sample": sample,
+                                    "median": info["median"], "median_at_best_threads": info["median_at_best_threads"],
+                                    "best_threads": info["best_threads"], "spread": info["spread"],
+                                    # per run: threads, rate, process CPU seconds / (wall x threads) and the
+                                    # cgroup's quota-throttled seconds (CPU contention)
+                                    "sweep": info["sweep"], "cgroup_throttled_s": info["cgroup_throttled_s"],
+                                    "process_threads": info["process_threads"],
                                     "host": f"{info['threads_used']}-CPU share (cgroup quota "
                                             f"{info['cgroup_quota_cpus']}) of a {info['logical_cpus']}-CPU host",
                                     "cpu_model": info["model"], "logical_cpus": info["logical_cpus"],

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define PNP_ABI_VERSION 6
+#define PNP_ABI_VERSION 7
 
 typedef struct pnp_ctx pnp_ctx;
 
@@ -90,12 +90,32 @@ enum pnp_precision {
                         three fp16 MFMAs per product (hi*hi + hi*lo + lo*hi), fp32
                         accumulation: near-fp32 results at 1/3 of the fp16 MFMA rate
                         (ABI 4)                                                      */
-  PNP_PREC_AUTO = 4   /* default (ABI 4): per solve, on the blur operator: FP16 for
+  PNP_PREC_AUTO = 4,  /* default (ABI 4): per solve, on the blur operator: FP16 for
                         A/B-Proposed, comparisonB-2, A-PnPFBS-DnCNN and A-RED-DnCNN up
-                        to gaussian_nl = 0.01; above it FP16W2 for A-Proposed and
-                        comparisonB-2 (each measured within 0.005 dB of the reference
-                        over its experiments' lengths); FP16X3 otherwise; single
-                        denoiser calls (pnp_op_denoise) run FP16X3                   */
+                        to gaussian_nl = 0.01; above it FP16W2 for A-Proposed (measured
+                        within 0.0005 dB of the reference over 1200 iterations at sigma
+                        0.02 / 0.04) and comparisonB-2 (0.0002 dB over 30 outer
+                        iterations at sigma 0.04); FP16X3 otherwise; single denoiser
+                        calls (pnp_op_denoise) run FP16X3.
+                        Where it runs FP16 or FP16W2, x and PSNR follow the reference
+                        (<= 0.0035 dB) but c_n (iteration.py:187) does not below ~3e-4:
+                        the fp16 activations' rounding sets a floor where successive
+                        iterates stop contracting (the reference's c_n reaches ~7e-8).
+                        Use PNP_PREC_CONVERGE where the c_n curve matters.            */
+  PNP_PREC_CONVERGE = 5, /* (ABI 7) per solve: AUTO's operands while the batch's smallest
+                        c_n is above a threshold (PNP_TUNE_CONVERGE_C, default 3e-3, ten
+                        times the fp16 floor), then split activations for the rest of the
+                        solve: FP16A2 where AUTO runs FP16 / FP16W2, FP16X3 elsewhere (where
+                        AUTO already runs it), so c_n follows the reference's down to ~1e-6
+                        (within 1-2 %; ~1.6e-7 floor).  Needs the metrics (record_metrics,
+                        within metrics_capacity) to watch c_n; without them it switches at
+                        once.  The switch is decided on the host one iteration behind the
+                        device (pnp_solver_iterate then blocks per iteration until it
+                        switches) and is per batch: see pnp_get_precision_switch.  Single
+                        denoiser calls run FP16X3.                                      */
+  PNP_PREC_FP16A2 = 6   /* (ABI 7) activations split into fp16 hi + lo halves, single fp16
+                        weights (rounded per filter as FP16's): two fp16 MFMAs per product in
+                        the 64->64 layers (hi*w + lo*w); head and tail as FP16X3           */
 };
 
 /* Scalar parameters of iteration.test_iter (iteration.py:10), same names/meaning. */
@@ -135,8 +155,12 @@ int pnp_set_denoiser(pnp_ctx* ctx, int channels, int depth, int width, const flo
  * pnp_get_precision: the requested value and the one the next solver step will use.   */
 int pnp_set_precision(pnp_ctx* ctx, int precision);
 int pnp_get_precision(pnp_ctx* ctx, int* requested, int* effective);
+/* (ABI 7) PNP_PREC_CONVERGE: the first iteration of the current solve that ran split
+ * activations (FP16A2 / FP16X3), or -1 when it has not switched (or the solve does not run
+ * PNP_PREC_CONVERGE).                                                                       */
+int pnp_get_precision_switch(pnp_ctx* ctx, int* iteration);
 
-/* Performance knobs (no effect on results).
+/* Performance knobs (no effect on results; PNP_TUNE_CONVERGE_C excepted).
  * PNP_TUNE_DENOISE_CHUNK: images per denoiser pass (0 = auto: the whole batch, unless its
  * activation ping-pong pair would exceed an eighth of the device's memory; then equal passes). */
 enum pnp_tuning_key {
@@ -148,9 +172,12 @@ enum pnp_tuning_key {
                                 intermediate stays in LDS), 3 (all: conv_stack16x2, two layers
                                 per tile hand-off when their number is even) or 4 (all:
                                 conv_stack16, one layer per hand-off).  Bit-identical results. */
-  PNP_TUNE_GRAPH = 3          /* 1: iteration launches replayed from a hipGraph (two iterations
+  PNP_TUNE_GRAPH = 3,         /* 1: iteration launches replayed from a hipGraph (two iterations
                                 per replay, methods A/B/C); 0: direct launches (default).
                                 Same results either way.                                       */
+  PNP_TUNE_CONVERGE_C = 4     /* (ABI 7) PNP_PREC_CONVERGE's c_n threshold in units of 1e-6
+                                (default 3000 = 3e-3).  Changes when the solve switches, so it
+                                changes results (within the tolerances of DESIGN.md §4).        */
 };
 int pnp_set_tuning(pnp_ctx* ctx, int key, int value);
 
@@ -205,9 +232,10 @@ int pnp_op_proj_l1_ball(pnp_ctx* ctx, const float* x, float* out, int B, int64_t
 int pnp_op_prox_gkl(pnp_ctx* ctx, const float* x, const float* x0, float* out, int64_t count,
                     double gamma, double alpha, void* stream);
 int pnp_op_denoise(pnp_ctx* ctx, const float* x, float* out, int B, int C, int H, int W, void* stream);
-/* (ABI 5) Synchronizes `stream` (NULL: the context's) and reports whether a single-op
- * denoiser call's persistent small-batch launch failed (PNP_E_INTERNAL: its results are
- * invalid).  The solver's own launches are checked by pnp_solver_fetch.               */
+/* (ABI 5) Synchronizes `stream` and the context's own stream (the persistent small-batch
+ * launches run there whatever stream a single op is given) and reports whether a single-op
+ * denoiser call's persistent launch failed (PNP_E_INTERNAL: its results are invalid).  The
+ * solver's own launches are checked by pnp_solver_fetch.                               */
 int pnp_op_status(pnp_ctx* ctx, void* stream);
 /* (ABI 5, host only, no device) The fp16 values the fp16 operand precisions store for conv
  * weights: n_filters 3x3 filters (9 floats each, [c_out][c_in][3][3] order) rounded to fp16

@@ -260,18 +260,22 @@ class OracleDenoiser:
     fp16 values from ``fp16_filter_round`` (fp32 accumulation, fp16 storage of hidden
     activations) — the device numerics of PNP_PREC_FP16.  ``emulate_fp16="w2"``: activations
     rounded to fp16, weights as the sum of that fp16 high half and the fp16 rounding of the
-    remainder (PNP_PREC_FP16W2).
+    remainder (PNP_PREC_FP16W2).  ``emulate_fp16="a2"``: activations kept (the device's hi + lo
+    pairs carry ~21 bits), the 64 -> 64 layers' weights at their fp16 values, head and tail
+    exact (PNP_PREC_FP16A2).
     """
 
     def __init__(self, weights, emulate_fp16=False):
         self.w = weights
-        self.emulate_fp16 = bool(emulate_fp16)
+        self.emulate_fp16 = emulate_fp16 in (True, "w2")      # fp16 activations
         self.tw = [torch.from_numpy(np.ascontiguousarray(a, np.float32)) for a in weights.weights]
         self.tb = [torch.from_numpy(np.ascontiguousarray(b, np.float32)) for b in weights.biases]
         if emulate_fp16:                     # the device's fp16 weights (fp16_filter_round)
             hi = [torch.from_numpy(fp16_filter_round(t.numpy())) for t in self.tw]
             if emulate_fp16 == "w2":          # + the fp16 rounding of the remainder
                 self.tw = [a + (t - a).half().float() for a, t in zip(hi, self.tw)]
+            elif emulate_fp16 == "a2":        # fp16 body weights only
+                self.tw = [hi[i] if 0 < i < len(hi) - 1 else t for i, t in enumerate(self.tw)]
             else:
                 self.tw = hi
 

@@ -124,7 +124,13 @@ __device__ __forceinline__ void s3_split(float a, float b, h4_t& hi, h4_t& lo, i
   lo[i] = (half_t)(v - (float)h);
 }
 
-template <int MODE, int ACT>
+// WLO = 0 (fp16a2, body only): the a_hi w_lo term is dropped, two MFMAs per product on split
+// activations and single fp16 weights (pnp_set_denoiser's filter-sum rounding).  Without the
+// w_lo registers a wave holds two M-subtiles (32 output channels) of two tile rows instead of one
+// M-subtile of four: a B fragment then feeds two MFMAs, so the LDS reads per K-step and CU halve
+// (with one M-subtile per wave the 8 reads of 8 MFMAs per wave fill the LDS array's 256 B/clk
+// exactly: r05 measured 2.59 ms per layer at the metric against fp16x3's 3.17, not 2/3 of it).
+template <int MODE, int ACT, int WLO = 1>
 __global__ __launch_bounds__(512, 1) void conv_s3_kernel(const half_t* __restrict__ in_hi,
                                                           const half_t* __restrict__ in_lo,
                                                           half_t* __restrict__ out_hi, half_t* __restrict__ out_lo,
@@ -135,27 +141,33 @@ __global__ __launch_bounds__(512, 1) void conv_s3_kernel(const half_t* __restric
                                                           ConvShape s, S3Geom g, int C, int residual_sign,
                                                           int clamp_out) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  constexpr int NT = MODE == 0 ? 4 : 1;                 // N-subtiles (tile rows) per wave
-  constexpr int NM = MODE == 0 ? 4 : 1;                 // 16-row M-tiles
+  constexpr bool A2 = MODE == 0 && !WLO;
+  constexpr int NT = MODE == 0 ? (A2 ? 2 : 4) : 1;      // N-subtiles (tile rows) per wave
+  constexpr int MW = A2 ? 2 : 1;                        // 16-row M-subtiles per wave
+  constexpr int NM = MODE == 0 ? 4 : 1;                 // 16-row M-tiles of the layer
+  constexpr int NWL = WLO ? kS3KSteps : 1;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int mt = MODE == 0 ? (wave & 3) : 0;
-  const int row0 = MODE == 0 ? 4 * (wave >> 2) : wave;
+  const int mt0 = MODE == 0 ? (A2 ? 2 * (wave & 1) : (wave & 3)) : 0;
+  const int row0 = MODE == 0 ? (A2 ? 2 * (wave >> 1) : 4 * (wave >> 2)) : wave;
   const int px = lane & 15, grp = lane >> 4;
 
-  half8_t wH[kS3KSteps], wL[kS3KSteps];
+  half8_t wH[MW][kS3KSteps], wL[NWL];
 #pragma unroll
   for (int ks = 0; ks < kS3KSteps; ++ks) {
-    const size_t o = ((size_t)(ks * NM + mt) * 64 + lane);
-    wH[ks] = __builtin_bit_cast(half8_t, w_hi[o]);
-    wL[ks] = __builtin_bit_cast(half8_t, w_lo[o]);
-  }
-  float bl[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int co = MODE == 0 ? 16 * mt + 4 * grp + i : i;
-    bl[i] = (MODE == 0 || co < C) ? bias[co] : 0.f;
+    for (int m = 0; m < MW; ++m)
+      wH[m][ks] = __builtin_bit_cast(half8_t, w_hi[(size_t)(ks * NM + mt0 + m) * 64 + lane]);
+    if (WLO) wL[ks % NWL] = __builtin_bit_cast(half8_t, w_lo[(size_t)(ks * NM + mt0) * 64 + lane]);
   }
+  float bl[MW][4];
+#pragma unroll
+  for (int m = 0; m < MW; ++m)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int co = MODE == 0 ? 16 * (mt0 + m) + 4 * grp + i : i;
+      bl[m][i] = (MODE == 0 || co < C) ? bias[co] : 0.f;
+    }
 
   // DMA: piece q = 8 j + wave (j < 6) covers half q / 24 (hi, lo), pixels 8 (q % 24) .. +7 (pixels
   // past 179 re-read pixel 179 into the padding slots)
@@ -233,9 +245,9 @@ __global__ __launch_bounds__(512, 1) void conv_s3_kernel(const half_t* __restric
       return *reinterpret_cast<const half8_t*>(fb + lofs[dx][ks & 1] + lo * kS3Half + (n + dy) * kS3HaloW * 128);
     };
     // B fragments are read PD K-steps ahead (the body's 12 MFMAs per K-step cover one step of LDS
-    // latency; the tail's 3 do not); per K-step the next reads are interleaved one per MFMA.
+    // latency; the tail's 3 do not); per K-step the next reads are interleaved with the MFMAs.
     constexpr int PD = MODE == 0 ? 1 : 3;
-    floatx4 acc[NT];
+    floatx4 acc[MW][NT];
     half8_t bh[PD + 1][NT], bo[PD + 1][NT];
 #pragma unroll
     for (int d = 0; d < PD; ++d)
@@ -256,46 +268,59 @@ __global__ __launch_bounds__(512, 1) void conv_s3_kernel(const half_t* __restric
         }
       }
 #pragma unroll
-      for (int n = 0; n < NT; ++n)
-        acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wH[ks], bh[r][n], ks == 0 ? s3_c0<MODE>(bl) : acc[n], 0, 0, 0);
+      for (int m = 0; m < MW; ++m)
 #pragma unroll
-      for (int n = 0; n < NT; ++n) acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wL[ks], bh[r][n], acc[n], 0, 0, 0);
+        for (int n = 0; n < NT; ++n)
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wH[m][ks], bh[r][n],
+                                                             ks == 0 ? s3_c0<MODE>(bl[m]) : acc[m][n], 0, 0, 0);
+      if (WLO) {
 #pragma unroll
-      for (int n = 0; n < NT; ++n) acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wH[ks], bo[r][n], acc[n], 0, 0, 0);
+        for (int n = 0; n < NT; ++n)
+          acc[0][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wL[ks % NWL], bh[r][n], acc[0][n], 0, 0, 0);
+      }
+#pragma unroll
+      for (int m = 0; m < MW; ++m)
+#pragma unroll
+        for (int n = 0; n < NT; ++n)
+          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wH[m][ks], bo[r][n], acc[m][n], 0, 0, 0);
       if (ks + PD < kS3KSteps) {
+        // fp16x3: one LDS read per MFMA, then NT MFMAs; fp16a2: one read per two MFMAs
 #pragma unroll
-        for (int i = 0; i < 2 * NT; ++i) {         // one LDS read, one MFMA
+        for (int i = 0; i < 2 * NT; ++i) {
           __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, MW, 0);
         }
-        __builtin_amdgcn_sched_group_barrier(0x008, NT, 0);
+        if (WLO) __builtin_amdgcn_sched_group_barrier(0x008, NT, 0);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
     if constexpr (MODE == 0) {
 #pragma unroll
-      for (int n = 0; n < NT; ++n) {
-        const int y = ty0 + row0 + n;
-        h4_t hi, lo;
+      for (int m = 0; m < MW; ++m)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) s3_split<ACT>(acc[n][i], bl[i], hi, lo, i);
-        const size_t rowb = (((size_t)b * s.Hp + y + s.pad) * s.Wp + tx0 + s.pad) * kWidth;
-        const int nrec = y < s.H ? min(kS3TileW, s.W - tx0) * 128 : 0;
-        const unsigned off = (unsigned)(px * 128 + (16 * mt + 4 * grp) * 2);
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2i_t, hi),
-                                              __builtin_amdgcn_make_buffer_rsrc(out_hi + rowb, (short)0, nrec, 0x00020000),
-                                              off, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2i_t, lo),
-                                              __builtin_amdgcn_make_buffer_rsrc(out_lo + rowb, (short)0, nrec, 0x00020000),
-                                              off, 0, 0);
-      }
+        for (int n = 0; n < NT; ++n) {
+          const int y = ty0 + row0 + n;
+          h4_t hi, lo;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) s3_split<ACT>(acc[m][n][i], bl[m][i], hi, lo, i);
+          const size_t rowb = (((size_t)b * s.Hp + y + s.pad) * s.Wp + tx0 + s.pad) * kWidth;
+          const int nrec = y < s.H ? min(kS3TileW, s.W - tx0) * 128 : 0;
+          const unsigned off = (unsigned)(px * 128 + (16 * (mt0 + m) + 4 * grp) * 2);
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2i_t, hi),
+                                                __builtin_amdgcn_make_buffer_rsrc(out_hi + rowb, (short)0, nrec, 0x00020000),
+                                                off, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2i_t, lo),
+                                                __builtin_amdgcn_make_buffer_rsrc(out_lo + rowb, (short)0, nrec, 0x00020000),
+                                                off, 0, 0);
+        }
       // tile t+1 landed: younger than its DMA are the DMA of t+2 (6) and this tile's 8 stores
+      static_assert(2 * MW * NT == 8, "the vmcnt below counts 8 stores per tile");
       asm volatile("s_waitcnt vmcnt(14) lgkmcnt(0)" ::: "memory");
     } else {
       // lanes 0..15 hold channels 0..3 of pixel (row0, px): D rows 4 (l >> 4) + i
 #pragma unroll
       for (int c = 0; c < kMaxC; ++c) {
-        const float nc = acc[0][c] + bl[c];
+        const float nc = acc[0][0][c] + bl[0][c];
         float o = residual_sign > 0 ? nc + xi[c] : xi[c] - nc;
         if (clamp_out) o = fminf(fmaxf(o, 0.f), 1.f);
         __builtin_amdgcn_raw_buffer_store_b32(
@@ -313,15 +338,17 @@ __global__ __launch_bounds__(512, 1) void conv_s3_kernel(const half_t* __restric
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA may land after the workgroup ends
 }
 
-#define PNP_S3_INST(M, A)                                                                                      \
-  template __global__ void conv_s3_kernel<M, A>(const half_t* __restrict__, const half_t* __restrict__,       \
+#define PNP_S3_INST(M, A, WL)                                                                                  \
+  template __global__ void conv_s3_kernel<M, A, WL>(const half_t* __restrict__, const half_t* __restrict__,       \
                                                 half_t* __restrict__, half_t* __restrict__,                    \
                                                 const uint4* __restrict__, const uint4* __restrict__,          \
                                                 const float* __restrict__, const float* __restrict__,          \
                                                 float* __restrict__, ConvShape, S3Geom, int, int, int);
-PNP_S3_INST(0, 0)
-PNP_S3_INST(0, 1)
-PNP_S3_INST(1, 0)
+PNP_S3_INST(0, 0, 1)
+PNP_S3_INST(0, 1, 1)
+PNP_S3_INST(1, 0, 1)
+PNP_S3_INST(0, 0, 0)
+PNP_S3_INST(0, 1, 0)
 #undef PNP_S3_INST
 
 // ------------------------------------------------------------------------------------
@@ -498,8 +525,9 @@ inline uint16_t f16_bits(float f) {
 }  // namespace
 
 hipError_t conv_s3_kernels_init() {
-  for (const void* k : {(const void*)conv_s3_kernel<0, 0>, (const void*)conv_s3_kernel<0, 1>,
-                        (const void*)conv_s3_kernel<1, 0>}) {
+  for (const void* k : {(const void*)conv_s3_kernel<0, 0, 1>, (const void*)conv_s3_kernel<0, 1, 1>,
+                        (const void*)conv_s3_kernel<1, 0, 1>, (const void*)conv_s3_kernel<0, 0, 0>,
+                        (const void*)conv_s3_kernel<0, 1, 0>}) {
     hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kS3Lds);
     if (e != hipSuccess) return e;
   }
@@ -534,12 +562,17 @@ void launch_conv_s3_body(const half_t* in_hi, const half_t* in_lo, half_t* out_h
                          hipStream_t st) {
   const S3Geom g = s3_geom(s);
   const int grid = g.tiles < num_cus ? g.tiles : num_cus;
-  if (act == 0)
-    hipLaunchKernelGGL((conv_s3_kernel<0, 0>), dim3(grid), dim3(512), kS3Lds, st, in_hi, in_lo, out_hi, out_lo,
-                       (const uint4*)w_hi, (const uint4*)w_lo, bias, nullptr, nullptr, s, g, kWidth, 1, 0);
-  else
-    hipLaunchKernelGGL((conv_s3_kernel<0, 1>), dim3(grid), dim3(512), kS3Lds, st, in_hi, in_lo, out_hi, out_lo,
-                       (const uint4*)w_hi, (const uint4*)w_lo, bias, nullptr, nullptr, s, g, kWidth, 1, 0);
+#define S3B(A, WL)                                                                                           \
+  hipLaunchKernelGGL((conv_s3_kernel<0, A, WL>), dim3(grid), dim3(512), kS3Lds, st, in_hi, in_lo, out_hi, out_lo, \
+                     (const uint4*)w_hi, (const uint4*)w_lo, bias, nullptr, nullptr, s, g, kWidth, 1, 0)
+  if (w_lo) {
+    if (act == 0) S3B(0, 1);
+    else S3B(1, 1);
+  } else {                                          // fp16a2: no w_lo term
+    if (act == 0) S3B(0, 0);
+    else S3B(1, 0);
+  }
+#undef S3B
 }
 
 void launch_conv_s3_tail(const half_t* in_hi, const half_t* in_lo, const float* xin, float* xout, const void* w_hi,

@@ -30,6 +30,10 @@ void launch_conv_body(const half_t* in, half_t* out, const void* w, const float*
                       int act, int num_cus, int ablate, hipStream_t st);
 #ifdef PNP_PROFILING
 constexpr int kTuneAblate = 99;   // pnp_set_tuning key of the profiling build (not in include/pnppds.h)
+constexpr int kTuneAblateK2 = 98; // profiling build: k2_blur_rb ablation legs (ops.hip ABL bits)
+#ifdef PNP_PROFILING
+void set_k2_ablate(int bits);
+#endif
 #endif
 void launch_conv_tail(const half_t* in, const float* xin, float* xout, const void* w, const void* w_lo,
                       const float* bias, const ConvShape& s, int C, int residual_sign, int clamp_out, int num_cus,

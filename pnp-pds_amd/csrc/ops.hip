@@ -1355,7 +1355,10 @@ __device__ __forceinline__ void rb_fill_k2_fast(float* lds, int i0, int j0, int 
 // x_obs (and B's s, w) and nothing is read twice.  partials: [B][cells][C][4] (per 32 x 32
 // cell and channel), reduced by k3 in that order: d2 per cell, e2 / n2 / t2 per tile in the
 // tile's first cell (zeros in the others).
-template <class T, int METHOD, int LAT = 0>   // LAT: as k1_blur_rb, and all 8 epilogue rows' loads in flight
+// ABL (PNP_PROFILING build only, results wrong): phases of K2 removed for the ablation legs of
+// tools/gpu_r05_k2abl.sh: 1 no stencil (each output takes one LDS value), 2 no fp64 partials
+// (no metric sums, no d2), 4 no epilogue stores, 8 no halo fill, 16 no epilogue loads.
+template <class T, int METHOD, int LAT = 0, int ABL = 0>   // LAT: as k1_blur_rb, and all 8 epilogue rows' loads in flight
 __global__ __launch_bounds__(256) void k2_blur_rb(const float* __restrict__ xn, const float* __restrict__ xo,
                                                    float* __restrict__ y, const float* __restrict__ xobs,
                                                    const float* __restrict__ xtrue, float* __restrict__ s,
@@ -1387,6 +1390,10 @@ __global__ __launch_bounds__(256) void k2_blur_rb(const float* __restrict__ xn, 
   auto load_epi = [&](int rb) {
 #pragma unroll
     for (int k = 0; k < EB; ++k) {
+      if (ABL & 16) {
+        yv[k] = bv[k] = sv[k] = wv[k] = f2_t{0.25f * (float)k, (float)rb};
+        continue;
+      }
       const bool vec = al && rw.nv(rb + k) == 2;
       yv[k] = ld2g(y, rw.ix(rb + k), rw.nv(rb + k), vec);
       bv[k] = ld2g(xobs, rw.ix(rb + k), rw.nv(rb + k), vec);
@@ -1397,12 +1404,14 @@ __global__ __launch_bounds__(256) void k2_blur_rb(const float* __restrict__ xn, 
     }
   };
   if (LAT) load_epi(0);
+  if (ABL & 2) record = 0;
   {
     double e2 = 0, n2 = 0, t2 = 0;
     float lo = __builtin_inff(), hi = -__builtin_inff();
-    rb_fill_k2_fast<G, LAT ? 32 : kRbFill>(lds, i0, j0, H, W, xn + (size_t)bc * plane, xo + (size_t)bc * plane,
-                                          xtrue ? xtrue + (size_t)bc * plane : nullptr, record != 0, e2, n2, t2,
-                                          lo, hi);
+    if (!(ABL & 8))
+      rb_fill_k2_fast<G, LAT ? 32 : kRbFill>(lds, i0, j0, H, W, xn + (size_t)bc * plane, xo + (size_t)bc * plane,
+                                            xtrue ? xtrue + (size_t)bc * plane : nullptr, record != 0, e2, n2, t2,
+                                            lo, hi);
     if (record) {                            // reduced here, so no fill value stays live past the fill
       e2 = wave_sum(e2);
       n2 = wave_sum(n2);
@@ -1425,7 +1434,15 @@ __global__ __launch_bounds__(256) void k2_blur_rb(const float* __restrict__ xn, 
     mm[chunk * 2 + 1] = fmaxf(fmaxf(redr[0][1], redr[1][1]), fmaxf(redr[2][1], redr[3][1]));
   }
   f2_t g[kRbRows];
-  rb_stencil<T>(lds, wd_fwd, g);
+  if (ABL & 1) {
+#pragma unroll
+    for (int r = 0; r < kRbRows; ++r) {
+      const float* bp = lds + ((threadIdx.x >> 5) * kRbRows + r + G::R) * G::LW + 2 * tx;
+      g[r] = f2_t{bp[0], bp[1]};
+    }
+  } else {
+    rb_stencil<T>(lds, wd_fwd, g);
+  }
   double d2 = 0;
   {
     const float th = METHOD == M_B ? theta[b] : 0.f;
@@ -1454,11 +1471,14 @@ __global__ __launch_bounds__(256) void k2_blur_rb(const float* __restrict__ xn, 
             yo[q] = (float)(v - gamma2 * p);
           } else {
             yo[q] = (float)v;
-            const double dd = v * inv_g2 - ob;
-            d2 += dd * dd;
+            if (!(ABL & 2)) {
+              const double dd = v * inv_g2 - ob;
+              d2 += dd * dd;
+            }
           }
         }
         const bool vec = al && rw.nv(r) == 2;
+        if ((ABL & 4) && !(yo[0] == 1234.5f && gamma2 == -7.0)) continue;   // keeps the values live
         st2g(y, rw.ix(r), yo, rw.nv(r), vec);
         if (METHOD == M_B) st2g(s, rw.ix(r), so, rw.nv(r), vec);
       }
@@ -1868,6 +1888,11 @@ static void launch_k2_kind(int method, dim3 grid, hipStream_t st, const float* x
 #undef K2_ARGS
 }
 
+#ifdef PNP_PROFILING
+static int g_k2_ablate = 0;   // kTuneAblateK2 (profiling build): k2_blur_rb's ABL legs at the metric shape
+void set_k2_ablate(int bits) { g_k2_ablate = bits; }
+#endif
+
 template <class T>
 static void launch_k2_rb(int method, hipStream_t st, const float* xn, const float* xo, float* y, const float* xobs,
                          const float* xtrue, float* s, const float* w, const float* theta, double* partials,
@@ -1878,6 +1903,14 @@ static void launch_k2_rb(int method, hipStream_t st, const float* xn, const floa
   const bool lat = B * C * tiles < op.num_cus;     // one block per CU at most: latency-bound
 #define K2RB_ARGS xn, xo, y, xobs, xtrue, s, w, theta, partials, reinterpret_cast<const f2_t*>(op.dense_fwd), C, H, W, \
                   tx, tiles, cells_x, cells, gamma2, 1.0 / gamma2, gkl_gamma, gkl_alpha, record, mm
+#ifdef PNP_PROFILING
+#define K2RB_ABL(M, A) if (g_k2_ablate == A) { hipLaunchKernelGGL((k2_blur_rb<T, M, 0, A>), grid, dim3(256), 0, st, K2RB_ARGS); return; }
+  if (method == M_A && !lat && g_k2_ablate) {
+    K2RB_ABL(M_A, 1) K2RB_ABL(M_A, 2) K2RB_ABL(M_A, 4) K2RB_ABL(M_A, 8) K2RB_ABL(M_A, 16) K2RB_ABL(M_A, 3)
+    K2RB_ABL(M_A, 6) K2RB_ABL(M_A, 20) K2RB_ABL(M_A, 7) K2RB_ABL(M_A, 9)
+  }
+#undef K2RB_ABL
+#endif
 #define K2RBL(M)                                                                                              \
   if (lat) hipLaunchKernelGGL((k2_blur_rb<T, M, 1>), grid, dim3(256), 0, st, K2RB_ARGS);                       \
   else hipLaunchKernelGGL((k2_blur_rb<T, M, 0>), grid, dim3(256), 0, st, K2RB_ARGS);

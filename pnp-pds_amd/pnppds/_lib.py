@@ -23,12 +23,15 @@ METHOD_A, METHOD_B, METHOD_C, METHOD_ADMM_B2 = 0, 1, 2, 3
  METHOD_C_PNPADMM, METHOD_C_RED) = range(4, 13)
 TV_METHODS = (METHOD_A_PDS_TV, METHOD_A_FBS_TV, METHOD_B_HTV)   # no denoiser
 OP_ID, OP_BLUR, OP_RANDOM_SAMPLING = 0, 1, 2
-PREC_FP16, PREC_FP32, PREC_FP16W2, PREC_FP16X3, PREC_AUTO = 0, 1, 2, 3, 4
-PRECISIONS = {"fp16": PREC_FP16, "fp32": PREC_FP32, "fp16w2": PREC_FP16W2, "fp16x3": PREC_FP16X3, "auto": PREC_AUTO}
+PREC_FP16, PREC_FP32, PREC_FP16W2, PREC_FP16X3, PREC_AUTO, PREC_CONVERGE, PREC_FP16A2 = 0, 1, 2, 3, 4, 5, 6
+PRECISIONS = {"fp16": PREC_FP16, "fp32": PREC_FP32, "fp16w2": PREC_FP16W2, "fp16x3": PREC_FP16X3, "auto": PREC_AUTO,
+              "converge": PREC_CONVERGE, "fp16a2": PREC_FP16A2}
 PRECISION_NAMES = {v: k for k, v in PRECISIONS.items()}
 TUNE_DENOISE_CHUNK = 1
 TUNE_BODY_LAYERS = 2
 TUNE_GRAPH = 3
+TUNE_CONVERGE_C = 4      # PNP_PREC_CONVERGE's c_n threshold, units of 1e-6 (ABI 7)
+TUNE_ABLATE_K2 = 98      # profiling build only: k2_blur_rb ablation legs (ops.hip ABL bits)
 TUNE_ABLATE = 99         # profiling build only (make PROFILING=1, lib_prof/): not in include/pnppds.h
 
 
@@ -46,7 +49,7 @@ class pnp_params(C.Structure):
                 ("record_ssim", C.c_int32)]
 
 
-ABI_VERSION = 6   # include/pnppds.h PNP_ABI_VERSION
+ABI_VERSION = 7   # include/pnppds.h PNP_ABI_VERSION
 class pnp_degrade_params(C.Structure):
     _fields_ = [("gaussian_nl", C.c_double), ("sp_nl", C.c_double), ("poisson_alpha", C.c_double),
                 ("poisson_noise", C.c_int32), ("seed", C.c_uint32)]
@@ -69,6 +72,7 @@ _SIGS = {
     "pnp_set_denoiser": ([_P, C.c_int, C.c_int, C.c_int, _F, C.c_size_t, C.c_int, C.c_int, C.c_int], C.c_int),
     "pnp_set_precision": ([_P, C.c_int], C.c_int),
     "pnp_get_precision": ([_P, C.POINTER(C.c_int), C.POINTER(C.c_int)], C.c_int),
+    "pnp_get_precision_switch": ([_P, C.POINTER(C.c_int)], C.c_int),
     "pnp_device_copy": ([_P, _P, _P, C.c_size_t, _P], C.c_int),
     "pnp_set_tuning": ([_P, C.c_int, C.c_int], C.c_int),
     "pnp_set_operator": ([_P, C.c_int, _D, C.c_int, C.c_int, C.POINTER(C.c_uint8), C.c_int, C.c_int], C.c_int),
@@ -247,8 +251,10 @@ class Context:
         below; include/pnppds.h PNP_PREC_AUTO), 'fp16' (fp32
         accumulation), 'fp16w2' (fp16 activations, weights as fp16 hi + lo pairs: two MFMAs per
         product), 'fp16x3' (activations and weights as hi + lo pairs: three MFMAs per product,
-        near-fp32) or 'fp32' (the reference's own precision, models/denoiser.py:37; about a
-        tenth of the fp16 throughput)."""
+        near-fp32), 'fp32' (the reference's own precision, models/denoiser.py:37; about a
+        tenth of the fp16 throughput) or 'converge' (auto's operands while the batch's smallest
+        c_n is above 3e-3, split fp16 after: c_n then follows the reference's curve, which fp16
+        activations stop following below ~3e-4; get_precision_switch() says when it switched)."""
         code = PRECISIONS[precision] if isinstance(precision, str) else int(precision)
         self._check(self.lib.pnp_set_precision(self.h, code))
         self.precision = code
@@ -258,6 +264,18 @@ class Context:
         r, e = C.c_int(), C.c_int()
         self._check(self.lib.pnp_get_precision(self.h, C.byref(r), C.byref(e)))
         return PRECISION_NAMES[r.value], PRECISION_NAMES[e.value]
+
+    def get_precision_switch(self) -> int:
+        """precision='converge': the first iteration of the current solve that ran split fp16
+        (fp16x3), or -1 if it has not switched (pnp_get_precision_switch)."""
+        it = C.c_int()
+        self._check(self.lib.pnp_get_precision_switch(self.h, C.byref(it)))
+        return it.value
+
+    def set_converge_threshold(self, c: float):
+        """precision='converge': switch to split fp16 once the batch's smallest c_n is below c
+        (default 3e-3; set in units of 1e-6, PNP_TUNE_CONVERGE_C)."""
+        self._check(self.lib.pnp_set_tuning(self.h, TUNE_CONVERGE_C, max(1, int(round(c * 1e6)))))
 
     def set_denoise_chunk(self, images: int):
         """Images per denoiser pass (0 = auto).  Performance only."""
@@ -280,6 +298,12 @@ class Context:
         results wrong): skip parts of the one-layer body kernel (1 = halo DMA, 2 = stores,
         4 = MFMA K-loop).  The product library rejects the key (PNP_E_UNSUPPORTED)."""
         self._check(self.lib.pnp_set_tuning(self.h, TUNE_ABLATE, int(bits)))
+
+    def set_ablate_k2(self, bits: int):
+        """Profiling build only (results wrong): blur K2 (k2_blur_rb, ours-A, batched) with phases
+        removed: 1 stencil, 2 fp64 partials, 4 epilogue stores, 8 halo fill, 16 epilogue loads
+        (and the combinations 3, 6, 7, 9, 20).  Process-wide."""
+        self._check(self.lib.pnp_set_tuning(self.h, TUNE_ABLATE_K2, int(bits)))
 
     def set_operator(self, kind: int, h=None, mask=None, key=None):
         if key is not None and key == self._operator_key:

@@ -63,16 +63,25 @@ BM3D_METHODS = ("A-PnPPDS-BM3D", "A-PnPFBS-BM3D", "comparisonB-1", "C-PnPPDS-BM3
 
 # Denoiser operand precision.  'auto' (the default) leaves the choice to the library, per solve
 # (include/pnppds.h PNP_PREC_AUTO, capi.hip auto_precision), from the reference's own long
-# trajectories (tests/test_gpu_long.py): fp16 operands hold every iteration
-# within 0.01 dB only for ours-A / ours-B / comparisonB-2 on the blur operator (0.0028 dB over
-# 1200 blur iterations at sigma 0.01, 0.0039 at 0.0025; comparisonB-2 0.0060 over 30 outer); on Id and random sampling (42-50 dB
-# restorations: gray Id 0.067 dB, A random sampling 0.05-0.11 dB over 3000) and for the Poisson
-# method (0.19 dB) they do not, and those run split fp16 (fp16x3: activations and weights as
-# fp16 hi + lo pairs, three MFMAs per product; <= 0.002 dB on every long golden).
+# trajectories (tests/test_gpu_long.py): on the blur operator fp16 operands (fp16w2
+# above sigma 0.01 for ours-A / comparisonB-2) for ours-A / ours-B / comparisonB-2 / PnP-FBS / RED,
+# every iteration's PSNR within 0.0035 dB of the reference; split fp16 (fp16x3: activations and
+# weights as fp16 hi + lo pairs, three MFMAs per product, near-fp32) everywhere else.
+# Under fp16 / fp16w2 operands x and PSNR follow the reference but the returned c (c_n,
+# iteration.py:187) does not below ~3e-4: the fp16 activations' rounding leaves successive
+# iterates ~3e-4 apart where the reference's keep contracting (to ~7e-8 after 1200 iterations).
+# 'converge' keeps auto's operands while the batch's smallest c_n is above 3e-3 and runs split
+# fp16 after that, so c follows the reference's curve (checked to 10 % wherever it is >= 1e-6);
+# last_precision_switch() reports the iteration it switched at.
 def resolve_precision(precision) -> str:
     if precision not in _lib.PRECISIONS:
         raise ValueError(f"precision must be one of {sorted(_lib.PRECISIONS)}, not {precision!r}")
     return precision
+
+
+def last_precision_switch(ctx=None) -> int:
+    """After a precision='converge' solve: the first iteration that ran split fp16 (-1: none)."""
+    return (ctx or get_ctx()).get_precision_switch()
 
 
 def resolve_method(method: str) -> int:
@@ -110,7 +119,8 @@ def test_iter_batch(x_0, x_obsrv, x_true, phi, adj_phi, gamma1, gamma2, alpha_s,
     denoiser's MFMA operands, 'fp16', 'fp16w2' (split weights, two MFMAs per product), 'fp32'
     (the reference's, about 10x slower), 'fp16x3' (split fp16: hi + lo activations and weights,
     three MFMAs per product, near-fp32) or 'auto' (default: the library's per-solve policy,
-    fp16 for ours-A/B and comparisonB-2 on blur, fp16x3 otherwise)."""
+    fp16 for ours-A/B and comparisonB-2 on blur, fp16x3 otherwise: c_n floors near 3e-4 under
+    fp16) or 'converge' (auto until c_n < 3e-3, then fp16x3: the reference's c_n curve)."""
     m = resolve_method(method)
     _check_ops(phi, adj_phi)
     x0 = np.asarray(x_0)
@@ -137,7 +147,8 @@ def test_iter(x_0, x_obsrv, x_true, phi, adj_phi, gamma1, gamma2, alpha_s, alpha
               gammaInADMMStep1, gaussian_nl, sp_nl, poisson_alpha, path_prox, max_iter, method="A-Proposed",
               ch=3, r=1, *, precision="auto"):
     """iteration.py:10 signature; x_0 etc. are (C,H,W) (RGB) or (H,W) (gray).  Keyword-only
-    extension: precision ('auto' default, 'fp16', 'fp16w2', 'fp16x3', 'fp32'; see test_iter_batch)."""
+    extension: precision ('auto' default, 'fp16', 'fp16w2', 'fp16x3', 'fp32', 'converge'; see
+    test_iter_batch and the precision notes above resolve_precision)."""
     x0 = np.asarray(x_0)
     shp = x0.shape
     to4 = (lambda a: np.asarray(a).reshape((1, 1) + shp)) if x0.ndim == 2 else \

@@ -308,8 +308,13 @@ LONG_CASES = [
     ("FBS_blur_s004_1200", "A-PnPFBS-DnCNN", "blur",  3, 128, 0.04,  0.0, False, 1.0,    0.99,        0.95, 1.0,  1.0, 0.8, 1200),
     ("RED_blur_s004_1200", "A-RED-DnCNN", "blur",     3, 128, 0.04,  0.0, False, 1.0,    0.99,        0.95, 1.0,  1.0, 0.8, 1200),
     ("ADMM_B2_s004_30", "comparisonB-2", "blur",      3, 128, 0.04, 0.1, False, 0.99,    0.99,        0.95, 0.95, 1.0, 0.8, 30),
+    # round 5: comparisonB-2 above sigma 0.01, where auto runs fp16w2, at the 200
+    # outer iterations (m1 = 35, m2 = 5) that qualified fp16 at sigma 0.01
+    ("ADMM_B2_s002_200", "comparisonB-2", "blur",     3, 128, 0.02, 0.1, False, 0.99,    0.99,        0.95, 0.95, 1.0, 0.8, 200),
+    ("ADMM_B2_s004_200", "comparisonB-2", "blur",     3, 128, 0.04, 0.1, False, 0.99,    0.99,        0.95, 0.95, 1.0, 0.8, 200),
 ]
-LONG_INNER = {"ADMM_B2_30": (35, 5), "ADMM_B2_200": (35, 5), "ADMM_B2_s004_30": (35, 5)}   # (m1, m2) if not 15, 15
+LONG_INNER = {"ADMM_B2_30": (35, 5), "ADMM_B2_200": (35, 5), "ADMM_B2_s004_30": (35, 5),   # (m1, m2) if not 15, 15
+              "ADMM_B2_s002_200": (35, 5), "ADMM_B2_s004_200": (35, 5)}
 
 
 def make_long_golden(ref_root="/root/reference", only=None):

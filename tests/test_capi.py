@@ -56,7 +56,7 @@ def test_exports_are_plain_c(lib):
 
 def test_abi_version_and_errors_without_gpu(lib):
     from pnppds import _lib
-    assert lib.pnp_abi_version() == _lib.ABI_VERSION == 6
+    assert lib.pnp_abi_version() == _lib.ABI_VERSION == 7
     lib.pnp_last_error.restype = ctypes.c_char_p
     h = ctypes.c_void_p()
     rc = lib.pnp_create(0, ctypes.byref(h))
@@ -69,6 +69,20 @@ def test_abi_version_and_errors_without_gpu(lib):
 def test_null_context_is_rejected(lib):
     assert lib.pnp_solver_iterate(None, 1) == -1
     assert lib.pnp_synchronize(None) == -1
+    it = ctypes.c_int(5)
+    assert lib.pnp_get_precision_switch(None, ctypes.byref(it)) == -1 and it.value == 5
+    assert lib.pnp_set_precision(None, 5) == -1
+
+
+def test_precision_enum_matches_python():
+    """The Python names of pnp_precision / the tuning keys are the header's values (ABI 7 added
+    PNP_PREC_CONVERGE, PNP_PREC_FP16A2 and PNP_TUNE_CONVERGE_C)."""
+    from pnppds import _lib
+    src = open(HEADER).read()
+    vals = {k: int(v) for k, v in re.findall(r"(PNP_(?:PREC|TUNE)_\w+)\s*=\s*(\d+)", src)}
+    assert {k[len("PNP_PREC_"):].lower(): v for k, v in vals.items() if k.startswith("PNP_PREC_")} == \
+        {("fp16" if k == "fp16" else k): v for k, v in _lib.PRECISIONS.items()}
+    assert vals["PNP_TUNE_CONVERGE_C"] == _lib.TUNE_CONVERGE_C and vals["PNP_TUNE_GRAPH"] == _lib.TUNE_GRAPH
 
 
 def test_params_struct_layout():

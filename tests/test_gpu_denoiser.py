@@ -156,6 +156,52 @@ def test_denoiser_fp16x3_ragged_batched(gpu_ctx, B, C, H, W):
     np.testing.assert_array_equal(one[0], out[B - 1])
 
 
+@pytest.mark.parametrize("B,C,H,W", [(3, 3, 50, 70), (2, 1, 33, 31), (1, 3, 8, 16), (1, 1, 5, 7), (2, 3, 256, 256),
+                                     (4, 3, 41, 100)])
+def test_denoiser_fp16a2_ragged_batched(gpu_ctx, B, C, H, W):
+    """fp16a2 (PNP_PREC_FP16A2, the converge mode's second phase): split activations, fp16 body
+    weights, two MFMAs per product, two M-subtiles per wave.  Against the oracle emulating it (fp16
+    body weights, fp32 activations) at split fp16's tolerance, nearer that than fp32; partial 8 x 16
+    tiles, tiny images; each image alone gives the batch's bits."""
+    rng = np.random.default_rng(B * 100 + H + 11)
+    w = random_weights(C, depth=6, seed=H + 3, scale=0.9)
+    x = rng.uniform(-0.1, 1.1, (B, C, H, W)).astype(np.float32)
+    gpu_ctx.set_precision("fp16a2")
+    try:
+        out = run_denoise(gpu_ctx, w, x)
+        one = run_denoise(gpu_ctx, w, x[B - 1:B])
+    finally:
+        gpu_ctx.set_precision("fp16")
+    emu = O.OracleDenoiser(w, emulate_fp16="a2").forward_batch(x)
+    ref = O.OracleDenoiser(w).forward_batch(x)
+    print(f"fp16a2 {B}x{C}x{H}x{W}: max|d| vs its emulation {np.abs(out - emu).max():.2e}, vs fp32 "
+          f"{np.abs(out - ref).max():.2e}")
+    np.testing.assert_allclose(out, emu, atol=TOL_X3)
+    np.testing.assert_array_equal(one[0], out[B - 1])
+
+
+@pytest.mark.parametrize("name", ["DnCNN_nobn_nch_3_nlev_0.01", "dncnn_color_blind"])
+def test_denoiser_fp16a2_golden(gpu_ctx, golden_denoiser, name):
+    """fp16a2 against the reference's own denoiser outputs: within the fp16 path's bound, and closer
+    than fp16 operands."""
+    w = DenoiserWeights.load_npz(os.path.join(WEIGHTS_DIR, name + ".npz"))
+    xin = golden_denoiser[f"in_{name}"]
+    x4 = xin.reshape((1, 1) + xin.shape) if xin.ndim == 2 else xin[None]
+    gpu_ctx.set_precision("fp16a2")
+    try:
+        out = run_denoise(gpu_ctx, w, x4).reshape(xin.shape)
+    finally:
+        gpu_ctx.set_precision("fp16")
+    ref = golden_denoiser[f"out_{name}"]
+    err = float(np.abs(out - ref).max())
+    e16 = float(np.abs(O.OracleDenoiser(w, emulate_fp16=True).forward_batch(x4).reshape(xin.shape) - ref).max())
+    emu = O.OracleDenoiser(w, emulate_fp16="a2").forward_batch(x4).reshape(xin.shape)
+    print(f"{name}: fp16a2 max|d| vs reference {err:.2e} (fp16 operands {e16:.2e}), vs its emulation "
+          f"{np.abs(out - emu).max():.2e}")
+    assert err < e16
+    assert np.abs(out - emu).max() <= TOL_X3 * max(1.0, float(np.abs(ref).max()))
+
+
 @pytest.mark.parametrize("B,C,H,W", [(3, 3, 50, 70), (2, 1, 33, 31), (1, 3, 8, 32), (2, 3, 256, 256)])
 def test_denoiser_fp32_ragged_batched(gpu_ctx, B, C, H, W):
     """fp32 path: partial tiles, tiny images, several images per launch; batch vs single bits."""

@@ -20,12 +20,42 @@ pytestmark = pytest.mark.gpu
 
 PSNR_TOL_DB = 0.01          # north_star: PSNR within 0.01 dB of the reference
 AUTO_FP16_MARGIN_DB = 0.005  # where PNP_PREC_AUTO picks plain fp16 operands: half the bound
-# c_n = ||x_n - x_prev|| / ||x_prev|| (iteration.py:187).  With fp16 denoiser operands the
-# iteration settles into a fixed point of the fp16-rounded map, where successive iterates
-# still differ by about one fp16 rounding (2^-11 relative): c_n stalls near 3e-4 while the
-# reference's fp32 iteration keeps contracting (to 7e-8 after 1200 iterations).  So c_n is
-# compared down to that floor for fp16, and down to 2e-6 for the fp32-operand path.
-C_FLOOR = {"fp16": 1e-3, "fp16w2": 1e-3, "fp16x3": 2e-5, "fp32": 2e-6}
+# c_n = ||x_n - x_prev|| / ||x_prev|| (iteration.py:187), the reference's convergence output
+# (c_evolution, main.py:82; plotted on a log axis by plot.py:26,49).  Checked to C_RTOL relative
+# wherever the reference's c is at least the mode's C_MIN:
+#  * near-fp32 operands (split fp16 'fp16x3', 'fp32', and 'converge' after its hand-over) follow
+#    the reference's c down to its ~7e-8 floor within a few per cent (r05 probe,
+#    profiles/r05/converge_probe.txt: <= 1.7 % wherever c_ref >= 1e-6; their own floor is
+#    ~1.6e-7, which is why C_MIN is 1e-6);
+#  * fp16 activations ('fp16', 'fp16w2') settle on the fp16-rounded map's fixed point, where
+#    successive iterates stay about one fp16 rounding apart: c stalls at FP16_C_FLOOR's order
+#    (2.3-2.8e-4 on every blur golden, r04 parity.txt) while the reference's keeps contracting.
+#    There c is checked to C_RTOL only where c_ref >= 10x that floor, and below it the stall is
+#    asserted not to exceed FP16_C_FLOOR (so a worse floor fails).  'converge' exists for the c
+#    curve: see test_converge_c_trajectory.
+C_RTOL = 0.10
+FP16_C_FLOOR = 5e-4
+C_MIN = {"fp16": 3e-3, "fp16w2": 3e-3, "fp16x3": 1e-6, "fp32": 1e-6, "fp16a2": 1e-6}   # fp16: ~10x its floor
+# x against the reference's final iterate (stored as fp16 in the golden: up to 2.4e-4 of the
+# error is the fixture's own rounding).  Measured max |dx| (r04 parity.txt, r05): fp16 / fp16w2
+# 5e-4 - 1e-3 on every non-chaotic golden (ours-B at 300 iterations: 1.9e-3, its l1-ball support
+# moving with the rounding), split fp16 / fp32 2.0-3.0e-4: bounds about 2-3x that.
+X_TOL = {"fp16": 1.5e-3, "fp16w2": 1.5e-3, "fp16x3": 5e-4, "fp32": 5e-4, "fp16a2": 1.5e-3}
+X_TOL_CASE = {("B_blur_300", "fp16"): 4e-3}
+
+
+def check_c(case, c, gc, prec):
+    """c (the device's c_n per iteration) against the golden's, per the mode's rule above."""
+    gc = np.asarray(gc, np.float64)
+    m = gc >= C_MIN[prec]
+    rel = np.abs(c[m] - gc[m]) / gc[m]
+    print(f"  c_n: max rel err {rel.max() if rel.size else 0:.4f} over {int(m.sum())} iterations with c_ref >= "
+          f"{C_MIN[prec]:.0e}; final {c[-1]:.3e} vs {gc[-1]:.3e}")
+    assert rel.size == 0 or rel.max() <= C_RTOL, (case, prec, float(rel.max()), int(np.argmax(rel)))
+    if prec in ("fp16", "fp16w2") and case not in CHAOTIC:
+        below = ~m
+        assert np.all(c[below] <= np.maximum(gc[below] * (1 + C_RTOL), FP16_C_FLOOR)), \
+            (case, prec, float(np.max(c[below])))
 
 
 # Ill-conditioned trajectories (tools/chaos_probe.py on the fp32 test oracle, DESIGN.md §4): ours-B
@@ -93,6 +123,9 @@ def run_long(g, precision=None):
                                             ("B_blur_s002_1200", "auto"), ("B_blur_s004_1200", "auto"),
                                             ("FBS_blur_s004_1200", "auto"), ("RED_blur_s004_1200", "auto"),
                                             ("ADMM_B2_s004_30", "auto"),
+                                            # round 5: comparisonB-2 above sigma 0.01 (auto:
+                                            # fp16w2) at the 200 outer iterations that qualified fp16
+                                            ("ADMM_B2_s004_200", "auto"),
                                             ("A_blur_s004_1200", "fp16x3")])
 def test_long_trajectory_psnr(case, precision):
     """Every iteration's PSNR within 0.01 dB of the reference's trajectory.  'auto' is the
@@ -110,17 +143,89 @@ def test_long_trajectory_psnr(case, precision):
         off = np.mean(np.abs(x - g["x_out"].astype(np.float32)) > 5e-3)
         print(f"  pixels off by > 5e-3: {off:.5f}")
         assert off <= CHAOTIC[case], (case, off)
-    else:
-        np.testing.assert_allclose(x, g["x_out"].astype(np.float32), atol=5e-3)
-    from pnppds._device import get_ctx
     prec = get_ctx().get_precision()[1]          # what 'auto' resolved to for this solve
+    if case not in CHAOTIC:
+        dx = np.abs(x - g["x_out"].astype(np.float32)).max()
+        print(f"  max|dx| {dx:.2e}")
+        assert dx <= X_TOL_CASE.get((case, prec), X_TOL[prec]), (case, prec, float(dx))
     if precision == "auto":
         assert prec == expected_auto(g), (case, prec)
         if prec in ("fp16", "fp16w2"):
             # the policy runs fp16 activations only with half the bound to spare
             assert d.max() <= AUTO_FP16_MARGIN_DB, (case, d.max())
-    np.testing.assert_allclose(c, g["c"], rtol=0.05, atol=C_FLOOR[prec])
-    print(f"  c_n final {c[-1]:.3e} vs {g['c'][-1]:.3e}")
+    check_c(case, c, g["c"], prec)
+
+
+CONVERGE_C = 3e-3   # PNP_PREC_CONVERGE's default threshold (include/pnppds.h PNP_TUNE_CONVERGE_C)
+
+
+@pytest.mark.parametrize("case", ["A_blur_1200", "B_blur_1200", "ADMM_B2_200", "A_blur_s004_1200",
+                                  "FBS_blur_1200", "RED_blur_s0025_1200", "A_blur_s0025_a100_1200"])
+def test_converge_c_trajectory(case):
+    """precision='converge' (PNP_PREC_CONVERGE): auto's fp16 / fp16w2 operands until the smallest
+    c_n of the batch falls below 3e-3, split activations (fp16a2) from two iterations later (the
+    host reads c_n one iteration behind the device).  The returned c follows the reference's within 10 % wherever
+    the reference's is >= 1e-6 (fp16 alone stalls near 3e-4 there, 1 100+ of 1 200 iterations of
+    long_A_blur_1200 unchecked before round 5), PSNR within the bound with auto's margin, x like
+    split fp16's; the reported switch iteration is where the rule puts it."""
+    from pnppds.iteration import last_precision_switch
+    g = load_golden(f"long_{case}.npz")
+    x, s, c, psnr, ssim, t = run_long(g, "converge")
+    sw = last_precision_switch()
+    below = np.nonzero(c < CONVERGE_C)[0]
+    assert below.size and sw == below[0] + 2, (case, sw, below[:3])
+    d = np.abs(psnr - g["psnr"])
+    dx = np.abs(x - g["x_out"].astype(np.float32)).max()
+    print(f"{case} converge: switch at {sw}; max|dPSNR| {d.max():.5f} dB at {int(d.argmax())}; max|dx| {dx:.2e}")
+    assert d.max() <= AUTO_FP16_MARGIN_DB, (case, d.max())
+    assert dx <= X_TOL["fp16a2"], (case, dx)       # after the hand-over: fp16a2 (fp16 weights)
+    check_c(case, c, g["c"], "fp16a2")
+
+
+def test_converge_handover_bits():
+    """The hand-over is a plain precision change between iterations: a converge solve that
+    switches at iteration k gives the bits of k fp16 iterations followed by fp16a2 ones; with no
+    metrics to watch it runs split activations from iteration 0 (switch 0, fp16a2's bits)."""
+    from pnppds import operators as ops
+    from pnppds._device import get_ctx
+    from pnppds.iteration import _resolve_denoiser, make_params, resolve_method
+    g = load_golden("long_A_blur_1200.npz")
+    g1, g2, as_, an, lam, m1, m2, gadmm, sig, sp, palpha, iters, ch, r = g["params"]
+    phi, adj = ops.get_observation_operators("blur", "blur_1", r)
+    ctx = get_ctx()
+    _resolve_denoiser(str(g["arch"]) + ".pth", 3).configure(ctx)
+    x0, xo, xt = (np.asarray(g[k], np.float32)[None] for k in ("x_0", "x_obs", "x_true"))
+    phi.configure(ctx, x0.shape[2], x0.shape[3])
+    n = 40
+
+    def solve(plan, record=True, threshold=None):
+        ctx.set_precision(plan[0][0])
+        if threshold:
+            ctx.set_converge_threshold(threshold)
+        ctx.solver_setup(resolve_method("A-Proposed"),
+                         make_params(g1, g2, as_, an, lam, m1, m2, gadmm, sig, sp, palpha, r, record, False),
+                         1, 3, x0.shape[2], x0.shape[3], n)
+        ctx.solver_load(x0, xo, xt)
+        for prec, k in plan:
+            ctx.set_precision(prec)
+            ctx.solver_iterate(k)
+        out = ctx.solver_fetch()
+        return out, ctx.get_precision_switch()
+
+    try:
+        (xc, _, cc, pc, _), sw = solve([("converge", n)], threshold=CONVERGE_C)
+        assert 2 <= sw < n, sw
+        (xm, _, cm, pm, _), _ = solve([("fp16", sw), ("fp16a2", n - sw)])
+        np.testing.assert_array_equal(xc, xm)
+        np.testing.assert_array_equal(cc, cm)
+        np.testing.assert_array_equal(pc, pm)
+        (xn, _, _, _, _), sw0 = solve([("converge", n)], record=False)
+        (xs, _, _, _, _), _ = solve([("fp16a2", n)], record=False)
+        assert sw0 == 0
+        np.testing.assert_array_equal(xn, xs)
+    finally:
+        ctx.set_converge_threshold(CONVERGE_C)
+        ctx.set_precision("auto")
 
 
 def _metric_batch(B=256, C=3, H=256, W=256):
@@ -162,7 +267,10 @@ def test_metric_batch_256_vs_oracle():
                                           0.99, 0.99, 1.0, 0.95, 1.0, 15, 15, 0.1, 0.01, 0.0, 300, den, iters,
                                           "A-Proposed", 3, 0.8)
         assert np.abs(psnr[b] - pr).max() < PSNR_TOL_DB, (b, np.abs(psnr[b] - pr).max())
-        np.testing.assert_allclose(x[b], xr, atol=2e-3)
+        dx = np.abs(x[b] - xr).max()
+        rel = np.abs(c[b] - cr) / cr
+        print(f"image {b}: max|dPSNR| {np.abs(psnr[b] - pr).max():.5f} dB, max|dx| {dx:.2e}, c rel {rel.max():.4f}")
+        assert dx <= X_TOL["fp16"], (b, dx)
         np.testing.assert_allclose(c[b], cr, rtol=0.05, atol=2e-4)
     x1, s1, c1, p1, _, _ = test_iter_batch(xo[127:128], xo[127:128], xt[127:128], phi, adj, *args)
     np.testing.assert_array_equal(x1[0], x[127])
