@@ -30,8 +30,8 @@ AUTO_FP16_MARGIN_DB = 0.005  # where PNP_PREC_AUTO picks plain fp16 operands: ha
 #  * fp16 activations ('fp16', 'fp16w2') settle on the fp16-rounded map's fixed point, where
 #    successive iterates stay about one fp16 rounding apart: c stalls at FP16_C_FLOOR's order
 #    (2.3-2.8e-4 on every blur golden, r04 parity.txt) while the reference's keeps contracting.
-#    There c is checked to C_RTOL only where c_ref >= 10x that floor, and below it the stall is
-#    asserted not to exceed FP16_C_FLOOR (so a worse floor fails).  'converge' exists for the c
+#    There c is checked to C_RTOL only where c_ref >= 10x that floor, and everywhere to
+#    |c - c_ref| <= C_RTOL c_ref + FP16_C_FLOOR (so a worse floor fails).  'converge' exists for the c
 #    curve: see test_converge_c_trajectory.
 C_RTOL = 0.10
 FP16_C_FLOOR = 5e-4
@@ -53,9 +53,9 @@ def check_c(case, c, gc, prec):
           f"{C_MIN[prec]:.0e}; final {c[-1]:.3e} vs {gc[-1]:.3e}")
     assert rel.size == 0 or rel.max() <= C_RTOL, (case, prec, float(rel.max()), int(np.argmax(rel)))
     if prec in ("fp16", "fp16w2") and case not in CHAOTIC:
-        below = ~m
-        assert np.all(c[below] <= np.maximum(gc[below] * (1 + C_RTOL), FP16_C_FLOOR)), \
-            (case, prec, float(np.max(c[below])))
+        # everywhere: the fp16 floor adds to the reference's c at most FP16_C_FLOOR
+        err = np.abs(c - gc) - C_RTOL * gc
+        assert np.all(err <= FP16_C_FLOOR), (case, prec, int(np.argmax(err)), float(err.max()))
 
 
 # Ill-conditioned trajectories (tools/chaos_probe.py on the fp32 test oracle): ours-B
@@ -125,7 +125,7 @@ def run_long(g, precision=None):
                                             ("ADMM_B2_s004_30", "auto"),
                                             # round 5: comparisonB-2 above sigma 0.01 (auto:
                                             # fp16w2) at the 200 outer iterations that qualified fp16
-                                            ("ADMM_B2_s004_200", "auto"),
+                                            ("ADMM_B2_s002_200", "auto"), ("ADMM_B2_s004_200", "auto"),
                                             ("A_blur_s004_1200", "fp16x3")])
 def test_long_trajectory_psnr(case, precision):
     """Every iteration's PSNR within 0.01 dB of the reference's trajectory.  'auto' is the
