@@ -491,14 +491,15 @@ void run_denoiser(pnp_ctx* ctx, const float* u32, float* xout, DevBuf (&act)[2],
       }
       int cur = 0;
       const int nbody = ctx->den_depth - 2;
-      const bool stack = !a2 && nbody > 0 && use_stack(ctx, s3_tiles(s), st);
+      const bool stack = nbody > 0 && use_stack(ctx, s3_tiles(s), st);
       if (stack) {                                 // every body layer in one launch
         ProfScope ps(ctx, "conv_stack_s3", st);
         int epoch = 0;
         int* err = nullptr;
         int* done = stack_flags(ctx, &act[0] == &ctx->act[0], s3_tiles(s), nbody, st, epoch, err);
         launch_conv_stack_s3(P<half_t>(act[0]), P<half_t>(alo[0]), P<half_t>(act[1]), P<half_t>(alo[1]),
-                             ctx->body_s3h.p, ctx->body_s3l.p, P<float>(ctx->body_b), nbody, s, ctx->den_act,
+                             a2 ? ctx->body_s3f.p : ctx->body_s3h.p, a2 ? nullptr : ctx->body_s3l.p,
+                             P<float>(ctx->body_b), nbody, s, ctx->den_act,
                              ctx->num_cus, done, epoch, err, st);
         check_launch(ctx, "conv_stack_s3");
         cur = nbody & 1;

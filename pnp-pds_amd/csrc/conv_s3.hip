@@ -364,7 +364,8 @@ constexpr int kS3StkLds = 2 * kS3Buf;                   // 98304 B
 constexpr int kS3StkPieces = 12;                        // LDS-DMA pieces per wave per tile (48 / 4)
 constexpr int kCpolDev = 16;                            // sc1: device-scope load / store
 
-template <int ACT>
+// WLO = 0: fp16a2 (no w_lo term), bit-identical to conv_s3_kernel<0, ACT, 0> launches.
+template <int ACT, int WLO = 1>
 __global__ __launch_bounds__(256, 1) void conv_stack_s3_kernel(half_t* __restrict__ aH, half_t* __restrict__ aL,
                                                                 half_t* __restrict__ bH, half_t* __restrict__ bL,
                                                                 const uint4* __restrict__ w_hi,
@@ -394,14 +395,15 @@ __global__ __launch_bounds__(256, 1) void conv_stack_s3_kernel(half_t* __restric
     const int pr = p / kS3HaloW, pc = p - pr * kS3HaloW;
     doff[j] = (unsigned)(((pr * s.Wp + pc) * kWidth + 8 * ((lane & 7) ^ s3_swz(pc))) * 2);
   }
-  half8_t wH[kS3KSteps], wL[kS3KSteps];
+  constexpr int NWL = WLO ? kS3KSteps : 1;
+  half8_t wH[kS3KSteps], wL[NWL];
   float bl[4];
   auto load_w = [&](int l) {
 #pragma unroll
     for (int ks = 0; ks < kS3KSteps; ++ks) {
       const size_t o = (size_t)l * (kBodyWBytes / 16) + (size_t)(ks * 4 + mt) * 64 + lane;
       wH[ks] = __builtin_bit_cast(half8_t, w_hi[o]);
-      wL[ks] = __builtin_bit_cast(half8_t, w_lo[o]);
+      if (WLO) wL[ks % NWL] = __builtin_bit_cast(half8_t, w_lo[o]);
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) bl[i] = bias[l * kWidth + 16 * mt + 4 * grp + i];
@@ -468,8 +470,11 @@ __global__ __launch_bounds__(256, 1) void conv_stack_s3_kernel(half_t* __restric
 #pragma unroll
           for (int n = 0; n < 4; ++n)
             acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wH[ks], bh[r][n], ks == 0 ? s3_c0<0>(bl) : acc[n], 0, 0, 0);
+          if (WLO) {
 #pragma unroll
-          for (int n = 0; n < 4; ++n) acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wL[ks], bh[r][n], acc[n], 0, 0, 0);
+            for (int n = 0; n < 4; ++n)
+              acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wL[ks % NWL], bh[r][n], acc[n], 0, 0, 0);
+          }
 #pragma unroll
           for (int n = 0; n < 4; ++n) acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wH[ks], bo[r][n], acc[n], 0, 0, 0);
         }
@@ -498,14 +503,17 @@ __global__ __launch_bounds__(256, 1) void conv_stack_s3_kernel(half_t* __restric
   }
 }
 
-template __global__ void conv_stack_s3_kernel<0>(half_t* __restrict__, half_t* __restrict__, half_t* __restrict__,
-                                                 half_t* __restrict__, const uint4* __restrict__,
-                                                 const uint4* __restrict__, const float* __restrict__, int, ConvShape,
-                                                 S3Geom, int* __restrict__, int, int* __restrict__);
-template __global__ void conv_stack_s3_kernel<1>(half_t* __restrict__, half_t* __restrict__, half_t* __restrict__,
-                                                 half_t* __restrict__, const uint4* __restrict__,
-                                                 const uint4* __restrict__, const float* __restrict__, int, ConvShape,
-                                                 S3Geom, int* __restrict__, int, int* __restrict__);
+#define PNP_STK_INST(A, WL)                                                                                     \
+  template __global__ void conv_stack_s3_kernel<A, WL>(half_t* __restrict__, half_t* __restrict__,              \
+                                                       half_t* __restrict__, half_t* __restrict__,              \
+                                                       const uint4* __restrict__, const uint4* __restrict__,    \
+                                                       const float* __restrict__, int, ConvShape, S3Geom,       \
+                                                       int* __restrict__, int, int* __restrict__);
+PNP_STK_INST(0, 1)
+PNP_STK_INST(1, 1)
+PNP_STK_INST(0, 0)
+PNP_STK_INST(1, 0)
+#undef PNP_STK_INST
 
 S3Geom s3_geom(const ConvShape& s) {
   S3Geom g;
@@ -531,7 +539,8 @@ hipError_t conv_s3_kernels_init() {
     hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kS3Lds);
     if (e != hipSuccess) return e;
   }
-  for (const void* k : {(const void*)conv_stack_s3_kernel<0>, (const void*)conv_stack_s3_kernel<1>}) {
+  for (const void* k : {(const void*)conv_stack_s3_kernel<0, 1>, (const void*)conv_stack_s3_kernel<1, 1>,
+                        (const void*)conv_stack_s3_kernel<0, 0>, (const void*)conv_stack_s3_kernel<1, 0>}) {
     hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kS3StkLds);
     if (e != hipSuccess) return e;
   }
@@ -591,8 +600,10 @@ void launch_conv_stack_s3(half_t* aH, half_t* aL, half_t* bH, half_t* bL, const 
                           int* err, hipStream_t st) {
   const S3Geom g = s3_geom(s);
   const int grid = g.tiles < num_cus ? g.tiles : num_cus;
-  (void)persistent_launch(act == 0 ? conv_stack_s3_kernel<0> : conv_stack_s3_kernel<1>, grid, 256, kS3StkLds, st, aH, aL,
-                    bH, bL, (const uint4*)w_hi, (const uint4*)w_lo, bias, nbody, s, g, done, epoch, err);
+  auto k = w_lo ? (act == 0 ? conv_stack_s3_kernel<0, 1> : conv_stack_s3_kernel<1, 1>)
+                : (act == 0 ? conv_stack_s3_kernel<0, 0> : conv_stack_s3_kernel<1, 0>);   // no w_lo: fp16a2
+  (void)persistent_launch(k, grid, 256, kS3StkLds, st, aH, aL, bH, bL, (const uint4*)w_hi, (const uint4*)w_lo, bias, nbody,
+                          s, g, done, epoch, err);
 }
 
 }  // namespace pnp

@@ -1356,8 +1356,9 @@ __device__ __forceinline__ void rb_fill_k2_fast(float* lds, int i0, int j0, int 
 // cell and channel), reduced by k3 in that order: d2 per cell, e2 / n2 / t2 per tile in the
 // tile's first cell (zeros in the others).
 // ABL (PNP_PROFILING build only, results wrong): phases of K2 removed for the ablation legs of
-// tools/gpu_r05_k2abl.sh: 1 no stencil (each output takes one LDS value), 2 no fp64 partials
-// (no metric sums, no d2), 4 no epilogue stores, 8 no halo fill, 16 no epilogue loads.
+// tools/gpu_r05_run1.sh: 1 no stencil (each output takes one LDS value), 2 no fp64 partials
+// (no metric sums, no d2), 4 no epilogue stores, 8 no halo fill, 16 no epilogue loads; 32: the
+// round-4 fp64 epilogue for ours-A (results right: an A/B leg).
 template <class T, int METHOD, int LAT = 0, int ABL = 0>   // LAT: as k1_blur_rb, and all 8 epilogue rows' loads in flight
 __global__ __launch_bounds__(256) void k2_blur_rb(const float* __restrict__ xn, const float* __restrict__ xo,
                                                    float* __restrict__ y, const float* __restrict__ xobs,
@@ -1443,9 +1444,17 @@ __global__ __launch_bounds__(256) void k2_blur_rb(const float* __restrict__ xn, 
   } else {
     rb_stencil<T>(lds, wd_fwd, g);
   }
+  // ours-A: the dual update and the l2-ball partial in float32 (round 5; ablation: the fp64
+  // partials and the fill's x_true loads together cost 27 % of the kernel); v = y + g2 Phi(.) is
+  // rounded to float32 for the state either way, and each thread's 16 terms of
+  // |v / g2 - x_obs|^2 are summed in float32 before the fixed-order fp64 reduction.  ours-B
+  // (whose sigma-0.04 golden is ill-conditioned: the float32 form moved 1.2 % of its final pixels
+  // by more than 5e-3 against 0.4 % for fp64) and ours-C's GKL prox stay in fp64.
   double d2 = 0;
   {
     const float th = METHOD == M_B ? theta[b] : 0.f;
+    const float g2f = (float)gamma2, ig2f = (float)inv_g2;
+    float d2f = 0.f;
 #pragma unroll
     for (int rb = 0; rb < kRbRows; rb += EB) {
       if (!LAT) load_epi(rb);
@@ -1456,25 +1465,32 @@ __global__ __launch_bounds__(256) void k2_blur_rb(const float* __restrict__ xn, 
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
           if (q >= rw.nv(r)) break;
-          double gv = g[r][q];
-          if (METHOD == M_B) {
-            const float wq = wv[k][q];
-            const float sp = copysignf(fmaxf(fabsf(wq) - th, 0.f), wq);   // operators.py:98
-            gv += 2.0 * (double)sp - (double)sv[k][q];
-            so[q] = sp;
-          }
-          const double v = (double)yv[k][q] + gamma2 * gv;
-          const double ob = bv[k][q];
-          if (METHOD == M_C) {
-            const double tt = v * inv_g2 - gkl_gamma * gkl_alpha;
-            const double p = 0.5 * (tt + sqrt(tt * tt + 4.0 * gkl_gamma * ob));
-            yo[q] = (float)(v - gamma2 * p);
-          } else {
-            yo[q] = (float)v;
-            if (!(ABL & 2)) {
+          if (METHOD == M_C || METHOD == M_B || (ABL & 32)) {   // fp64 (ABL 32: the round-4 form for ours-A)
+            double gv = g[r][q];
+            if (METHOD == M_B) {
+              const float wq = wv[k][q];
+              const float sp = copysignf(fmaxf(fabsf(wq) - th, 0.f), wq);   // operators.py:98
+              gv += 2.0 * (double)sp - (double)sv[k][q];
+              so[q] = sp;
+            }
+            const double v = (double)yv[k][q] + gamma2 * gv;
+            const double ob = bv[k][q];
+            if (METHOD == M_C) {
+              const double tt = v * inv_g2 - gkl_gamma * gkl_alpha;
+              const double p = 0.5 * (tt + sqrt(tt * tt + 4.0 * gkl_gamma * ob));
+              yo[q] = (float)(v - gamma2 * p);
+            } else {
+              yo[q] = (float)v;
               const double dd = v * inv_g2 - ob;
               d2 += dd * dd;
             }
+            continue;
+          }
+          const float v = fmaf(g2f, g[r][q], yv[k][q]);
+          yo[q] = v;
+          if (!(ABL & 2)) {
+            const float dd = fmaf(v, ig2f, -bv[k][q]);
+            d2f = fmaf(dd, dd, d2f);
           }
         }
         const bool vec = al && rw.nv(r) == 2;
@@ -1483,6 +1499,7 @@ __global__ __launch_bounds__(256) void k2_blur_rb(const float* __restrict__ xn, 
         if (METHOD == M_B) st2g(s, rw.ix(r), so, rw.nv(r), vec);
       }
     }
+    d2 += d2f;
   }
   // d2: a wave is two thread rows (2 kRbRows tile rows) x 32 threads; a 32 x 32 cell is 16
   // threads (tx) of WPC = 32 / (2 kRbRows) waves: reduce each wave's two column halves in the
@@ -1575,7 +1592,12 @@ __device__ __forceinline__ float ssim_s(float ux, float uy, float uxx, float uyy
   const float vxy = cov_norm * (uxy - ux * uy);
   const float A1 = 2.f * ux * uy + C1, A2 = 2.f * vxy + C2;
   const float B1 = ux * ux + uy * uy + C1, B2 = vx + vy + C2;
-  return (A1 * A2) / (B1 * B2);
+  // the quotient by the hardware reciprocal and one Newton step (within 1 ulp of numpy's IEEE
+  // division; 3 instructions instead of v_div_scale / fmas / fixup's ~10)
+  const float n = A1 * A2, d = B1 * B2;
+  const float r = __builtin_amdgcn_rcpf(d);
+  const float q = n * r;
+  return fmaf(fmaf(-d, q, n), r, q);
 }
 
 // Window sums in float32 (round 5): running sums over 8 outputs per thread
@@ -1608,19 +1630,28 @@ __global__ __launch_bounds__(256) void ssim_rgb_kernel(const float* __restrict__
     const float R = ssim_range_wave(mm, b, chunks, lane);
     if (lane == 0) { cst[0] = (0.01f * R) * (0.01f * R); cst[1] = (0.03f * R) * (0.03f * R); }
   }
-  const float* pa = xt + (size_t)bc * H * W;
-  const float* pb = x + (size_t)bc * H * W;
+  const __amdgpu_buffer_rsrc_t qa = plane_rsrc(xt + (size_t)bc * H * W, H, W);
+  const __amdgpu_buffer_rsrc_t qb = plane_rsrc(x + (size_t)bc * H * W, H, W);
   // ---- vertical: columns j0-3+c (c < 62), rows i0 + 8*wv .. +8 ----
   if (lane < kSsVW) {
     const int c = lane;
     const int gj = min(max(j0 - 3 + c, 0), W - 1);
     const int r0 = i0 + 8 * wv;
     float ra[14], rb[14];
+    if (__builtin_amdgcn_readfirstlane((int)(r0 >= 3 && r0 + 11 <= H))) {   // no row clamp: an index add per row
+      int idx = (r0 - 3) * W + gj;
 #pragma unroll
-    for (int d = 0; d < 14; ++d) {
-      const int gi = min(max(r0 - 3 + d, 0), H - 1);
-      ra[d] = pa[(size_t)gi * W + gj];
-      rb[d] = pb[(size_t)gi * W + gj];
+      for (int d = 0; d < 14; ++d, idx += W) {
+        ra[d] = bld(qa, idx);
+        rb[d] = bld(qb, idx);
+      }
+    } else {
+#pragma unroll
+      for (int d = 0; d < 14; ++d) {
+        const int idx = min(max(r0 - 3 + d, 0), H - 1) * W + gj;
+        ra[d] = bld(qa, idx);
+        rb[d] = bld(qb, idx);
+      }
     }
     float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f, s4 = 0.f;
 #pragma unroll
@@ -1910,7 +1941,7 @@ static void launch_k2_rb(int method, hipStream_t st, const float* xn, const floa
 #define K2RB_ABL(M, A) if (g_k2_ablate == A) { hipLaunchKernelGGL((k2_blur_rb<T, M, 0, A>), grid, dim3(256), 0, st, K2RB_ARGS); return; }
   if (method == M_A && !lat && g_k2_ablate) {
     K2RB_ABL(M_A, 1) K2RB_ABL(M_A, 2) K2RB_ABL(M_A, 4) K2RB_ABL(M_A, 8) K2RB_ABL(M_A, 16) K2RB_ABL(M_A, 3)
-    K2RB_ABL(M_A, 6) K2RB_ABL(M_A, 20) K2RB_ABL(M_A, 7) K2RB_ABL(M_A, 9)
+    K2RB_ABL(M_A, 6) K2RB_ABL(M_A, 20) K2RB_ABL(M_A, 7) K2RB_ABL(M_A, 9) K2RB_ABL(M_A, 32)
   }
 #undef K2RB_ABL
 #endif

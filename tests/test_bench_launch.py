@@ -80,11 +80,11 @@ def test_cpu_baseline_fields_on_cpu():
     obs, x0 = O.make_observation(xt, "blur", h, 0.8, 0.01, 0.0, False, 300.0)
     rate, sample, psnr, info = bench.cpu_baseline(cfg, xt, obs.astype(np.float32), x0.astype(np.float32), h, 1.0, 8)
     sweep = bench.thread_sweep(info["threads_used"])
-    assert len(info["sweep"]) == 2 * len(sweep) and [r["threads"] for r in info["sweep"]][::2] == sweep
+    assert len(info["sweep"]) == 3 * len(sweep) and [r["threads"] for r in info["sweep"]] == 3 * sweep
     assert rate == max(r["rate"] for r in info["sweep"]) and rate > 0
     assert info["best_threads"] in sweep and 0 < info["median"] <= rate and info["spread"] >= 0
     assert all(r["cpu_use_of_threads"] > 0 for r in info["sweep"])
-    assert "cgroup_throttled_s" in info and "2 runs at each of" in sample
+    assert "cgroup_throttled_s" in info and "3 interleaved rounds" in sample
     assert psnr is not None and len(psnr) == info["sweep"][-1]["iters"]
 
 

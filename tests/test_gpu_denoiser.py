@@ -291,13 +291,14 @@ def test_denoiser_full_size_rgb(gpu_ctx):
                                           ("dncnn_15", 2, 1, 37, 45),                         # odd layer count
                                           ("dncnn_color_blind", 1, 3, 9, 33),                 # ReLU, tiny image
                                           ("DnCNN_nobn_nch_3_nlev_0.01", 3, 3, 256, 256)])    # 1536 tiles: 6 per WG
-def test_fp16x3_all_layers_one_launch_bit_identical(gpu_ctx, name, B, C, H, W):
+@pytest.mark.parametrize("prec", ["fp16x3", "fp16a2"])
+def test_fp16x3_all_layers_one_launch_bit_identical(gpu_ctx, name, B, C, H, W, prec):
     """conv_stack_s3 (every split-fp16 body layer in one persistent launch) gives the bits of
-    one conv_s3 launch per layer."""
+    one conv_s3 launch per layer, with (fp16x3) and without (fp16a2) the w_lo term."""
     rng = np.random.default_rng(13)
     w = DenoiserWeights.load_npz(os.path.join(WEIGHTS_DIR, name + ".npz"))
     x = rng.uniform(0, 1, (B, C, H, W)).astype(np.float32)
-    gpu_ctx.set_precision("fp16x3")
+    gpu_ctx.set_precision(prec)
     try:
         gpu_ctx.set_body_layers(1)
         single = run_denoise(gpu_ctx, w, x)

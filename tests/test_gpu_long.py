@@ -39,9 +39,12 @@ C_MIN = {"fp16": 3e-3, "fp16w2": 3e-3, "fp16x3": 1e-6, "fp32": 1e-6, "fp16a2": 1
 # x against the reference's final iterate (stored as fp16 in the golden: up to 2.4e-4 of the
 # error is the fixture's own rounding).  Measured max |dx| (r04 parity.txt, r05): fp16 / fp16w2
 # 5e-4 - 1e-3 on every non-chaotic golden (ours-B at 300 iterations: 1.9e-3, its l1-ball support
-# moving with the rounding), split fp16 / fp32 2.0-3.0e-4: bounds about 2-3x that.
+# moving with the rounding), split fp16 / fp32 2.0-3.0e-4: bounds about 2-3x that.  Two
+# goldens sit above that under split fp16 (r05 pytest_all.log): ours-C x 3000 (2.2e-3: 3000 primal
+# steps of gamma1 = 3.5e-4 integrate the split's residual error through the dual; PSNR 0.0018 dB)
+# and RED at sigma 0.04 (1.25e-3: the grid's ill-conditioned noise level, as CHAOTIC's two).
 X_TOL = {"fp16": 1.5e-3, "fp16w2": 1.5e-3, "fp16x3": 5e-4, "fp32": 5e-4, "fp16a2": 1.5e-3}
-X_TOL_CASE = {("B_blur_300", "fp16"): 4e-3}
+X_TOL_CASE = {("B_blur_300", "fp16"): 4e-3, ("C_rs_3000", "fp16x3"): 4e-3, ("RED_blur_s004_1200", "fp16x3"): 2.5e-3}
 
 
 def check_c(case, c, gc, prec):
