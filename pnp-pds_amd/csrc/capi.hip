@@ -613,12 +613,15 @@ bool want_ssim(pnp_ctx* ctx) {
   return p.record_metrics && p.record_ssim && ctx->has_true && (ctx->capturing || ctx->it < ctx->cap);
 }
 
-// mm_chunks > 0: K2 already wrote x+'s (min, max) partials to ctx->ssim_mm
-void record_ssim(pnp_ctx* ctx, const float* xn, hipStream_t st, int mm_chunks = 0) {
+// mm_chunks > 0: K2 already wrote x+'s (min, max) partials to ctx->ssim_mm.  psnr: the PSNR of
+// this iteration comes from the SSIM pass too (it loads x_true and x+ anyway): K2 then skipped its
+// x_true loads (r05 A/B at the metric: K2 0.279 -> 0.239 ms), and what k3_norm wrote from K2's
+// partials for the PSNR is overwritten here, later in the same iteration.
+void record_ssim(pnp_ctx* ctx, const float* xn, hipStream_t st, int mm_chunks = 0, bool psnr = false) {
   if (!want_ssim(ctx)) return;
   ProfScope ps(ctx, "ssim", st);
   launch_ssim(P<float>(ctx->xtrue), xn, ctx->ssim_scr.p, P<double>(ctx->metrics), ctx->B, ctx->C, ctx->H, ctx->W,
-              ctx->it, ctx->cap, st, mm_chunks > 0 ? P<float>(ctx->ssim_mm) : nullptr, mm_chunks, ctx->itp);
+              ctx->it, ctx->cap, st, mm_chunks > 0 ? P<float>(ctx->ssim_mm) : nullptr, mm_chunks, ctx->itp, psnr);
   check_launch(ctx, "ssim");
 }
 
@@ -653,6 +656,7 @@ void solver_iteration(pnp_ctx* ctx) {
   const int record = p.record_metrics && (ctx->capturing || ctx->it < ctx->cap);
   const bool fused = dual_fused(ctx, od);
   float* y = fused ? dual_buf(ctx, ctx->cur ^ 1) : P<float>(ctx->y);   // the dual K2 reads and updates
+  const bool psnr_in_ssim = want_ssim(ctx);   // the SSIM pass computes the PSNR (record_ssim)
   {
     ProfScope ps(ctx, "k1_primal_pre", st);
     if (fused)
@@ -676,7 +680,7 @@ void solver_iteration(pnp_ctx* ctx) {
     ProfScope ps(ctx, "k2_dual", st);
     const double gkl_gamma = p.my_lambda / p.gamma2;   // iteration.py:63
     mm_chunks = launch_k2(od.kind, ctx->method, xn, xo, y, P<float>(ctx->xobs),
-                          ctx->has_true ? P<float>(ctx->xtrue) : nullptr, P<float>(ctx->s), P<float>(ctx->w),
+                          ctx->has_true && !psnr_in_ssim ? P<float>(ctx->xtrue) : nullptr, P<float>(ctx->s), P<float>(ctx->w),
                           P<float>(ctx->theta), P<double>(ctx->partials), od, B, C, H, W, p.gamma2, gkl_gamma,
                           p.poisson_alpha, record, want_ssim(ctx) ? P<float>(ctx->ssim_mm) : nullptr, st);
     check_launch(ctx, "k2");
@@ -693,7 +697,7 @@ void solver_iteration(pnp_ctx* ctx) {
               l2_eps(ctx, n), P<double>(ctx->metrics), ctx->it, ctx->cap, record, ctx->has_true, st, ctx->itp);
     check_launch(ctx, "k3");
   }
-  record_ssim(ctx, xn, st, mm_chunks);
+  record_ssim(ctx, xn, st, mm_chunks, psnr_in_ssim);
   if (ctx->capturing) launch_it_advance(P<int>(ctx->it_dev), st);
   ctx->cur ^= 1;
   ctx->it += 1;

@@ -190,9 +190,12 @@ void launch_admm_poisson_step(float* x, const float* g, const float* c1, const f
 constexpr int kMetrics = 3;
 // SSIM of x against xt (utils_eval.py:9-12) into metrics[b][it][2]; scratch >= ssim_scratch_bytes
 size_t ssim_scratch_bytes(int B, int C, int H, int W);
-// mm_ext / mm_chunks: x's (min, max) partials from launch_k2, or null (then computed here)
+// mm_ext / mm_chunks: x's (min, max) partials from launch_k2, or null (then computed here).
+// psnr: also PSNR of x against xt into metrics[b][it][1], from this pass's loads (the solver's
+// ours-A/B/C path then runs K2 without x_true)
 void launch_ssim(const float* xt, const float* x, void* scratch, double* metrics, int B, int C, int H, int W,
-                 int it, int cap, hipStream_t st, const float* mm_ext = nullptr, int mm_chunks = 0, const int* itp = nullptr);
+                 int it, int cap, hipStream_t st, const float* mm_ext = nullptr, int mm_chunks = 0, const int* itp = nullptr,
+                 bool psnr = false);
 // comparisonB-2: out = k + ca*a + cb*b + cc*c + cd*d (null inputs skipped), fp64 arithmetic
 void launch_lincomb(float* out, double k, const float* a, double ca, const float* b, double cb, const float* c,
                     double cc, const float* d, double cd, size_t count, hipStream_t st);

@@ -1357,8 +1357,8 @@ __device__ __forceinline__ void rb_fill_k2_fast(float* lds, int i0, int j0, int 
 // tile's first cell (zeros in the others).
 // ABL (PNP_PROFILING build only, results wrong): phases of K2 removed for the ablation legs of
 // tools/gpu_r05_run1.sh: 1 no stencil (each output takes one LDS value), 2 no fp64 partials
-// (no metric sums, no d2), 4 no epilogue stores, 8 no halo fill, 16 no epilogue loads; 32: the
-// round-4 fp64 epilogue for ours-A (results right: an A/B leg).
+// (no metric sums, no d2), 4 no epilogue stores, 8 no halo fill, 16 no epilogue loads, 64 no
+// x_true loads (PSNR wrong, the rest right).
 template <class T, int METHOD, int LAT = 0, int ABL = 0>   // LAT: as k1_blur_rb, and all 8 epilogue rows' loads in flight
 __global__ __launch_bounds__(256) void k2_blur_rb(const float* __restrict__ xn, const float* __restrict__ xo,
                                                    float* __restrict__ y, const float* __restrict__ xobs,
@@ -1411,8 +1411,8 @@ __global__ __launch_bounds__(256) void k2_blur_rb(const float* __restrict__ xn, 
     float lo = __builtin_inff(), hi = -__builtin_inff();
     if (!(ABL & 8))
       rb_fill_k2_fast<G, LAT ? 32 : kRbFill>(lds, i0, j0, H, W, xn + (size_t)bc * plane, xo + (size_t)bc * plane,
-                                            xtrue ? xtrue + (size_t)bc * plane : nullptr, record != 0, e2, n2, t2,
-                                            lo, hi);
+                                            (xtrue && !(ABL & 64)) ? xtrue + (size_t)bc * plane : nullptr,
+                                            record != 0, e2, n2, t2, lo, hi);
     if (record) {                            // reduced here, so no fill value stays live past the fill
       e2 = wave_sum(e2);
       n2 = wave_sum(n2);
@@ -1444,17 +1444,13 @@ __global__ __launch_bounds__(256) void k2_blur_rb(const float* __restrict__ xn, 
   } else {
     rb_stencil<T>(lds, wd_fwd, g);
   }
-  // ours-A: the dual update and the l2-ball partial in float32 (round 5; ablation: the fp64
-  // partials and the fill's x_true loads together cost 27 % of the kernel); v = y + g2 Phi(.) is
-  // rounded to float32 for the state either way, and each thread's 16 terms of
-  // |v / g2 - x_obs|^2 are summed in float32 before the fixed-order fp64 reduction.  ours-B
-  // (whose sigma-0.04 golden is ill-conditioned: the float32 form moved 1.2 % of its final pixels
-  // by more than 5e-3 against 0.4 % for fp64) and ours-C's GKL prox stay in fp64.
+  // The dual update and the l2-ball partial in fp64 (v is rounded to float32 for the state).  A
+  // float32 form for ours-A measured the same time (r05 A/B on one box: 0.2717-0.2733 vs
+  // 0.2698-0.2735 ms, profiles/r05/k2_ablation.txt) and moved ours-B's ill-conditioned sigma-0.04
+  // golden, so it was not kept.
   double d2 = 0;
   {
     const float th = METHOD == M_B ? theta[b] : 0.f;
-    const float g2f = (float)gamma2, ig2f = (float)inv_g2;
-    float d2f = 0.f;
 #pragma unroll
     for (int rb = 0; rb < kRbRows; rb += EB) {
       if (!LAT) load_epi(rb);
@@ -1465,32 +1461,25 @@ __global__ __launch_bounds__(256) void k2_blur_rb(const float* __restrict__ xn, 
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
           if (q >= rw.nv(r)) break;
-          if (METHOD == M_C || METHOD == M_B || (ABL & 32)) {   // fp64 (ABL 32: the round-4 form for ours-A)
-            double gv = g[r][q];
-            if (METHOD == M_B) {
-              const float wq = wv[k][q];
-              const float sp = copysignf(fmaxf(fabsf(wq) - th, 0.f), wq);   // operators.py:98
-              gv += 2.0 * (double)sp - (double)sv[k][q];
-              so[q] = sp;
-            }
-            const double v = (double)yv[k][q] + gamma2 * gv;
-            const double ob = bv[k][q];
-            if (METHOD == M_C) {
-              const double tt = v * inv_g2 - gkl_gamma * gkl_alpha;
-              const double p = 0.5 * (tt + sqrt(tt * tt + 4.0 * gkl_gamma * ob));
-              yo[q] = (float)(v - gamma2 * p);
-            } else {
-              yo[q] = (float)v;
+          double gv = g[r][q];
+          if (METHOD == M_B) {
+            const float wq = wv[k][q];
+            const float sp = copysignf(fmaxf(fabsf(wq) - th, 0.f), wq);   // operators.py:98
+            gv += 2.0 * (double)sp - (double)sv[k][q];
+            so[q] = sp;
+          }
+          const double v = (double)yv[k][q] + gamma2 * gv;
+          const double ob = bv[k][q];
+          if (METHOD == M_C) {
+            const double tt = v * inv_g2 - gkl_gamma * gkl_alpha;
+            const double p = 0.5 * (tt + sqrt(tt * tt + 4.0 * gkl_gamma * ob));
+            yo[q] = (float)(v - gamma2 * p);
+          } else {
+            yo[q] = (float)v;
+            if (!(ABL & 2)) {
               const double dd = v * inv_g2 - ob;
               d2 += dd * dd;
             }
-            continue;
-          }
-          const float v = fmaf(g2f, g[r][q], yv[k][q]);
-          yo[q] = v;
-          if (!(ABL & 2)) {
-            const float dd = fmaf(v, ig2f, -bv[k][q]);
-            d2f = fmaf(dd, dd, d2f);
           }
         }
         const bool vec = al && rw.nv(r) == 2;
@@ -1499,7 +1488,6 @@ __global__ __launch_bounds__(256) void k2_blur_rb(const float* __restrict__ xn, 
         if (METHOD == M_B) st2g(s, rw.ix(r), so, rw.nv(r), vec);
       }
     }
-    d2 += d2f;
   }
   // d2: a wave is two thread rows (2 kRbRows tile rows) x 32 threads; a 32 x 32 cell is 16
   // threads (tx) of WPC = 32 / (2 kRbRows) waves: reduce each wave's two column halves in the
@@ -1617,9 +1605,12 @@ constexpr int kSsVW = kSsTW + 6, kSsVS = 63;      // odd LDS row stride
 // grid (tiles, B*C), block 256 = 4 waves.  Vertical pass: thread (column, 8-row segment) with
 // running sums straight from HBM/L2; horizontal pass: thread (row, 8-column segment) with
 // running sums over LDS.  ps[bc][tile] = sum of S over the tile's cropped pixels.
+// t2o (PSNR from this pass, round 5): per (bc, tile) the sum of (xt - x)^2 over the tile's own
+// pixels, from the vertical pass's loads (K2 then skips its x_true loads: 16 % of its bytes).
 __global__ __launch_bounds__(256) void ssim_rgb_kernel(const float* __restrict__ xt, const float* __restrict__ x,
-                                                       const float* __restrict__ mm, double* __restrict__ ps, int C,
-                                                       int H, int W, int tiles_x, int tiles, int chunks) {
+                                                       const float* __restrict__ mm, double* __restrict__ ps,
+                                                       double* __restrict__ t2o, int C, int H, int W, int tiles_x,
+                                                       int tiles, int chunks) {
   __shared__ float v[5][kSsTH][kSsVS];             // axis-0 window means of x, y, xx, yy, xy
   __shared__ double red[4];
   __shared__ float cst[2];
@@ -1633,6 +1624,7 @@ __global__ __launch_bounds__(256) void ssim_rgb_kernel(const float* __restrict__
   const __amdgpu_buffer_rsrc_t qa = plane_rsrc(xt + (size_t)bc * H * W, H, W);
   const __amdgpu_buffer_rsrc_t qb = plane_rsrc(x + (size_t)bc * H * W, H, W);
   // ---- vertical: columns j0-3+c (c < 62), rows i0 + 8*wv .. +8 ----
+  float se = 0.f;                                  // this thread's own pixels' sum of (xt - x)^2
   if (lane < kSsVW) {
     const int c = lane;
     const int gj = min(max(j0 - 3 + c, 0), W - 1);
@@ -1651,6 +1643,13 @@ __global__ __launch_bounds__(256) void ssim_rgb_kernel(const float* __restrict__
         const int idx = min(max(r0 - 3 + d, 0), H - 1) * W + gj;
         ra[d] = bld(qa, idx);
         rb[d] = bld(qb, idx);
+      }
+    }
+    if (t2o && c >= 3 && c < kSsTW + 3 && j0 - 3 + c < W) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float dd = ra[k + 3] - rb[k + 3];
+        se = r0 + k < H ? fmaf(dd, dd, se) : se;
       }
     }
     float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f, s4 = 0.f;
@@ -1706,12 +1705,16 @@ __global__ __launch_bounds__(256) void ssim_rgb_kernel(const float* __restrict__
   }
   const double tot = block_sum((double)acc, red);
   if (threadIdx.x == 0) ps[(size_t)bc * tiles + tile] = tot;
+  if (t2o) {
+    const double te = block_sum((double)se, red);
+    if (threadIdx.x == 0) t2o[(size_t)bc * tiles + tile] = te;
+  }
 }
 
 // grayscale: grid (ceil(H/4), B), one wave per row; rows[b][row] = mean S of the row (float32)
 __global__ __launch_bounds__(256) void ssim_gray_kernel(const float* __restrict__ xt, const float* __restrict__ x,
                                                         const float* __restrict__ mm, float* __restrict__ rows,
-                                                        int H, int W, int chunks) {
+                                                        double* __restrict__ t2o, int H, int W, int chunks) {
   const int b = blockIdx.y, row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= H) return;
   const float R = ssim_range_wave(mm, b, chunks, lane);
@@ -1730,16 +1733,35 @@ __global__ __launch_bounds__(256) void ssim_gray_kernel(const float* __restrict_
   }
   acc = wave_sum(acc);
   if (lane == 0) rows[(size_t)b * H + row] = (float)(acc / (double)(W - 6));
+  if (t2o) {                                       // PSNR: the row's sum of (xt - x)^2
+    float se = 0.f;
+    for (int j = lane; j < W; j += 64) {
+      const float dd = a[j] - e[j];
+      se = fmaf(dd, dd, se);
+    }
+    const double te = wave_sum((double)se);
+    if (lane == 0) t2o[(size_t)b * H + row] = te;
+  }
 }
 
 // per image: RGB mean over channels of (sum S / cropped count); gray mean over rows
+// t2o: PSNR (utils_eval.py:4-7) from the SSIM pass's squared-error sums, fixed order (or null)
 __global__ __launch_bounds__(256) void ssim_final_kernel(const double* __restrict__ ps, const float* __restrict__ rows,
-                                                         double* __restrict__ metrics, int C, int H, int W, int tiles,
-                                                         int gray, int it, int cap, const int* __restrict__ itp) {
+                                                         const double* __restrict__ t2o, double* __restrict__ metrics,
+                                                         int C, int H, int W, int tiles, int gray, int it, int cap,
+                                                         const int* __restrict__ itp) {
   __shared__ double red[4];
   const int b = blockIdx.x;
   if (itp) it = *itp;
   if (it >= cap) return;
+  if (t2o) {
+    const int nq = gray ? H : C * tiles;
+    double a = 0;
+    for (int q = threadIdx.x; q < nq; q += 256) a += t2o[(size_t)b * nq + q];
+    const double t2 = block_sum(a, red);
+    if (threadIdx.x == 0)
+      metrics[((size_t)b * cap + it) * kMetrics + 1] = 10.0 * log10(1.0 / (t2 / ((double)C * H * W)));
+  }
   double val;
   if (gray) {
     double a = 0;
@@ -1941,7 +1963,7 @@ static void launch_k2_rb(int method, hipStream_t st, const float* xn, const floa
 #define K2RB_ABL(M, A) if (g_k2_ablate == A) { hipLaunchKernelGGL((k2_blur_rb<T, M, 0, A>), grid, dim3(256), 0, st, K2RB_ARGS); return; }
   if (method == M_A && !lat && g_k2_ablate) {
     K2RB_ABL(M_A, 1) K2RB_ABL(M_A, 2) K2RB_ABL(M_A, 4) K2RB_ABL(M_A, 8) K2RB_ABL(M_A, 16) K2RB_ABL(M_A, 3)
-    K2RB_ABL(M_A, 6) K2RB_ABL(M_A, 20) K2RB_ABL(M_A, 7) K2RB_ABL(M_A, 9) K2RB_ABL(M_A, 32)
+    K2RB_ABL(M_A, 6) K2RB_ABL(M_A, 20) K2RB_ABL(M_A, 7) K2RB_ABL(M_A, 9) K2RB_ABL(M_A, 64)
   }
 #undef K2RB_ABL
 #endif
@@ -2200,19 +2222,22 @@ namespace pnp {
 size_t ssim_scratch_bytes(int B, int C, int H, int W) {
   const size_t n = (size_t)C * H * W;
   const int tiles = ((W + kSsTW - 1) / kSsTW) * ((H + kSsTH - 1) / kSsTH);
+  const size_t t2q = (size_t)B * (C == 1 ? H : C * tiles);
   return (size_t)B * chunk_count(n) * 2 * sizeof(float) + (size_t)B * C * tiles * sizeof(double) +
-         (size_t)B * H * sizeof(float) + 256;
+         t2q * sizeof(double) + (size_t)B * H * sizeof(float) + 256;
 }
 
 void launch_ssim(const float* xt, const float* x, void* scratch, double* metrics, int B, int C, int H, int W,
-                 int it, int cap, hipStream_t st, const float* mm_ext, int mm_chunks, const int* itp) {
+                 int it, int cap, hipStream_t st, const float* mm_ext, int mm_chunks, const int* itp, bool psnr) {
   const size_t n = (size_t)C * H * W;
   int chunks = chunk_count(n);
   const int tx = (W + kSsTW - 1) / kSsTW, tiles = tx * ((H + kSsTH - 1) / kSsTH);
   float* mm = static_cast<float*>(scratch);
   double* ps = reinterpret_cast<double*>(
       (reinterpret_cast<uintptr_t>(mm + (size_t)B * chunks * 2) + 255) & ~(uintptr_t)255);
-  float* rows = reinterpret_cast<float*>(ps + (size_t)B * C * tiles);
+  double* t2 = ps + (size_t)B * C * tiles;
+  float* rows = reinterpret_cast<float*>(t2 + (size_t)B * (C == 1 ? H : C * tiles));
+  double* t2o = psnr ? t2 : nullptr;
   if (mm_ext && mm_chunks > 0) {          // x+'s range came from K2 (one pass over x+ fewer)
     mm = const_cast<float*>(mm_ext);
     chunks = mm_chunks;
@@ -2221,12 +2246,12 @@ void launch_ssim(const float* xt, const float* x, void* scratch, double* metrics
   }
   const int gray = C == 1;
   if (gray)
-    hipLaunchKernelGGL(ssim_gray_kernel, dim3((H + 3) / 4, B), dim3(256), 0, st, xt, x, mm, rows, H, W, chunks);
+    hipLaunchKernelGGL(ssim_gray_kernel, dim3((H + 3) / 4, B), dim3(256), 0, st, xt, x, mm, rows, t2o, H, W, chunks);
   else
-    hipLaunchKernelGGL(ssim_rgb_kernel, dim3(tiles, B * C), dim3(256), 0, st, xt, x, mm, ps, C, H, W, tx, tiles,
+    hipLaunchKernelGGL(ssim_rgb_kernel, dim3(tiles, B * C), dim3(256), 0, st, xt, x, mm, ps, t2o, C, H, W, tx, tiles,
                        chunks);
-  hipLaunchKernelGGL(ssim_final_kernel, dim3(B), dim3(256), 0, st, ps, rows, metrics, C, H, W, tiles, gray, it, cap,
-                     itp);
+  hipLaunchKernelGGL(ssim_final_kernel, dim3(B), dim3(256), 0, st, ps, rows, t2o, metrics, C, H, W, tiles, gray, it,
+                     cap, itp);
 }
 
 }  // namespace pnp

@@ -22,7 +22,7 @@ def main():
     ap.add_argument("--random", action="store_true", help="uniform-random input instead of structured images")
     ap.add_argument("--ablate", type=int, default=0,
                     help="profiling build only (PNP_LIB_PATH=.../lib_prof/libpnppds.so): 1 DMA, 2 stores, 4 MFMA skipped")
-    ap.add_argument("--precision", default="fp16", choices=["fp16", "fp32", "fp16w2"])
+    ap.add_argument("--precision", default="fp16", choices=["fp16", "fp32", "fp16w2", "fp16x3", "fp16a2"])
     ap.add_argument("--body-layers", type=int, default=0)
     a = ap.parse_args()
     import torch
