@@ -306,7 +306,8 @@ def cpu_baseline(cfg, x_true, x_obs, x_0, h, budget_s, max_iter):
         return rec, res
 
     sweep = thread_sweep(info["threads_used"])
-    t_cal, _ = run(1, sweep[-1])                                   # warm-up and calibration
+    run(1, sweep[-1])                                              # warm-up (thread pool, caches)
+    t_cal, _ = run(1, sweep[-1])                                   # calibration
     per_iter = max(t_cal["iters"] / (t_cal["rate"] * scale), 1e-3)
     # three interleaved rounds over the thread counts: the host's speed drifts within a run (r05:
     # one box's calibration ran at 10 iterations/s, its later runs at 4-5; another box ran 4 and 8

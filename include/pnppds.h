@@ -175,9 +175,12 @@ enum pnp_tuning_key {
   PNP_TUNE_GRAPH = 3,         /* 1: iteration launches replayed from a hipGraph (two iterations
                                 per replay, methods A/B/C); 0: direct launches (default).
                                 Same results either way.                                       */
-  PNP_TUNE_CONVERGE_C = 4     /* (ABI 7) PNP_PREC_CONVERGE's c_n threshold in units of 1e-6
+  PNP_TUNE_CONVERGE_C = 4,    /* (ABI 7) PNP_PREC_CONVERGE's c_n threshold in units of 1e-6
                                 (default 3000 = 3e-3).  Changes when the solve switches, so it
                                 changes results (within the tolerances of DESIGN.md §4).        */
+  PNP_TUNE_FUSE_ENDS = 5      /* (ABI 7) 1 (default): when the two-layer launches run (FP16, even
+                                body depth), the head runs inside the first one and the tail
+                                inside the last; 0: separate head / tail launches.  Bit-identical. */
 };
 int pnp_set_tuning(pnp_ctx* ctx, int key, int value);
 

@@ -57,6 +57,7 @@ struct pnp_ctx {
   int den_C = 0, den_depth = 0, den_act = 0, den_residual = 1, den_clamp = 1;
   int den_chunk = 0;   // images per denoiser pass; 0 = auto
   int ablate = 0;         // PNP_PROFILING build only: parts of conv_body_v3 skipped, results wrong
+  int fuse_ends = 0;      // PNP_TUNE_FUSE_ENDS: head / tail inside the first / last pair launch
   int body_layers = 0;    // PNP_TUNE_BODY_LAYERS: 0 auto, 1 conv_body_v3, 2 conv_body_f2, 3 conv_stack16(x2), 4 conv_stack16
   bool den_ready = false;
   int prec_req = PNP_PREC_AUTO;   // pnp_set_precision (default: the per-solve policy, auto_precision)
@@ -534,7 +535,22 @@ void run_denoiser(pnp_ctx* ctx, const float* u32, float* xout, DevBuf (&act)[2],
     const bool stack_pairs = ctx->body_layers != 4;
     // the two-layer stack computes the head itself (its first pair's input halo)
     const bool head_in_stack = stack && stack16_takes_head(nbody, stack_pairs);
-    if (!head_in_stack) {
+    // head + L0 and L(n-1) + tail in the first and last pair launches (conv_body_x8_kernel's HEAD /
+    // TAIL modes): the pairs L1 .. L(n-2) between need an even body depth
+    const bool fuse = !w2 && pair && !stack && !ctx->ablate && ctx->fuse_ends && nbody >= 2 && nbody % 2 == 0 &&
+                      C <= kMaxC;
+    if (fuse) {
+      ProfScope ps(ctx, "conv_body_f2h", st);
+      X8Ends e;
+      e.u32 = xin;
+      e.hw = ctx->head_w.p;
+      e.hb = P<float>(ctx->head_b);
+      e.C = C;
+      const char* w16 = (const char*)ctx->body_w16.p;
+      launch_conv_body_f2(nullptr, P<half_t>(act[0]), w16, w16, ctx->body_w.p, ctx->body_w.p, P<float>(ctx->body_b),
+                          P<float>(ctx->body_b), s, ctx->den_act, ctx->num_cus, st, kX8Head, &e);
+      check_launch(ctx, "conv_body_f2h");
+    } else if (!head_in_stack) {
       ProfScope ps(ctx, "conv_head", st);
       launch_conv_head(xin, C, P<half_t>(act[0]), ctx->head_w.p, w2 ? ctx->head_wlo.p : nullptr, P<float>(ctx->head_b),
                        s, ctx->den_act, ctx->num_cus, 4, st);
@@ -550,7 +566,7 @@ void run_denoiser(pnp_ctx* ctx, const float* u32, float* xout, DevBuf (&act)[2],
                                 head_in_stack ? xin : nullptr, C, ctx->head_w.p, P<float>(ctx->head_b));
       check_launch(ctx, "conv_stack16");
     }
-    for (int l = stack ? nbody : 0; l < nbody;) {
+    for (int l = stack ? nbody : fuse ? 1 : 0; l < (fuse ? nbody - 1 : nbody);) {
       const char* wl = (const char*)ctx->body_w.p + (size_t)l * kBodyWBytes;
       const float* bl = P<float>(ctx->body_b) + l * kWidth;
       if (!w2 && pair && !ctx->ablate && l + 1 < nbody) {   // layers l, l+1 in one launch
@@ -578,7 +594,24 @@ void run_denoiser(pnp_ctx* ctx, const float* u32, float* xout, DevBuf (&act)[2],
       l += 1;
       cur ^= 1;
     }
-    {
+    if (fuse) {
+      ProfScope ps(ctx, "conv_body_f2t", st);
+      X8Ends e;
+      e.u32 = xin;
+      e.xout = xo;
+      e.tw = ctx->tail_w.p;
+      e.tb = P<float>(ctx->tail_b);
+      e.C = C;
+      e.residual_sign = ctx->den_residual;
+      e.clamp_out = ctx->den_clamp;
+      const size_t l = nbody - 1;
+      const char* w16 = (const char*)ctx->body_w16.p + l * kBodyWBytes;
+      const char* wl = (const char*)ctx->body_w.p + l * kBodyWBytes;
+      const float* bl = P<float>(ctx->body_b) + l * kWidth;
+      launch_conv_body_f2(P<half_t>(act[cur]), nullptr, w16, w16, wl, wl, bl, bl, s, ctx->den_act, ctx->num_cus, st,
+                          kX8Tail, &e);
+      check_launch(ctx, "conv_body_f2t");
+    } else {
       ProfScope ps(ctx, "conv_tail", st);
       launch_conv_tail(P<half_t>(act[cur]), xin, xo, ctx->tail_w.p, w2 ? ctx->tail_wlo.p : nullptr,
                        P<float>(ctx->tail_b), s, C, ctx->den_residual, ctx->den_clamp, ctx->num_cus, st);
@@ -1350,6 +1383,11 @@ int pnp_set_tuning(pnp_ctx* ctx, int key, int value) {
     if (key == PNP_TUNE_CONVERGE_C) {
       if (value < 1) fail(ctx, PNP_E_ARG, "the c_n threshold (units of 1e-6) must be >= 1");
       ctx->conv_c = value * 1e-6;
+      return;
+    }
+    if (key == PNP_TUNE_FUSE_ENDS) {
+      if (value < 0 || value > 1) fail(ctx, PNP_E_ARG, "fuse-ends must be 0 (off) or 1 (on)");
+      ctx->fuse_ends = value;
       return;
     }
     if (key == PNP_TUNE_BODY_LAYERS) {

@@ -463,14 +463,23 @@ __device__ __forceinline__ half8_t x8_act(const floatx4 (&a)[2]) {
   return o;
 }
 
-template <int ACT>
+// MODE kX8Head: layer l is the head (C -> 64, conv_head_kernel's PREC 0 arithmetic: its packed
+// weights, three v_mfma_f32_32x32x16_f16 per output from a zero accumulator over the fp16-rounded
+// input quads, bias_act8) computed into the intermediate ring from the fp32 input, which layer l's
+// waves stage as fp16 quads (18 rows x 36 pixels x 8 B) one step ahead instead of the 64-channel
+// DMA ring; layer l + 1 is the first body layer.  MODE kX8Tail: layer l + 1 is the tail
+// (conv_tail_kernel's arithmetic: 64 -> C on v_mfma_f32_16x16x32_f16 from a zero accumulator,
+// + bias, +/- the fp32 residual, clamp), storing x+ in fp32 NCHW; layer l is the last body layer.
+// Both give the bits of the separate head / tail launches around a plain pair, without the head's
+// 2.15 GB write and the tail's 2.15 GB read at the metric.
+template <int ACT, int MODE = kX8Pair>
 __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __restrict__ in,
                                                                half_t* __restrict__ out,
                                                                const uint4* __restrict__ w1,
                                                                const float* __restrict__ b1,
                                                                const uint4* __restrict__ w2,
                                                                const float* __restrict__ b2, ConvShape s,
-                                                               int strips_x, int nstrips, int sb) {
+                                                               int strips_x, int nstrips, int sb, X8Ends ends) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned char* ring = smem;
   unsigned char* mid = smem + kF2Mid;
@@ -478,17 +487,35 @@ __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __re
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int layer = wave >> 2, m = wave & 1, half = (wave >> 1) & 1;
   const int g = lane >> 4, px = lane & 15;               // chunk-in-M-tile, pixel of an N-subtile
+  const bool head_wave = MODE == kX8Head && layer == 0, tail_wave = MODE == kX8Tail && layer == 1;
   const uint4* wsrc = layer ? w2 : w1;
   half8_t wA[kX8KSteps][2];
+  if (head_wave) {                                       // conv_head's fragments of M-tile m
 #pragma unroll
-  for (int ks = 0; ks < kX8KSteps; ++ks)
+    for (int ks = 0; ks < kHeadKSteps; ++ks)
+      wA[ks][0] = *reinterpret_cast<const half8_t*>(reinterpret_cast<const unsigned char*>(ends.hw) +
+                                                    ((ks * 2 + m) * 64 + lane) * 16);
+  } else if (tail_wave) {                                // conv_tail's fragments: [ks][lane]
 #pragma unroll
-    for (int q = 0; q < 2; ++q)
-      wA[ks][q] = *reinterpret_cast<const half8_t*>(reinterpret_cast<const unsigned char*>(wsrc) +
-                                                    (((ks * 2 + m) * 2 + q) * 64 + lane) * 16);
+    for (int ks = 0; ks < kX8KSteps; ++ks)
+      wA[ks][0] = *reinterpret_cast<const half8_t*>(reinterpret_cast<const unsigned char*>(ends.tw) +
+                                                    (ks * 64 + lane) * 16);
+  } else {
+#pragma unroll
+    for (int ks = 0; ks < kX8KSteps; ++ks)
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+        wA[ks][q] = *reinterpret_cast<const half8_t*>(reinterpret_cast<const unsigned char*>(wsrc) +
+                                                      (((ks * 2 + m) * 2 + q) * 64 + lane) * 16);
+  }
   float bl[8];
+  float tbl[MODE == kX8Tail ? kMaxC : 1];
+  if (MODE == kX8Tail && tail_wave) {
 #pragma unroll
-  for (int r = 0; r < 8; ++r) bl[r] = (layer ? b2 : b1)[32 * m + 8 * g + r];
+    for (int c = 0; c < kMaxC; ++c) tbl[c % (MODE == kX8Tail ? kMaxC : 1)] = c < ends.C ? ends.tb[c] : 0.f;
+  }
+#pragma unroll
+  for (int r = 0; r < 8; ++r) bl[r] = (head_wave || tail_wave) ? 0.f : (layer ? b2 : b1)[32 * m + 8 * g + r];
   const floatx4 c0[2] = {floatx4{bl[0], bl[1], bl[2], bl[3]}, floatx4{bl[4], bl[5], bl[6], bl[7]}};   // first MFMA's C
 #ifdef X8_CLOCK   // diagnostic build (tools/x8_clock.py): shader clock vs the 100 MHz real-time clock
   unsigned long long c0_, r0_;
@@ -542,10 +569,61 @@ __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __re
       __builtin_amdgcn_raw_ptr_buffer_load_lds(dsrc, (__attribute__((address_space(3))) void*)(ddst + c * kF2InPlane),
                                                16, dvo + 16 * c, 0, 0, 0);   // (nt: 2.17 -> 2.52 ms, r03)
   };
-  for (int r = wave; r < 10; r += 8) {
-    dma_at(r - 1, 0);
+  // HEAD: the input ring holds fp16 quads of the fp32 input (channels >= C and pixels outside the
+  // image 0, as conv_head_kernel's quad()): stream row R, pixel p (column x0 - 2 + p) at
+  // ring + (f2_slot(R) * kF2InW + p) * 8.  stage_load: thread t (< 256, layer l's waves) loads the
+  // quads t and t + 256 of nrows rows from R0; stage_store writes them.
+  float sv[2][kMaxC];
+  int sslot[2];
+  auto stage_load = [&](int R0, int nrows, int kJ_) {
+    const unsigned plane = (unsigned)(s.H * s.W);
+#pragma unroll
+    for (int k2 = 0; k2 < 2; ++k2) {
+      const int q = tid + 256 * k2;
+      sslot[k2] = -1;
+      if (q >= nrows * kF2InW) continue;
+      const int R = R0 + q / kF2InW, p = q - (q / kF2InW) * kF2InW;
+      int k, r;
+      locate(R, kJ_, k, r);
+      const SGeom G = pick(k);
+      const int x = G.x0 - 2 + p;
+      const bool inside = R >= 0 && k < K && r < s.H && x >= 0 && x < s.W;
+      const __amdgpu_buffer_rsrc_t ru = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(ends.u32 + (size_t)G.b * ends.C * plane), (short)0, inside ? (int)(ends.C * plane * 4u) : 0,
+          0x00020000);
+      const unsigned o = inside ? (unsigned)(r * s.W + x) : 0u;
+#pragma unroll
+      for (int ch = 0; ch < kMaxC; ++ch)
+        sv[k2][ch] = __builtin_bit_cast(
+            float, __builtin_amdgcn_raw_buffer_load_b32(ru, ((unsigned)min(ch, ends.C - 1) * plane + o) * 4u, 0, 0));
+      sslot[k2] = (f2_slot(R) * kF2InW + p) * 8;
+      if (!inside) sslot[k2] |= 1 << 30;                   // zero quad
+    }
+  };
+  auto stage_store = [&]() {
+#pragma unroll
+    for (int k2 = 0; k2 < 2; ++k2) {
+      if (sslot[k2] < 0) continue;
+      const bool zero = (sslot[k2] >> 30) & 1;
+      _Float16 h4[4];
+#pragma unroll
+      for (int ch = 0; ch < 4; ++ch) h4[ch] = (ch < ends.C && !zero) ? (_Float16)sv[k2][ch] : (_Float16)0;
+      *reinterpret_cast<uint2*>(ring + (sslot[k2] & ~(1 << 30))) =
+          make_uint2((uint32_t)__builtin_bit_cast(uint16_t, h4[0]) | ((uint32_t)__builtin_bit_cast(uint16_t, h4[1]) << 16),
+                     (uint32_t)__builtin_bit_cast(uint16_t, h4[2]) | ((uint32_t)__builtin_bit_cast(uint16_t, h4[3]) << 16));
+    }
+  };
+  if (MODE == kX8Head) {
+    if (layer == 0) {                                      // rows -1 .. 8 of the first strip
+      stage_load(-1, 10, 0);                               // 10 x 36 = 360 quads: two per thread at most
+      stage_store();
+    }
+  } else {
+    for (int r = wave; r < 10; r += 8) {
+      dma_at(r - 1, 0);
 #pragma unroll 1
-    for (int c = 0; c < 8; ++c) dma_plane(c);
+      for (int c = 0; c < 8; ++c) dma_plane(c);
+    }
   }
   for (int q = tid; q < 8 * kF2MidW; q += 512) {
     const int c = q / kF2MidW, p = q - c * kF2MidW;
@@ -557,11 +635,65 @@ __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __re
 
   for (int J = 0; J <= K * sb; ++J) {
     auto side = [&](int ks) {                            // this wave's DMA row of the next step
+      if constexpr (MODE == kX8Head) return;             // (HEAD: layer l's waves stage the quads)
       if (ks == 0) dma_at(8 * J + 9 + wave, kJ);
       if ((ks & 1) == 0 && (ks >> 1) < 8) dma_plane(ks >> 1);
     };
     auto noside = [](int) {};
-    if (layer == 0) {
+    if (MODE == kX8Head && layer == 0) {
+      // the next step's input rows 8J+9 .. 8J+16: loads now, LDS stores after this step's MFMAs
+      if (J < K * sb) stage_load(8 * J + 9, 8, kJ);
+      else sslot[0] = sslot[1] = -1;
+      const int x0 = gcx, hh = lane >> 5, col = lane & 31;
+      if (J < K * sb && 8 * jb < s.H) {
+        // the head's bias, channels 32m + 16h .. (loaded per step: held across the loop it would
+        // stay live through layer l+1's code too, 16 VGPRs over the pair's budget)
+        float hbl[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) hbl[r] = ends.hb[32 * m + 16 * hh + r];
+        // ring-row byte offsets of input row 8J - 1 + q and mid-ring row 8J + q (q may vary by lane)
+        const int sl0 = f2_slot(8 * J - 1);
+        auto rin = [&](int q) { const int t = sl0 + q; return (t >= kF2Ring ? t - kF2Ring : t) * (kF2InW * 8); };
+        auto rmid = [&](int q) { const int t = sl0 + 1 + q; return (t >= kF2Ring ? t - kF2Ring : t) * (kF2MidW * 16); };
+        // N-tile u < 8: intermediate row u, columns x0 .. x0+31 (pixel column 1 + col); u == 8: the
+        // strip halo, lane col < 16 -> row col >> 1, column x0 - 1 or x0 + 32
+        auto htile = [&](int u) {
+          const int prow = u < 8 ? u : (col & 15) >> 1;
+          const int pcol = u < 8 ? 1 + col : ((col & 1) ? kF2MidW - 1 : 0);
+          floatx16 acc = {};
+#pragma unroll
+          for (int ks = 0; ks < kHeadKSteps; ++ks) {
+            const int t0 = 4 * ks + 2 * hh;               // this lane's two taps (k = 8hh .. 8hh+7)
+            uint2 q0 = make_uint2(0, 0), q1 = make_uint2(0, 0);
+            if (t0 < 9) q0 = *reinterpret_cast<const uint2*>(ring + rin(prow + t0 / 3) + (pcol + t0 % 3) * 8);
+            if (t0 + 1 < 9)
+              q1 = *reinterpret_cast<const uint2*>(ring + rin(prow + (t0 + 1) / 3) + (pcol + (t0 + 1) % 3) * 8);
+            const uint4 q = make_uint4(q0.x, q0.y, q1.x, q1.y);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wA[ks][0], *reinterpret_cast<const half8_t*>(&q), acc, 0, 0, 0);
+          }
+          half8_t v0 = bias_act8<ACT>(acc, 0, hbl), v1 = bias_act8<ACT>(acc, 8, hbl + 8);
+          const int x = x0 - 1 + pcol;
+          if (!(8 * jb + prow < s.H && x >= 0 && x < s.W)) v0 = v1 = half8_t{};   // the next layer's zero padding
+          if (u < 8 || col < 16) {
+            unsigned char* dst = mid + rmid(prow) + pcol * 16;
+            *reinterpret_cast<half8_t*>(dst + (4 * m + 2 * hh) * kF2MidPlane) = v0;
+            *reinterpret_cast<half8_t*>(dst + (4 * m + 2 * hh + 1) * kF2MidPlane) = v1;
+          }
+        };
+        if (half == 0) {
+          htile(0); htile(1); htile(2); htile(3); htile(8);
+        } else {
+          htile(4); htile(5); htile(6); htile(7);
+        }
+      } else {
+        for (int q = lane; q < 4 * kF2MidW * 4; q += 64) {
+          const int c = q / (4 * kF2MidW), p = q - c * (4 * kF2MidW), rr = p / kF2MidW, pc = p - rr * kF2MidW;
+          *reinterpret_cast<v4i_t*>(mid + (4 * m + c) * kF2MidPlane +
+                                    (f2_slot(8 * J + 4 * half + rr) * kF2MidW + pc) * 16) = v4i_t{0, 0, 0, 0};
+        }
+      }
+      stage_store();
+    } else if (layer == 0) {
       const int x0 = gcx;
       if (J < K * sb && 8 * jb < s.H) {
         int sl = f2_slot(8 * J - 1);
@@ -643,6 +775,81 @@ __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __re
         }
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else if (MODE == kX8Tail) {
+      if (J > 0) {
+        // the tail on output rows 8J-9 + 4 half + i, i = 0..3, columns 16 m .. 16 m + 15 (one
+        // N-subtile each): 64 -> C (A rows = output channels, c >= C zero), K order as conv_tail
+        int sl = f2_slot(8 * J - 10 + 4 * half);
+        int rowoff[6];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) {
+          rowoff[q] = sl * (kF2MidW * 16);
+          sl = sl == kF2Ring - 1 ? 0 : sl + 1;
+        }
+        const int lb = g * kF2MidPlane + px * 16;
+        int av[4][3];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int dy = 0; dy < 3; ++dy) {
+            av[i][dy] = (int)(size_t)mid + lb + rowoff[i + dy] + 16 * 16 * m;
+            asm volatile("" : "+v"(av[i][dy]));
+          }
+        // the residual input (lanes 0..15: pixel px of N-subtile i), loaded before the DMA
+        const unsigned plane = (unsigned)(s.H * s.W);
+        float xi[4][kMaxC];
+        __amdgpu_buffer_rsrc_t ro[4];
+        unsigned toff[4];
+        int bimg[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int R = 8 * J - 9 + 4 * half + i;
+          int k, r;
+          locate(R, kJ, k, r);
+          const SGeom G = pick(k);
+          bimg[i] = G.b;
+          const int x = G.x0 + 16 * m + px;
+          const bool ok = R >= 0 && k < K && r < s.H && x < s.W && lane < 16;
+          toff[i] = ok ? (unsigned)(r * s.W + x) * 4u : 0x80000000u;       // out of range: dropped
+          ro[i] = __builtin_amdgcn_make_buffer_rsrc((void*)(ends.u32 + (size_t)G.b * ends.C * plane), (short)0,
+                                                    (int)(ends.C * plane * 4u), 0x00020000);
+#pragma unroll
+          for (int c = 0; c < kMaxC; ++c)
+            xi[i][c] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                      ro[i], toff[i] + (unsigned)min(c, ends.C - 1) * plane * 4u, 0, 0));
+        }
+        __builtin_amdgcn_sched_barrier(0);               // the residual loads stay older than the DMA
+        typedef const __attribute__((address_space(3))) half8_t* lds_h8p;
+        floatx4 acc[4] = {};
+#pragma unroll
+        for (int ks = 0; ks < kX8KSteps; ++ks) {
+          const int tap = ks >> 1, hs = ks & 1, dy = tap / 3, dx = tap - 3 * dy;
+          half8_t fb[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) fb[i] = *(lds_h8p)(size_t)(unsigned)(av[i][dy] + (4 * hs * kF2MidPlane + 16 * dx));
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wA[ks][0], fb[i], acc[i], 0, 0, 0);
+          side(ks);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int c = 0; c < kMaxC; ++c) {
+            const float nc = acc[i][c] + tbl[c];
+            float o = ends.residual_sign > 0 ? nc + xi[i][c] : xi[i][c] - nc;
+            if (ends.clamp_out) o = fminf(fmaxf(o, 0.f), 1.f);
+            __builtin_amdgcn_raw_buffer_store_b32(
+                __builtin_bit_cast(int, o),
+                __builtin_amdgcn_make_buffer_rsrc((void*)(ends.xout + ((size_t)bimg[i] * ends.C + (c < ends.C ? c : 0)) * plane),
+                                                  (short)0, c < ends.C ? (int)(plane * 4u) : 0, 0x00020000),
+                toff[i], 0, kNtTail);
+          }
+        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");   // the DMAs (older than the 16 stores) landed
+      } else {
+#pragma unroll 1
+        for (int ks = 0; ks < kX8KSteps; ++ks) side(ks);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
     } else {
       if (J > 0) {
         // output rows 8J-9 + 4 half + t, t = 0..3: N-subtiles (t, column half), two per group
@@ -722,14 +929,18 @@ __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __re
 #endif
 }
 
-template __global__ void conv_body_x8_kernel<0>(const half_t* __restrict__, half_t* __restrict__,
-                                                const uint4* __restrict__, const float* __restrict__,
-                                                const uint4* __restrict__, const float* __restrict__, ConvShape,
-                                                int, int, int);
-template __global__ void conv_body_x8_kernel<1>(const half_t* __restrict__, half_t* __restrict__,
-                                                const uint4* __restrict__, const float* __restrict__,
-                                                const uint4* __restrict__, const float* __restrict__, ConvShape,
-                                                int, int, int);
+#define PNP_X8_INST(A, M)                                                                                      \
+  template __global__ void conv_body_x8_kernel<A, M>(const half_t* __restrict__, half_t* __restrict__,        \
+                                                     const uint4* __restrict__, const float* __restrict__,   \
+                                                     const uint4* __restrict__, const float* __restrict__,   \
+                                                     ConvShape, int, int, int, X8Ends);
+PNP_X8_INST(0, kX8Pair)
+PNP_X8_INST(1, kX8Pair)
+PNP_X8_INST(0, kX8Head)
+PNP_X8_INST(1, kX8Head)
+PNP_X8_INST(0, kX8Tail)
+PNP_X8_INST(1, kX8Tail)
+#undef PNP_X8_INST
 
 // ------------------------------------------------------------------------------------
 // Body layer with split weights (PNP_PREC_FP16W2): W = W_hi + W_lo, both fp16 (W_lo =
@@ -1728,7 +1939,9 @@ hipError_t conv_kernels_init() {
     e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kV3Lds);
     if (e != hipSuccess) return e;
   }
-  for (const void* k : {(const void*)conv_body_x8_kernel<0>, (const void*)conv_body_x8_kernel<1>}) {
+  for (const void* k : {(const void*)conv_body_x8_kernel<0, kX8Pair>, (const void*)conv_body_x8_kernel<1, kX8Pair>,
+                        (const void*)conv_body_x8_kernel<0, kX8Head>, (const void*)conv_body_x8_kernel<1, kX8Head>,
+                        (const void*)conv_body_x8_kernel<0, kX8Tail>, (const void*)conv_body_x8_kernel<1, kX8Tail>}) {
     e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kF2Lds);
     if (e != hipSuccess) return e;
   }
@@ -1777,17 +1990,28 @@ void launch_conv_head(const float* in32, int C, half_t* out, const void* w, cons
 // git history before round 3; DESIGN.md §3 keeps their measurements.)
 void launch_conv_body_f2(const half_t* in, half_t* out, const void* w16_1, const void* w16_2, const void* w32_1,
                          const void* w32_2, const float* b1, const float* b2, const ConvShape& s, int act,
-                         int num_cus, hipStream_t st) {
+                         int num_cus, hipStream_t st, int mode, const X8Ends* ends) {
   const int strips_x = (s.W + kTileW - 1) / kTileW, nstrips = s.B * strips_x;
-  const int sb = (s.H + 1 + 7) / 8;                         // 8-row blocks per strip: S = 8 sb >= H + 1
+  // 8-row blocks per strip: S = 8 sb >= H + 1, and >= 16 so that a step's lookahead rows (up to
+  // 8 J + 16) lie at most one strip ahead (locate())
+  const int sb = (s.H + 1 + 7) / 8 < 2 ? 2 : (s.H + 1 + 7) / 8;
   const int grid = nstrips < num_cus ? nstrips : num_cus;
+  const X8Ends e = ends ? *ends : X8Ends{};
 #define F2_LAUNCH(KERN, NT, W1, W2)                                                                              \
   hipLaunchKernelGGL((KERN), dim3(grid), dim3(NT), kF2Lds, st, in, out, (const uint4*)(W1), b1, (const uint4*)(W2), \
-                     b2, s, strips_x, nstrips, sb)
-  if (act == 0) F2_LAUNCH(conv_body_x8_kernel<0>, 512, w16_1, w16_2);
-  else F2_LAUNCH(conv_body_x8_kernel<1>, 512, w16_1, w16_2);
+                     b2, s, strips_x, nstrips, sb, e)
+  if (mode == kX8Head) {
+    if (act == 0) F2_LAUNCH((conv_body_x8_kernel<0, kX8Head>), 512, w16_1, w16_2);
+    else F2_LAUNCH((conv_body_x8_kernel<1, kX8Head>), 512, w16_1, w16_2);
+  } else if (mode == kX8Tail) {
+    if (act == 0) F2_LAUNCH((conv_body_x8_kernel<0, kX8Tail>), 512, w16_1, w16_2);
+    else F2_LAUNCH((conv_body_x8_kernel<1, kX8Tail>), 512, w16_1, w16_2);
+  } else {
+    if (act == 0) F2_LAUNCH((conv_body_x8_kernel<0, kX8Pair>), 512, w16_1, w16_2);
+    else F2_LAUNCH((conv_body_x8_kernel<1, kX8Pair>), 512, w16_1, w16_2);
+  }
 #undef F2_LAUNCH
-  (void)w16_1; (void)w16_2; (void)w32_1; (void)w32_2;
+  (void)w32_1; (void)w32_2;
 }
 
 void launch_conv_body_w2(const half_t* in, half_t* out, const void* w, const void* w_lo, const float* bias,

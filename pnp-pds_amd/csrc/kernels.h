@@ -38,10 +38,27 @@ void set_k2_ablate(int bits);
 void launch_conv_tail(const half_t* in, const float* xin, float* xout, const void* w, const void* w_lo,
                       const float* bias, const ConvShape& s, int C, int residual_sign, int clamp_out, int num_cus,
                       hipStream_t st);
-// two 64 -> 64 layers in one launch, streamed down 32-pixel column strips (needs pad >= 2)
+// The denoiser's ends inside the first / last two-layer launch (round 5): HEAD = the head layer
+// (C -> 64, from the fp32 NCHW input u32) and the first body layer; TAIL = the last body layer and
+// the tail (64 -> C + residual + clamp, fp32 NCHW out).  Bit-identical to the separate
+// conv_head / conv_tail launches around plain pairs.
+struct X8Ends {
+  const float* u32 = nullptr;     // HEAD: the denoiser input; TAIL: the residual input
+  const void* hw = nullptr;       // HEAD: conv_head's packed weights (pack_head_weights)
+  const float* hb = nullptr;
+  float* xout = nullptr;          // TAIL: the output x+
+  const void* tw = nullptr;       // TAIL: packed tail weights (pack_tail_weights)
+  const float* tb = nullptr;
+  int C = 0, residual_sign = 1, clamp_out = 1;
+};
+enum X8Mode { kX8Pair = 0, kX8Head = 1, kX8Tail = 2 };
+// two 64 -> 64 layers in one launch, streamed down 32-pixel column strips (needs pad >= 2);
+// mode kX8Head: in is not read, layer 1 is the head (ends: u32, C, hw, hb; w16_1 / b1 unused);
+// mode kX8Tail: out is not written, layer 2 is the tail (ends: u32, xout, C, tw, tb, residual_sign,
+// clamp_out; w16_2 / b2 unused)
 void launch_conv_body_f2(const half_t* in, half_t* out, const void* w16_1, const void* w16_2, const void* w32_1,
                          const void* w32_2, const float* b1, const float* b2, const ConvShape& s, int act,
-                         int num_cus, hipStream_t st);
+                         int num_cus, hipStream_t st, int mode = kX8Pair, const X8Ends* ends = nullptr);
 // all nbody 64 -> 64 layers in one launch for small batches (grid = min(tiles, CUs)); returns
 // where the result is (0: a, 1: b).  pairs: two layers per hand-off (conv_stack16x2, even
 // nbody), else one.  done: s.tiles progress words (zeroed once), epoch: this launch's tag

@@ -31,6 +31,7 @@ TUNE_DENOISE_CHUNK = 1
 TUNE_BODY_LAYERS = 2
 TUNE_GRAPH = 3
 TUNE_CONVERGE_C = 4      # PNP_PREC_CONVERGE's c_n threshold, units of 1e-6 (ABI 7)
+TUNE_FUSE_ENDS = 5       # head / tail inside the first / last two-layer launch (ABI 7)
 TUNE_ABLATE_K2 = 98      # profiling build only: k2_blur_rb ablation legs (ops.hip ABL bits)
 TUNE_ABLATE = 99         # profiling build only (make PROFILING=1, lib_prof/): not in include/pnppds.h
 
@@ -292,6 +293,11 @@ class Context:
         CU), 1, 2, 3 (all, two layers per tile hand-off) or 4 (all, one per hand-off).  Same bits
         either way."""
         self._check(self.lib.pnp_set_tuning(self.h, TUNE_BODY_LAYERS, int(n)))
+
+    def set_fuse_ends(self, on: int):
+        """1 (default): with the two-layer launches (FP16, even body depth) the head runs inside
+        the first one and the tail inside the last; 0: separate head / tail launches.  Same bits."""
+        self._check(self.lib.pnp_set_tuning(self.h, TUNE_FUSE_ENDS, int(on)))
 
     def set_ablate(self, bits: int):
         """Profiling build only (make PROFILING=1, PNP_LIB_PATH=.../lib_prof/libpnppds.so;

@@ -245,6 +245,38 @@ def test_body_two_layers_per_launch_bit_identical(gpu_ctx, name, B, C, H, W):
     np.testing.assert_array_equal(fused, single)
 
 
+@pytest.mark.parametrize("depth,act,residual,clamp,B,C,H,W",
+                         [(20, 0, +1, 1, 2, 3, 256, 256), (20, 0, +1, 1, 3, 3, 50, 70), (6, 1, -1, 0, 2, 1, 37, 45),
+                          (6, 0, +1, 1, 1, 1, 8, 32), (4, 1, -1, 0, 1, 3, 9, 33), (20, 1, +1, 0, 90, 3, 20, 70),
+                          (6, 0, -1, 1, 300, 1, 9, 33), (8, 0, +1, 1, 5, 3, 64, 96),
+                          (6, 0, +1, 1, 40, 3, 5, 40)])      # H < 8: strips padded to 16 rows
+def test_head_tail_inside_pair_launches_bit_identical(gpu_ctx, depth, act, residual, clamp, B, C, H, W):
+    """conv_body_x8_kernel's HEAD / TAIL modes (the head inside the first two-layer launch, the
+    tail inside the last: PNP_TUNE_FUSE_ENDS) give the separate conv_head / conv_tail launches'
+    bits: both activations, both residual signs, clamp on / off, ragged shapes, images narrower
+    than a strip, several strips per workgroup."""
+    rng = np.random.default_rng(depth * 7 + B)
+    w = random_weights(C, depth=depth, seed=B + H, scale=0.9)
+    w.act, w.residual, w.clamp_io = act, residual, clamp
+    x = rng.uniform(-0.1, 1.1, (B, C, H, W)).astype(np.float32)
+    if clamp:
+        x = np.clip(x, 0, 1)
+    try:
+        gpu_ctx.set_body_layers(2)
+        gpu_ctx.set_fuse_ends(0)
+        apart = run_denoise(gpu_ctx, w, x)
+        gpu_ctx.set_fuse_ends(1)
+        fused = run_denoise(gpu_ctx, w, x)
+        fused2 = run_denoise(gpu_ctx, w, x)
+    finally:
+        gpu_ctx.set_body_layers(0)
+        gpu_ctx.set_fuse_ends(1)
+    np.testing.assert_array_equal(fused, apart)
+    np.testing.assert_array_equal(fused2, apart)
+    emu = O.OracleDenoiser(w, emulate_fp16=True).forward_batch(x[:1])
+    np.testing.assert_allclose(fused[:1], emu, atol=TOL_VS_FP16_EMU)
+
+
 @pytest.mark.parametrize("name,B,C,H,W", [("DnCNN_nobn_nch_3_nlev_0.01", 1, 3, 256, 256),     # 256 tiles: 1 per CU
                                           ("DnCNN_nobn_nch_1_nlev_0.01", 2, 1, 256, 256),     # 512: 2 per workgroup
                                           ("DnCNN_nobn_nch_3_nlev_0.01", 3, 3, 256, 256),     # 768: 3 per workgroup

@@ -24,6 +24,7 @@ def main():
                     help="profiling build only (PNP_LIB_PATH=.../lib_prof/libpnppds.so): 1 DMA, 2 stores, 4 MFMA skipped")
     ap.add_argument("--precision", default="fp16", choices=["fp16", "fp32", "fp16w2", "fp16x3", "fp16a2"])
     ap.add_argument("--body-layers", type=int, default=0)
+    ap.add_argument("--fuse-ends", type=int, default=1, help="0: separate head / tail launches")
     a = ap.parse_args()
     import torch
     from pnppds import _lib
@@ -36,6 +37,7 @@ def main():
         ctx.set_ablate(a.ablate)
     if a.body_layers:
         ctx.set_body_layers(a.body_layers)
+    ctx.set_fuse_ends(a.fuse_ends)
     B, C, H, W = a.batch, 3, a.size, a.size
     if a.random:
         x = torch.rand((B, C, H, W), device="cuda:0")
