@@ -57,7 +57,7 @@ struct pnp_ctx {
   int den_C = 0, den_depth = 0, den_act = 0, den_residual = 1, den_clamp = 1;
   int den_chunk = 0;   // images per denoiser pass; 0 = auto
   int ablate = 0;         // PNP_PROFILING build only: parts of conv_body_v3 skipped, results wrong
-  int fuse_ends = 0;      // PNP_TUNE_FUSE_ENDS: head / tail inside the first / last pair launch
+  int fuse_ends = 1;      // PNP_TUNE_FUSE_ENDS: head / tail inside the first / last pair launch
   int body_layers = 0;    // PNP_TUNE_BODY_LAYERS: 0 auto, 1 conv_body_v3, 2 conv_body_f2, 3 conv_stack16(x2), 4 conv_stack16
   bool den_ready = false;
   int prec_req = PNP_PREC_AUTO;   // pnp_set_precision (default: the per-solve policy, auto_precision)

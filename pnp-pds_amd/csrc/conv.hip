@@ -392,6 +392,7 @@ __device__ __forceinline__ int f2_slot(int row) { return (row + 1 + 18 * 64) % k
 // Weights: pack_body_weights16, [18 ks][2 M-tiles][2 subtiles][64 lanes][8 x f16].
 // ------------------------------------------------------------------------------------
 constexpr int kX8KSteps = 18;
+constexpr int kX8HeadFrag = 8192;     // HEAD mode: the head's fragments in the (quad-sized) input ring's LDS
 // Non-temporal output stores (A/B at the metric, r03, ms per launch): the head's 0.446 -> 0.439
 // (kept); conv_body_x8 2.248 -> 2.267 and the tail unchanged (not kept).
 constexpr int kNtX8 = 0, kNtTail = 0;                          // buffer-store cache policy (2 = nt)
@@ -487,35 +488,25 @@ __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __re
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int layer = wave >> 2, m = wave & 1, half = (wave >> 1) & 1;
   const int g = lane >> 4, px = lane & 15;               // chunk-in-M-tile, pixel of an N-subtile
-  const bool head_wave = MODE == kX8Head && layer == 0, tail_wave = MODE == kX8Tail && layer == 1;
-  const uint4* wsrc = layer ? w2 : w1;
+  // HEAD: every wave runs L0 (M-tile m) and a share of the head, whose fragments sit in LDS;
+  // TAIL: every wave runs L(n-1) and a share of the tail, whose fragments stream from L2
+  const uint4* wsrc = MODE == kX8Head ? w2 : MODE == kX8Tail ? w1 : layer ? w2 : w1;
   half8_t wA[kX8KSteps][2];
-  if (head_wave) {                                       // conv_head's fragments of M-tile m
 #pragma unroll
-    for (int ks = 0; ks < kHeadKSteps; ++ks)
-      wA[ks][0] = *reinterpret_cast<const half8_t*>(reinterpret_cast<const unsigned char*>(ends.hw) +
-                                                    ((ks * 2 + m) * 64 + lane) * 16);
-  } else if (tail_wave) {                                // conv_tail's fragments: [ks][lane]
+  for (int ks = 0; ks < kX8KSteps; ++ks)
 #pragma unroll
-    for (int ks = 0; ks < kX8KSteps; ++ks)
-      wA[ks][0] = *reinterpret_cast<const half8_t*>(reinterpret_cast<const unsigned char*>(ends.tw) +
-                                                    (ks * 64 + lane) * 16);
-  } else {
-#pragma unroll
-    for (int ks = 0; ks < kX8KSteps; ++ks)
-#pragma unroll
-      for (int q = 0; q < 2; ++q)
-        wA[ks][q] = *reinterpret_cast<const half8_t*>(reinterpret_cast<const unsigned char*>(wsrc) +
-                                                      (((ks * 2 + m) * 2 + q) * 64 + lane) * 16);
-  }
+    for (int q = 0; q < 2; ++q)
+      wA[ks][q] = *reinterpret_cast<const half8_t*>(reinterpret_cast<const unsigned char*>(wsrc) +
+                                                    (((ks * 2 + m) * 2 + q) * 64 + lane) * 16);
   float bl[8];
   float tbl[MODE == kX8Tail ? kMaxC : 1];
-  if (MODE == kX8Tail && tail_wave) {
+  if (MODE == kX8Tail) {
 #pragma unroll
     for (int c = 0; c < kMaxC; ++c) tbl[c % (MODE == kX8Tail ? kMaxC : 1)] = c < ends.C ? ends.tb[c] : 0.f;
   }
 #pragma unroll
-  for (int r = 0; r < 8; ++r) bl[r] = (head_wave || tail_wave) ? 0.f : (layer ? b2 : b1)[32 * m + 8 * g + r];
+  for (int r = 0; r < 8; ++r)
+    bl[r] = (MODE == kX8Head ? b2 : MODE == kX8Tail ? b1 : layer ? b2 : b1)[32 * m + 8 * g + r];
   const floatx4 c0[2] = {floatx4{bl[0], bl[1], bl[2], bl[3]}, floatx4{bl[4], bl[5], bl[6], bl[7]}};   // first MFMA's C
 #ifdef X8_CLOCK   // diagnostic build (tools/x8_clock.py): shader clock vs the 100 MHz real-time clock
   unsigned long long c0_, r0_;
@@ -571,53 +562,49 @@ __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __re
   };
   // HEAD: the input ring holds fp16 quads of the fp32 input (channels >= C and pixels outside the
   // image 0, as conv_head_kernel's quad()): stream row R, pixel p (column x0 - 2 + p) at
-  // ring + (f2_slot(R) * kF2InW + p) * 8.  stage_load: thread t (< 256, layer l's waves) loads the
-  // quads t and t + 256 of nrows rows from R0; stage_store writes them.
-  float sv[2][kMaxC];
-  int sslot[2];
+  // ring + (f2_slot(R) * kF2InW + p) * 8 (5 184 B of the ring's LDS; the head's fragments follow
+  // at hfr).  stage_load: thread t loads quad t of nrows rows from R0 (nrows <= 14);
+  // stage_store writes it.
+  unsigned char* hfr = ring + kX8HeadFrag;
+  float sv[kMaxC];
+  int sslot = -1;
   auto stage_load = [&](int R0, int nrows, int kJ_) {
     const unsigned plane = (unsigned)(s.H * s.W);
+    const int q = tid;
+    sslot = -1;
+    if (q >= nrows * kF2InW) return;
+    const int R = R0 + q / kF2InW, p = q - (q / kF2InW) * kF2InW;
+    int k, r;
+    locate(R, kJ_, k, r);
+    const SGeom G = pick(k);
+    const int x = G.x0 - 2 + p;
+    const bool inside = R >= 0 && k < K && r < s.H && x >= 0 && x < s.W;
+    const __amdgpu_buffer_rsrc_t ru = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(ends.u32 + (size_t)G.b * ends.C * plane), (short)0, inside ? (int)(ends.C * plane * 4u) : 0,
+        0x00020000);
+    const unsigned o = inside ? (unsigned)(r * s.W + x) : 0u;
 #pragma unroll
-    for (int k2 = 0; k2 < 2; ++k2) {
-      const int q = tid + 256 * k2;
-      sslot[k2] = -1;
-      if (q >= nrows * kF2InW) continue;
-      const int R = R0 + q / kF2InW, p = q - (q / kF2InW) * kF2InW;
-      int k, r;
-      locate(R, kJ_, k, r);
-      const SGeom G = pick(k);
-      const int x = G.x0 - 2 + p;
-      const bool inside = R >= 0 && k < K && r < s.H && x >= 0 && x < s.W;
-      const __amdgpu_buffer_rsrc_t ru = __builtin_amdgcn_make_buffer_rsrc(
-          (void*)(ends.u32 + (size_t)G.b * ends.C * plane), (short)0, inside ? (int)(ends.C * plane * 4u) : 0,
-          0x00020000);
-      const unsigned o = inside ? (unsigned)(r * s.W + x) : 0u;
-#pragma unroll
-      for (int ch = 0; ch < kMaxC; ++ch)
-        sv[k2][ch] = __builtin_bit_cast(
-            float, __builtin_amdgcn_raw_buffer_load_b32(ru, ((unsigned)min(ch, ends.C - 1) * plane + o) * 4u, 0, 0));
-      sslot[k2] = (f2_slot(R) * kF2InW + p) * 8;
-      if (!inside) sslot[k2] |= 1 << 30;                   // zero quad
-    }
+    for (int ch = 0; ch < kMaxC; ++ch)
+      sv[ch] = __builtin_bit_cast(
+          float, __builtin_amdgcn_raw_buffer_load_b32(ru, ((unsigned)min(ch, ends.C - 1) * plane + o) * 4u, 0, 0));
+    sslot = (f2_slot(R) * kF2InW + p) * 8;
+    if (!inside) sslot |= 1 << 30;                         // zero quad
   };
   auto stage_store = [&]() {
+    if (sslot < 0) return;
+    const bool zero = (sslot >> 30) & 1;
+    _Float16 h4[4];
 #pragma unroll
-    for (int k2 = 0; k2 < 2; ++k2) {
-      if (sslot[k2] < 0) continue;
-      const bool zero = (sslot[k2] >> 30) & 1;
-      _Float16 h4[4];
-#pragma unroll
-      for (int ch = 0; ch < 4; ++ch) h4[ch] = (ch < ends.C && !zero) ? (_Float16)sv[k2][ch] : (_Float16)0;
-      *reinterpret_cast<uint2*>(ring + (sslot[k2] & ~(1 << 30))) =
-          make_uint2((uint32_t)__builtin_bit_cast(uint16_t, h4[0]) | ((uint32_t)__builtin_bit_cast(uint16_t, h4[1]) << 16),
-                     (uint32_t)__builtin_bit_cast(uint16_t, h4[2]) | ((uint32_t)__builtin_bit_cast(uint16_t, h4[3]) << 16));
-    }
+    for (int ch = 0; ch < 4; ++ch) h4[ch] = (ch < ends.C && !zero) ? (_Float16)sv[ch] : (_Float16)0;
+    *reinterpret_cast<uint2*>(ring + (sslot & ~(1 << 30))) =
+        make_uint2((uint32_t)__builtin_bit_cast(uint16_t, h4[0]) | ((uint32_t)__builtin_bit_cast(uint16_t, h4[1]) << 16),
+                   (uint32_t)__builtin_bit_cast(uint16_t, h4[2]) | ((uint32_t)__builtin_bit_cast(uint16_t, h4[3]) << 16));
   };
   if (MODE == kX8Head) {
-    if (layer == 0) {                                      // rows -1 .. 8 of the first strip
-      stage_load(-1, 10, 0);                               // 10 x 36 = 360 quads: two per thread at most
-      stage_store();
-    }
+    stage_load(-1, 10, 0);                                 // rows -1 .. 8 of the first strip: 360 quads
+    stage_store();
+    for (int i = tid; i < kHeadKSteps * 2 * 64; i += 512)  // conv_head's packed fragments, [ks][m][lane]
+      *reinterpret_cast<uint4*>(hfr + 16 * i) = reinterpret_cast<const uint4*>(ends.hw)[i];
   } else {
     for (int r = wave; r < 10; r += 8) {
       dma_at(r - 1, 0);
@@ -631,7 +618,7 @@ __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __re
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (layer == 1) __builtin_amdgcn_s_setprio(1);   // layer l+1's waves (4-7, the second-dispatched half)
+  if (MODE == kX8Pair && layer == 1) __builtin_amdgcn_s_setprio(1);   // layer l+1's waves (4-7, the second-dispatched half)
 
   for (int J = 0; J <= K * sb; ++J) {
     auto side = [&](int ks) {                            // this wave's DMA row of the next step
@@ -640,61 +627,133 @@ __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __re
       if ((ks & 1) == 0 && (ks >> 1) < 8) dma_plane(ks >> 1);
     };
     auto noside = [](int) {};
-    if (MODE == kX8Head && layer == 0) {
-      // the next step's input rows 8J+9 .. 8J+16: loads now, LDS stores after this step's MFMAs
+    if constexpr (MODE == kX8Head) {
+      // every wave: a share of the head's N-tiles (intermediate rows 8J .. 8J+7), then two of L0's
+      // output rows (8J-9 + 2 qr, + 1); quads of the next step's input rows staged around them
+      const int qr = wave >> 1;                            // quarter: 0 .. 3
       if (J < K * sb) stage_load(8 * J + 9, 8, kJ);
-      else sslot[0] = sslot[1] = -1;
+      else sslot = -1;
       const int x0 = gcx, hh = lane >> 5, col = lane & 31;
-      if (J < K * sb && 8 * jb < s.H) {
-        // the head's bias, channels 32m + 16h .. (loaded per step: held across the loop it would
-        // stay live through layer l+1's code too, 16 VGPRs over the pair's budget)
-        float hbl[16];
+      auto head_part = [&]() {
+        if (J < K * sb && 8 * jb < s.H) {
+          float hbl[16];                                   // channels 32m + 16h .. (per step: short-lived)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) hbl[r] = ends.hb[32 * m + 16 * hh + r];
-        // ring-row byte offsets of input row 8J - 1 + q and mid-ring row 8J + q (q may vary by lane)
-        const int sl0 = f2_slot(8 * J - 1);
-        auto rin = [&](int q) { const int t = sl0 + q; return (t >= kF2Ring ? t - kF2Ring : t) * (kF2InW * 8); };
-        auto rmid = [&](int q) { const int t = sl0 + 1 + q; return (t >= kF2Ring ? t - kF2Ring : t) * (kF2MidW * 16); };
-        // N-tile u < 8: intermediate row u, columns x0 .. x0+31 (pixel column 1 + col); u == 8: the
-        // strip halo, lane col < 16 -> row col >> 1, column x0 - 1 or x0 + 32
-        auto htile = [&](int u) {
-          const int prow = u < 8 ? u : (col & 15) >> 1;
-          const int pcol = u < 8 ? 1 + col : ((col & 1) ? kF2MidW - 1 : 0);
-          floatx16 acc = {};
+          for (int r = 0; r < 16; ++r) hbl[r] = ends.hb[32 * m + 16 * hh + r];
+          // ring-row byte offsets of input row 8J - 1 + q and mid-ring row 8J + q (q may vary by lane)
+          const int sl0 = f2_slot(8 * J - 1);
+          auto rin = [&](int q) { const int t = sl0 + q; return (t >= kF2Ring ? t - kF2Ring : t) * (kF2InW * 8); };
+          auto rmid = [&](int q) { const int t = sl0 + 1 + q; return (t >= kF2Ring ? t - kF2Ring : t) * (kF2MidW * 16); };
+          typedef const __attribute__((address_space(3))) half8_t* lds_h8p;
+          // N-tile u < 8: intermediate row u, columns x0 .. x0+31 (pixel column 1 + col); u == 8: the
+          // strip halo, lane col < 16 -> row col >> 1, column x0 - 1 or x0 + 32.  NT tiles' MFMA
+          // chains interleaved.
+          auto htiles = [&](auto ntc, int ua, int ub, int uc) {
+            constexpr int NT = decltype(ntc)::value;
+            int uu[NT], prow[NT], pcol[NT];
+            floatx16 acc[NT];
 #pragma unroll
-          for (int ks = 0; ks < kHeadKSteps; ++ks) {
-            const int t0 = 4 * ks + 2 * hh;               // this lane's two taps (k = 8hh .. 8hh+7)
-            uint2 q0 = make_uint2(0, 0), q1 = make_uint2(0, 0);
-            if (t0 < 9) q0 = *reinterpret_cast<const uint2*>(ring + rin(prow + t0 / 3) + (pcol + t0 % 3) * 8);
-            if (t0 + 1 < 9)
-              q1 = *reinterpret_cast<const uint2*>(ring + rin(prow + (t0 + 1) / 3) + (pcol + (t0 + 1) % 3) * 8);
-            const uint4 q = make_uint4(q0.x, q0.y, q1.x, q1.y);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wA[ks][0], *reinterpret_cast<const half8_t*>(&q), acc, 0, 0, 0);
+            for (int n = 0; n < NT; ++n) {
+              uu[n] = n == 0 ? ua : n == 1 ? ub : uc;
+              prow[n] = uu[n] < 8 ? uu[n] : (col & 15) >> 1;
+              pcol[n] = uu[n] < 8 ? 1 + col : ((col & 1) ? kF2MidW - 1 : 0);
+              acc[n] = floatx16{};
+            }
+#pragma unroll
+            for (int ks = 0; ks < kHeadKSteps; ++ks) {
+              const int t0 = 4 * ks + 2 * hh;             // this lane's two taps (k = 8hh .. 8hh+7)
+              const half8_t ha = *(lds_h8p)(size_t)(unsigned)(size_t)(hfr + ((ks * 2 + m) * 64 + lane) * 16);
+#pragma unroll
+              for (int n = 0; n < NT; ++n) {
+                uint2 q0 = make_uint2(0, 0), q1 = make_uint2(0, 0);
+                if (t0 < 9) q0 = *reinterpret_cast<const uint2*>(ring + rin(prow[n] + t0 / 3) + (pcol[n] + t0 % 3) * 8);
+                if (t0 + 1 < 9)
+                  q1 = *reinterpret_cast<const uint2*>(ring + rin(prow[n] + (t0 + 1) / 3) + (pcol[n] + (t0 + 1) % 3) * 8);
+                const uint4 q = make_uint4(q0.x, q0.y, q1.x, q1.y);
+                acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ha, *reinterpret_cast<const half8_t*>(&q), acc[n], 0, 0, 0);
+              }
+            }
+#pragma unroll
+            for (int n = 0; n < NT; ++n) {
+              half8_t v0 = bias_act8<ACT>(acc[n], 0, hbl), v1 = bias_act8<ACT>(acc[n], 8, hbl + 8);
+              const int x = x0 - 1 + pcol[n];
+              if (!(8 * jb + prow[n] < s.H && x >= 0 && x < s.W)) v0 = v1 = half8_t{};   // the next layer's zero padding
+              if (uu[n] < 8 || col < 16) {
+                unsigned char* dst = mid + rmid(prow[n]) + pcol[n] * 16;
+                *reinterpret_cast<half8_t*>(dst + (4 * m + 2 * hh) * kF2MidPlane) = v0;
+                *reinterpret_cast<half8_t*>(dst + (4 * m + 2 * hh + 1) * kF2MidPlane) = v1;
+              }
+            }
+          };
+          using I1 = std::integral_constant<int, 1>;
+          htiles(I1{}, 2 * qr, 0, 0);
+          htiles(I1{}, 2 * qr + 1, 0, 0);
+          if (qr == 0) htiles(I1{}, 8, 0, 0);
+        } else {
+          for (int q = lane; q < 4 * kF2MidW * 2; q += 64) {
+            const int c = q / (2 * kF2MidW), p = q - c * (2 * kF2MidW), rr = p / kF2MidW, pc = p - rr * kF2MidW;
+            *reinterpret_cast<v4i_t*>(mid + (4 * m + c) * kF2MidPlane +
+                                      (f2_slot(8 * J + 2 * qr + rr) * kF2MidW + pc) * 16) = v4i_t{0, 0, 0, 0};
           }
-          half8_t v0 = bias_act8<ACT>(acc, 0, hbl), v1 = bias_act8<ACT>(acc, 8, hbl + 8);
-          const int x = x0 - 1 + pcol;
-          if (!(8 * jb + prow < s.H && x >= 0 && x < s.W)) v0 = v1 = half8_t{};   // the next layer's zero padding
-          if (u < 8 || col < 16) {
-            unsigned char* dst = mid + rmid(prow) + pcol * 16;
-            *reinterpret_cast<half8_t*>(dst + (4 * m + 2 * hh) * kF2MidPlane) = v0;
-            *reinterpret_cast<half8_t*>(dst + (4 * m + 2 * hh + 1) * kF2MidPlane) = v1;
+        }
+      };
+      auto l0_part = [&]() {
+        if (J == 0) return;
+        // L0 on output rows 8J-9 + 2 qr + t, t = 0, 1: N-subtiles v = 0..3 (row v >> 1, column half v & 1)
+        int sl = f2_slot(8 * J - 10 + 2 * qr);
+        int rowoff[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          rowoff[q] = sl * (kF2MidW * 16);
+          sl = sl == kF2Ring - 1 ? 0 : sl + 1;
+        }
+        const int lb = g * kF2MidPlane + px * 16;
+        auto rowrs = [&](int t) {
+          const int R = 8 * J - 9 + 2 * qr + t;
+          int k, r;
+          locate(R, kJ, k, r);
+          const bool ok = R >= 0 && k < K && r < s.H;
+          const SGeom G = pick(k);
+          half_t* row = out + (((size_t)G.b * s.Hp + r + s.pad) * s.Wp + G.x0 + s.pad) * kWidth;
+          return __builtin_amdgcn_make_buffer_rsrc(ok ? (void*)row : (void*)out, (short)0,
+                                                   ok ? min(kTileW, s.W - G.x0) * 128 : 0, 0x00020000);
+        };
+        auto group = [&](int v0, int v1) {
+          int ad[2][3];
+#pragma unroll
+          for (int n = 0; n < 2; ++n) {
+            const int v = n ? v1 : v0;
+#pragma unroll
+            for (int dy = 0; dy < 3; ++dy) ad[n][dy] = lb + rowoff[(v >> 1) + dy] + 16 * 16 * (v & 1);
+          }
+          floatx4 acc[2][2];
+          x8_kloop<2, kF2MidPlane, decltype(noside)&, 2>(wA, mid, ad, acc, noside, c0);
+#pragma unroll
+          for (int n = 0; n < 2; ++n) {
+            const int v = n ? v1 : v0;
+            const half8_t o = x8_act<ACT>(acc[n]);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i_t, o), rowrs(v >> 1),
+                                                   (unsigned)((16 * (v & 1) + px) * 128 + 64 * m + 16 * g), 0,
+                                                   kNtX8);
           }
         };
-        if (half == 0) {
-          htile(0); htile(1); htile(2); htile(3); htile(8);
-        } else {
-          htile(4); htile(5); htile(6); htile(7);
-        }
+        group(0, 1);
+        group(2, 3);
+      };
+      // the two waves of a SIMD (w, w + 4) run the parts in opposite orders: one's L0 MFMA stream
+      // covers the other's head-tile latency
+      if (layer == 0) {
+        head_part();
+        l0_part();
       } else {
-        for (int q = lane; q < 4 * kF2MidW * 4; q += 64) {
-          const int c = q / (4 * kF2MidW), p = q - c * (4 * kF2MidW), rr = p / kF2MidW, pc = p - rr * kF2MidW;
-          *reinterpret_cast<v4i_t*>(mid + (4 * m + c) * kF2MidPlane +
-                                    (f2_slot(8 * J + 4 * half + rr) * kF2MidW + pc) * 16) = v4i_t{0, 0, 0, 0};
-        }
+        l0_part();
+        head_part();
       }
       stage_store();
-    } else if (layer == 0) {
-      const int x0 = gcx;
+    } else if (layer == 0 || MODE == kX8Tail) {
+      // (TAIL: every wave runs a quarter of L(n-1)'s N-subtiles here, then one output row of the
+      // tail below)
+      const int x0 = gcx, qr = wave >> 1;
+      auto lpart = [&]() {
       if (J < K * sb && 8 * jb < s.H) {
         int sl = f2_slot(8 * J - 1);
         int rowoff[10];
@@ -756,7 +815,21 @@ __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __re
         using I1 = std::integral_constant<int, 1>;
         using I2 = std::integral_constant<int, 2>;
         using I3 = std::integral_constant<int, 3>;
-        if (half == 0) {                                 // 8 N-subtiles + one A-subtile of the halo each
+        if constexpr (MODE == kX8Tail) {                // 4 N-subtiles (+ one halo A-subtile: quarters 0, 1)
+          if (qr == 0) {
+            group(I3{}, I3{}, 0, 1, 2, true);
+            group(I2{}, I1{}, 3, 16, 16, false);
+          } else if (qr == 1) {
+            group(I3{}, I3{}, 4, 5, 6, true);
+            group(I2{}, I2{}, 7, 16, 16, false);
+          } else if (qr == 2) {
+            group(I3{}, I3{}, 8, 9, 10, true);
+            group(I1{}, I3{}, 11, 11, 11, false);
+          } else {
+            group(I3{}, I3{}, 12, 13, 14, true);
+            group(I1{}, I3{}, 15, 15, 15, false);
+          }
+        } else if (half == 0) {                          // 8 N-subtiles + one A-subtile of the halo each
           group(I3{}, I3{}, 0, 1, 2, true);
           group(I3{}, I3{}, 3, 4, 5, false);
           group(I3{}, I1{}, 6, 7, 16, false);
@@ -768,88 +841,105 @@ __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __re
       } else {
 #pragma unroll 1
         for (int ks = 0; ks < kX8KSteps; ++ks) side(ks);
-        for (int q = lane; q < 4 * kF2MidW * 4; q += 64) {
-          const int c = q / (4 * kF2MidW), p = q - c * (4 * kF2MidW), rr = p / kF2MidW, pc = p - rr * kF2MidW;
+        constexpr int ZR = MODE == kX8Tail ? 2 : 4;       // rows this wave zero-fills
+        const int zr0 = MODE == kX8Tail ? 2 * qr : 4 * half;
+        for (int q = lane; q < 4 * kF2MidW * ZR; q += 64) {
+          const int c = q / (ZR * kF2MidW), p = q - c * (ZR * kF2MidW), rr = p / kF2MidW, pc = p - rr * kF2MidW;
           *reinterpret_cast<v4i_t*>(mid + (4 * m + c) * kF2MidPlane +
-                                    (f2_slot(8 * J + 4 * half + rr) * kF2MidW + pc) * 16) = v4i_t{0, 0, 0, 0};
+                                    (f2_slot(8 * J + zr0 + rr) * kF2MidW + pc) * 16) = v4i_t{0, 0, 0, 0};
         }
       }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else if (MODE == kX8Tail) {
-      if (J > 0) {
-        // the tail on output rows 8J-9 + 4 half + i, i = 0..3, columns 16 m .. 16 m + 15 (one
-        // N-subtile each): 64 -> C (A rows = output channels, c >= C zero), K order as conv_tail
-        int sl = f2_slot(8 * J - 10 + 4 * half);
-        int rowoff[6];
+      };
+      auto tpart = [&]() {
+        if (MODE == kX8Tail && J > 0) {
+          // the tail on output row 8J-9 + wave, columns 16 i + px (N-subtiles i = 0, 1): 64 -> C
+          // (A rows = output channels, c >= C zero), conv_tail's K order; its fragments stream from
+          // L2 (no registers or LDS left for them beside L(n-1)'s), 6 K-steps ahead
+          const int R = 8 * J - 9 + wave;
+          int sl = f2_slot(R - 1);
+          int rowoff[3];
 #pragma unroll
-        for (int q = 0; q < 6; ++q) {
-          rowoff[q] = sl * (kF2MidW * 16);
-          sl = sl == kF2Ring - 1 ? 0 : sl + 1;
-        }
-        const int lb = g * kF2MidPlane + px * 16;
-        int av[4][3];
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int dy = 0; dy < 3; ++dy) {
-            av[i][dy] = (int)(size_t)mid + lb + rowoff[i + dy] + 16 * 16 * m;
-            asm volatile("" : "+v"(av[i][dy]));
+          for (int q = 0; q < 3; ++q) {
+            rowoff[q] = sl * (kF2MidW * 16);
+            sl = sl == kF2Ring - 1 ? 0 : sl + 1;
           }
-        // the residual input (lanes 0..15: pixel px of N-subtile i), loaded before the DMA
-        const unsigned plane = (unsigned)(s.H * s.W);
-        float xi[4][kMaxC];
-        __amdgpu_buffer_rsrc_t ro[4];
-        unsigned toff[4];
-        int bimg[4];
+          const int lb = g * kF2MidPlane + px * 16;
+          int av[2][3];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int R = 8 * J - 9 + 4 * half + i;
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int dy = 0; dy < 3; ++dy) {
+              av[i][dy] = (int)(size_t)mid + lb + rowoff[dy] + 16 * 16 * i;
+              asm volatile("" : "+v"(av[i][dy]));
+            }
+          unsigned tw_off = (unsigned)lane * 16u;
+          asm volatile("" : "+v"(tw_off));                // per step: not hoisted out of the loop
+          const __amdgpu_buffer_rsrc_t trs =
+              __builtin_amdgcn_make_buffer_rsrc((void*)ends.tw, (short)0, kX8KSteps * 64 * 16, 0x00020000);
+          constexpr int TP = 6;
+          half8_t ta[TP + 1];
+          auto ldA = [&](int ks) {
+            return __builtin_bit_cast(half8_t, __builtin_amdgcn_raw_buffer_load_b128(trs, tw_off + ks * 1024u, 0, 0));
+          };
+#pragma unroll
+          for (int ks = 0; ks < TP; ++ks) ta[ks] = ldA(ks);
+          // the residual input (lanes 0..15: pixel px of N-subtile i)
+          const unsigned plane = (unsigned)(s.H * s.W);
           int k, r;
           locate(R, kJ, k, r);
           const SGeom G = pick(k);
-          bimg[i] = G.b;
-          const int x = G.x0 + 16 * m + px;
-          const bool ok = R >= 0 && k < K && r < s.H && x < s.W && lane < 16;
-          toff[i] = ok ? (unsigned)(r * s.W + x) * 4u : 0x80000000u;       // out of range: dropped
-          ro[i] = __builtin_amdgcn_make_buffer_rsrc((void*)(ends.u32 + (size_t)G.b * ends.C * plane), (short)0,
-                                                    (int)(ends.C * plane * 4u), 0x00020000);
+          float xi[2][kMaxC];
+          unsigned toff[2];
+          const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+              (void*)(ends.u32 + (size_t)G.b * ends.C * plane), (short)0, (int)(ends.C * plane * 4u), 0x00020000);
 #pragma unroll
-          for (int c = 0; c < kMaxC; ++c)
-            xi[i][c] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                                      ro[i], toff[i] + (unsigned)min(c, ends.C - 1) * plane * 4u, 0, 0));
-        }
-        __builtin_amdgcn_sched_barrier(0);               // the residual loads stay older than the DMA
-        typedef const __attribute__((address_space(3))) half8_t* lds_h8p;
-        floatx4 acc[4] = {};
+          for (int i = 0; i < 2; ++i) {
+            const int x = G.x0 + 16 * i + px;
+            const bool ok = R >= 0 && k < K && r < s.H && x < s.W && lane < 16;
+            toff[i] = ok ? (unsigned)(r * s.W + x) * 4u : 0x80000000u;     // out of range: dropped
 #pragma unroll
-        for (int ks = 0; ks < kX8KSteps; ++ks) {
-          const int tap = ks >> 1, hs = ks & 1, dy = tap / 3, dx = tap - 3 * dy;
-          half8_t fb[4];
-#pragma unroll
-          for (int i = 0; i < 4; ++i) fb[i] = *(lds_h8p)(size_t)(unsigned)(av[i][dy] + (4 * hs * kF2MidPlane + 16 * dx));
-#pragma unroll
-          for (int i = 0; i < 4; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wA[ks][0], fb[i], acc[i], 0, 0, 0);
-          side(ks);
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int c = 0; c < kMaxC; ++c) {
-            const float nc = acc[i][c] + tbl[c];
-            float o = ends.residual_sign > 0 ? nc + xi[i][c] : xi[i][c] - nc;
-            if (ends.clamp_out) o = fminf(fmaxf(o, 0.f), 1.f);
-            __builtin_amdgcn_raw_buffer_store_b32(
-                __builtin_bit_cast(int, o),
-                __builtin_amdgcn_make_buffer_rsrc((void*)(ends.xout + ((size_t)bimg[i] * ends.C + (c < ends.C ? c : 0)) * plane),
-                                                  (short)0, c < ends.C ? (int)(plane * 4u) : 0, 0x00020000),
-                toff[i], 0, kNtTail);
+            for (int c = 0; c < kMaxC; ++c)
+              xi[i][c] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                        ro, toff[i] + (unsigned)min(c, ends.C - 1) * plane * 4u, 0, 0));
           }
-        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");   // the DMAs (older than the 16 stores) landed
+          typedef const __attribute__((address_space(3))) half8_t* lds_h8p;
+          floatx4 acc[2] = {};
+#pragma unroll
+          for (int ks = 0; ks < kX8KSteps; ++ks) {
+            if (ks + TP < kX8KSteps) ta[(ks + TP) % (TP + 1)] = ldA(ks + TP);
+            const int tap = ks >> 1, hs = ks & 1, dy = tap / 3, dx = tap - 3 * dy;
+            half8_t fb[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) fb[i] = *(lds_h8p)(size_t)(unsigned)(av[i][dy] + (4 * hs * kF2MidPlane + 16 * dx));
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+              acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ta[ks % (TP + 1)], fb[i], acc[i], 0, 0, 0);
+          }
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int c = 0; c < kMaxC; ++c) {
+              const float nc = acc[i][c] + tbl[c];
+              float o = ends.residual_sign > 0 ? nc + xi[i][c] : xi[i][c] - nc;
+              if (ends.clamp_out) o = fminf(fmaxf(o, 0.f), 1.f);
+              __builtin_amdgcn_raw_buffer_store_b32(
+                  __builtin_bit_cast(int, o),
+                  __builtin_amdgcn_make_buffer_rsrc((void*)(ends.xout + ((size_t)G.b * ends.C + (c < ends.C ? c : 0)) * plane),
+                                                    (short)0, c < ends.C ? (int)(plane * 4u) : 0, 0x00020000),
+                  toff[i], 0, kNtTail);
+            }
+        }
+      };
+      // TAIL: the two waves of a SIMD (w, w + 4) run the parts in opposite orders, so one's MFMA
+      // stream covers the other's latencies (the tail's L2 fragment loads)
+      if (MODE != kX8Tail || layer == 0) {
+        lpart();
+        tpart();
       } else {
-#pragma unroll 1
-        for (int ks = 0; ks < kX8KSteps; ++ks) side(ks);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        tpart();
+        lpart();
       }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     } else {
       if (J > 0) {
         // output rows 8J-9 + 4 half + t, t = 0..3: N-subtiles (t, column half), two per group
