@@ -3,8 +3,8 @@
 D=${1:-gpurun_out/prof}; shift
 mkdir -p $D; export TMPDIR=/tmp
 timeout -k 10 400 python3 bench.py "$@" > $D/bench.json 2> $D/bench.log || exit 20
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $D -o trace --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline "$@" > $D/trace.log 2>&1 || exit 21
-P="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --profile 0 $*"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $D -o trace --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --converge-run 0 "$@" > $D/trace.log 2>&1 || exit 21
+P="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --converge-run 0 --profile 0 $*"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $D -o pmc_fetch --output-format csv -- $P > $D/pmc_fetch.log 2>&1 || exit 22
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $D -o pmc_write --output-format csv -- $P > $D/pmc_write.log 2>&1 || exit 23
 timeout -k 10 300 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU -d $D -o pmc_sq --output-format csv -- $P > $D/pmc_sq.log 2>&1 || exit 24

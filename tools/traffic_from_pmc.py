@@ -23,6 +23,9 @@ FETCH_CORRECTION = 2.0   # every access width (profiles/r04/probe/fetch_probe_su
 
 def short(name):
     n = re.sub(r"\(.*", "", name)
+    mode = re.search(r"conv_body_x8_kernelILi\dELi(\d)E", name)
+    if mode and mode.group(1) in "12":                                      # head + L0 / L(n-1) + tail
+        return "conv_body_f2h" if mode.group(1) == "1" else "conv_body_f2t"
     if any(k in n for k in ("conv_body_x8", "conv_body_f8", "conv_body_f2")):   # the two-layer launch (bench scope "conv_body_f2")
         return "conv_body_f2"
     if "conv_s3_kernel" in n:                                               # split fp16: body (MODE 0) / tail
