@@ -529,9 +529,10 @@ def main():
     ap.add_argument("--full-run", action="store_true",
                     help="time one whole solve of --steps iterations from iteration 0 (state reloaded after the "
                          "warm-up): with --precision converge, the experiments' 1200-iteration run")
-    ap.add_argument("--converge-run", type=int, default=1200,
+    ap.add_argument("--converge-run", type=int, default=None,
                     help="N = 1, precision auto: also time a whole precision='converge' solve of this many "
-                         "iterations (the c_n-faithful mode; 0 = skip)")
+                         "iterations (the c_n-faithful mode; 0 = skip; default 1200 on the metric config, "
+                         "0 on the others: cfg5's step is a 2.9-s outer iteration)")
     ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of CPU-baseline work")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile", type=int, default=1, help="HIP-event per-kernel timing in the timed region")
@@ -740,9 +741,10 @@ def main():
         line["ssim_img0"] = [round(float(ssim_hist[0, 0]), 5), round(float(ssim_hist[0, last]), 5)]
         if prec_req == "converge" or args.full_run:
             line["c_img0"] = [float(c_hist[0, 0]), float(c_hist[0, last])]
-        if world == 1 and args.converge_run > 0 and prec_req == "auto" and not args.full_run:
+        conv_n = args.converge_run if args.converge_run is not None else (1200 if args.config == "metric" else 0)
+        if world == 1 and conv_n > 0 and prec_req == "auto" and not args.full_run:
             line["converge_full_run"] = converge_full_run(ctx, torch, d_x0, d_obs, d_true, prm, resolve_method(cfg["method"]),
-                                                          B, C, H, W, args.converge_run)
+                                                          B, C, H, W, conv_n)
         if cpu_res is not None:
             rate, sample, ps_cpu, info = cpu_res
             line["cpu_baseline"] = {"value": round(rate, 4), "unit": "image-iterations/s",
