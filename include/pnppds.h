@@ -219,7 +219,9 @@ int pnp_solver_iterations_done(pnp_ctx* ctx, int* n);
 int pnp_solver_state(pnp_ctx* ctx, const float** d_x, const float** d_y, const float** d_s);
 
 /* Per-kernel timing of the last iterate() call: fills up to `cap` entries of
- * name/avg-ms pairs measured with hipEvents on the solver stream (profiling aid).   */
+ * name/avg-ms pairs measured with hipEvents on the solver stream (profiling aid).  enable:
+ * 0 off, 1 every launch, 2 (ABI 7) only the denoiser's body launches (conv_body*, conv32_body*,
+ * conv_stack*), so the other launches run without event packets between them.            */
 int pnp_profile_enable(pnp_ctx* ctx, int enable);
 int pnp_profile_read(pnp_ctx* ctx, int cap, const char** names, double* avg_ms, int* calls, int* n);
 

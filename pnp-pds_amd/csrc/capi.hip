@@ -132,7 +132,7 @@ struct pnp_ctx {
   int stack_epoch = 0, scr_stack_epoch = 0;
 
   // profiling
-  bool prof = false;
+  int prof = 0;           // pnp_profile_enable: 0 off, 1 every launch, 2 body launches only
   std::vector<ProfEntry> prof_log;
   std::vector<hipEvent_t> ev_pool;
   size_t ev_used = 0;
@@ -230,14 +230,20 @@ struct ProfScope {
   const char* name;
   hipStream_t st;
   hipEvent_t a = nullptr;
+  // prof 2: only the denoiser's body launches (the bench's timed region: the dominant kernel's
+  // duration without the other scopes' event packets between launches)
+  static bool body(const char* n) {
+    return !strncmp(n, "conv_body", 9) || !strncmp(n, "conv32_body", 11) || !strncmp(n, "conv_stack", 10);
+  }
+  bool on() const { return ctx->prof == 1 || (ctx->prof == 2 && body(name)); }
   ProfScope(pnp_ctx* c, const char* n, hipStream_t s) : ctx(c), name(n), st(s) {
-    if (ctx->prof) {
+    if (on()) {
       a = next_event(ctx);
       HIPCHK(ctx, hipEventRecord(a, st));
     }
   }
   ~ProfScope() noexcept(false) {
-    if (ctx->prof) {
+    if (a) {
       hipEvent_t b = next_event(ctx);
       HIPCHK(ctx, hipEventRecord(b, st));
       ctx->prof_log.push_back({name, a, b});
@@ -1735,7 +1741,8 @@ int pnp_run(pnp_ctx* ctx, int method, const pnp_params* params, int B, int C, in
 int pnp_profile_enable(pnp_ctx* ctx, int enable) {
   if (!ctx) return PNP_E_ARG;
   ctx->gen++;
-  ctx->prof = enable != 0;
+  if (enable < 0 || enable > 2) return PNP_E_ARG;
+  ctx->prof = enable;
   ctx->prof_log.clear();
   ctx->ev_used = 0;
   return PNP_OK;

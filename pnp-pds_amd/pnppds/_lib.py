@@ -374,7 +374,8 @@ class Context:
         return x.value, y.value, sv.value
 
     def profile_enable(self, on=True):
-        self._check(self.lib.pnp_profile_enable(self.h, 1 if on else 0))
+        """on: False / 0 off, True / 1 every launch, 2 only the denoiser's body launches."""
+        self._check(self.lib.pnp_profile_enable(self.h, int(on)))
 
     def profile_read(self):
         cap = 64

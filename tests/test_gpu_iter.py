@@ -154,3 +154,42 @@ def test_metrics_paths_do_not_change_iterates(case):
         np.testing.assert_array_equal(other[1], full[1])     # s
     np.testing.assert_array_equal(no_true[2], full[2])       # c_n does not use x_true
     assert np.isnan(no_true[3]).all() and np.isfinite(full[3]).all()
+
+
+def test_profile_modes():
+    """pnp_profile_enable: 1 times every launch, 2 only the denoiser's body launches (the bench's
+    timed region), 0 none; other values are rejected.  The iterates do not depend on it."""
+    from pnppds import operators as ops
+    from pnppds._device import get_ctx
+    from pnppds.iteration import _resolve_denoiser, make_params, resolve_method
+    from pnppds._lib import PnpError
+    g = load_golden("iter_A_blur.npz")
+    g1, g2, as_, an, lam, m1, m2, gadmm, sig, sp, palpha, iters, ch, r = g["params"]
+    phi, adj = ops.get_observation_operators(str(g["deg_op"]), "blur_1", r)
+    ctx = get_ctx()
+    den = _resolve_denoiser(str(g["arch"]) + ".pth", int(ch))
+    den.configure(ctx)
+    x0 = np.asarray(g["x_0"], np.float32)
+    to4 = lambda a: np.asarray(a, np.float32).reshape((1,) + x0.shape)   # noqa: E731
+    B, C, H, W = to4(x0).shape
+    phi.configure(ctx, H, W)
+    prm = make_params(g1, g2, as_, an, lam, m1, m2, gadmm, sig, sp, palpha, r, True, False)
+    xs = []
+    for mode in (0, 1, 2):
+        ctx.solver_setup(resolve_method(str(g["method"])), prm, B, C, H, W, 4)
+        ctx.solver_load(to4(x0), to4(g["x_obs"]), to4(g["x_true"]))
+        ctx.profile_enable(mode)
+        ctx.solver_iterate(4)
+        names = set(ctx.profile_read())
+        ctx.profile_enable(0)
+        xs.append(ctx.solver_fetch()[0])
+        if mode == 0:
+            assert not names
+        elif mode == 1:
+            assert any(n.startswith("k2") for n in names) and any(n.startswith("conv") for n in names)
+        else:
+            assert names and all(n.startswith(("conv_body", "conv32_body", "conv_stack")) for n in names), names
+    np.testing.assert_array_equal(xs[1], xs[0])
+    np.testing.assert_array_equal(xs[2], xs[0])
+    with pytest.raises(PnpError):
+        ctx.profile_enable(3)
