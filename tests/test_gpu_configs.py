@@ -6,6 +6,8 @@ pipeline, bit-identical to the reference's numpy stream), and the whole batch th
 size-independent properties:
 * the last image of the batch gives the same bits alone (what sharding over GPUs relies on);
 * the iteration's own invariants: s inside the l1 ball of radius eta (B), finite duals (C).
+The x / s bounds are 2-3x what the product measured against the oracle (round 5); the PSNR
+bound is north_star's 0.01 dB.
 Per-GPU shard sizes: cfg4 = 256 images / 8 GPUs, cfg5 = 512 / 8.
 """
 import numpy as np
@@ -60,9 +62,11 @@ def test_cfg3_ours_b_blur_sparse_batch64():
     assert np.isfinite(x).all() and np.isfinite(c).all()
     # image 0 vs the oracle on the same observation
     xo, so, co, po, _, _ = _oracle_image0(xt, xobs, "blur", r, prm, iters, "B-Proposed")
+    print(f"cfg3: |dPSNR| {np.abs(psnr[0] - po).max():.5f} dB, max|dx| {np.abs(x[0] - xo).max():.2e}, "
+          f"max|ds| {np.abs(s[0] - so).max():.2e}")
     np.testing.assert_allclose(psnr[0], po, atol=0.01)
-    np.testing.assert_allclose(x[0], xo, atol=5e-3)
-    np.testing.assert_allclose(s[0], so, atol=5e-3)
+    np.testing.assert_allclose(x[0], xo, atol=2e-3)        # fp16 (auto): measured 9.5e-4 (r05)
+    np.testing.assert_allclose(s[0], so, atol=1e-3)        # measured 3.0e-4
     # s stays in the l1 ball of radius eta = alpha_s * N * sp_nl * r * 0.5 (operators.py:94-100)
     eta = 0.95 * x[0].size * 0.1 * r * 0.5
     l1 = np.abs(s.astype(np.float64) - 0.5).reshape(B, -1).sum(1)
@@ -86,9 +90,11 @@ def test_cfg4_ours_c_random_sampling_poisson_512():
     assert np.isfinite(x).all() and np.isfinite(psnr).all()
     np.testing.assert_array_equal(s, np.float32(0.5))                        # C never touches s
     xo, so, co, po, _, _ = _oracle_image0(xt, xobs, "random_sampling", r, prm, iters, "C-Proposed", poisson=True)
+    print(f"cfg4: |dPSNR| {np.abs(psnr[0] - po).max():.5f} dB, max|dx| {np.abs(x[0] - xo).max():.2e}, "
+          f"c rel {np.abs(c[0] - co).max() / np.abs(co).min():.2e}")
     np.testing.assert_allclose(psnr[0], po, atol=0.01)
-    np.testing.assert_allclose(x[0], xo, atol=5e-3)
-    np.testing.assert_allclose(c[0], co, rtol=0.05, atol=2e-4)
+    np.testing.assert_allclose(x[0], xo, atol=1e-5)        # split fp16 (auto): measured 3.5e-6 (r05)
+    np.testing.assert_allclose(c[0], co, rtol=1e-4, atol=1e-9)   # measured 9e-6 relative
     x1, s1, c1, p1, _, _ = _run(xt, xobs, x0, phi, adj, prm, iters, "ours-C", r, sl=slice(B - 1, B))
     np.testing.assert_array_equal(x1[0], x[B - 1])
     np.testing.assert_array_equal(p1[0], psnr[B - 1])
@@ -112,9 +118,11 @@ def test_cfg5_admm_blur_sparse_1024():
     prm2 = prm[:5] + (2, 2) + prm[7:]
     xb, sb, cb, pb, _, _ = _run(xt, xobs, x0, phi, adj, prm2, 1, "comparisonB-2", r, sl=slice(0, 1))
     xo, so, co, po, _, _ = _oracle_image0(xt, xobs, "blur", r, prm2, 1, "comparisonB-2")
+    print(f"cfg5 m1=m2=2: |dPSNR| {np.abs(pb[0] - po).max():.5f} dB, max|dx| {np.abs(xb[0] - xo).max():.2e}, "
+          f"max|ds| {np.abs(sb[0] - so).max():.2e}")
     np.testing.assert_allclose(pb[0], po, atol=0.01)
-    np.testing.assert_allclose(xb[0], xo, atol=5e-3)
-    np.testing.assert_allclose(sb[0], so, atol=5e-3)
+    np.testing.assert_allclose(xb[0], xo, atol=7.5e-4)     # fp16 (auto): measured 2.5e-4 (r05)
+    np.testing.assert_allclose(sb[0], so, atol=1.5e-4)     # measured 4.4e-5
 
 
 def test_cfg5_admm_full_inner_counts_256_crop():
@@ -126,7 +134,8 @@ def test_cfg5_admm_full_inner_counts_256_crop():
     phi, adj, xobs, x0 = _observe(xt, "blur", r, 0.01, 0.1, False, 300.0)
     x, s, c, psnr, _, _ = _run(xt, xobs, x0, phi, adj, prm, 1, "comparisonB-2", r)
     xo, so, co, po, _, _ = _oracle_image0(xt, xobs, "blur", r, prm, 1, "comparisonB-2")
-    print(f"cfg5 crop m1=35 m2=5: |dPSNR| {abs(psnr[0, 0] - po[0]):.5f} dB, max|dx| {np.abs(x[0] - xo).max():.2e}")
+    print(f"cfg5 crop m1=35 m2=5: |dPSNR| {abs(psnr[0, 0] - po[0]):.5f} dB, max|dx| {np.abs(x[0] - xo).max():.2e}, "
+          f"max|ds| {np.abs(s[0] - so).max():.2e}")
     np.testing.assert_allclose(psnr[0], po, atol=0.01)
-    np.testing.assert_allclose(x[0], xo, atol=5e-3)
-    np.testing.assert_allclose(s[0], so, atol=5e-3)
+    np.testing.assert_allclose(x[0], xo, atol=7.5e-4)      # fp16 (auto): measured 2.7e-4 (r05)
+    np.testing.assert_allclose(s[0], so, atol=2e-4)        # measured 6.4e-5
