@@ -1259,7 +1259,7 @@ __device__ __forceinline__ void rb_fill_k2_cols(float* lds, int i0, int j0, int 
 // the tile's own rows, which need no wrap or clamp (a row step is an index add) and no
 // per-element "inside" test: a thread's column is inside the tile or not, so the sums of a
 // batch are kept or dropped once per batch.
-template <class G, int NB = kRbFill>
+template <class G, int NB = kRbFill, bool XT = true>   // XT false: no x_true (no loads, t2 stays 0)
 __device__ __forceinline__ void rb_fill_k2_fast(float* lds, int i0, int j0, int H, int W, const float* xnp,
                                                 const float* xop, const float* xtp, bool record, double& e2,
                                                 double& n2, double& t2, float& lo, float& hi) {
@@ -1320,7 +1320,7 @@ __device__ __forceinline__ void rb_fill_k2_fast(float* lds, int i0, int j0, int 
         const int ii = (ly0 + TPC * (k0 + k) < kRbH) ? idx : idx - TPC * W;   // past the last tile row: any loaded row, not stored
         a[k] = bld(rn, ii);
         bb[k] = bld(ro, ii);
-        t[k] = bld(rt, ii);
+        t[k] = XT ? bld(rt, ii) : 0.f;
         idx += TPC * W;
       }
     }
@@ -1335,7 +1335,7 @@ __device__ __forceinline__ void rb_fill_k2_fast(float* lds, int i0, int j0, int 
         const float o = bb[k];
         be = fmaf(ok ? d : 0.f, d, be);
         bn = fmaf(ok ? o : 0.f, o, bn);
-        bt = fmaf(ok ? tt : 0.f, tt, bt);
+        if (XT) bt = fmaf(ok ? tt : 0.f, tt, bt);
         bl = ok ? fminf(bl, a[k]) : bl;               // x+ range for SSIM's data_range (utils_eval.py:11)
         bh = ok ? fmaxf(bh, a[k]) : bh;
       }
@@ -1359,7 +1359,8 @@ __device__ __forceinline__ void rb_fill_k2_fast(float* lds, int i0, int j0, int 
 // tools/gpu_r05_run1.sh: 1 no stencil (each output takes one LDS value), 2 no fp64 partials
 // (no metric sums, no d2), 4 no epilogue stores, 8 no halo fill, 16 no epilogue loads, 64 no
 // x_true loads (PSNR wrong, the rest right).
-template <class T, int METHOD, int LAT = 0, int ABL = 0>   // LAT: as k1_blur_rb, and all 8 epilogue rows' loads in flight
+// XT: x_true given (false when the SSIM pass sums the PSNR's squared error: no x_true stream)
+template <class T, int METHOD, int LAT = 0, int ABL = 0, bool XT = true>   // LAT: as k1_blur_rb, and all 8 epilogue rows' loads in flight
 __global__ __launch_bounds__(256) void k2_blur_rb(const float* __restrict__ xn, const float* __restrict__ xo,
                                                    float* __restrict__ y, const float* __restrict__ xobs,
                                                    const float* __restrict__ xtrue, float* __restrict__ s,
@@ -1410,7 +1411,7 @@ __global__ __launch_bounds__(256) void k2_blur_rb(const float* __restrict__ xn, 
     double e2 = 0, n2 = 0, t2 = 0;
     float lo = __builtin_inff(), hi = -__builtin_inff();
     if (!(ABL & 8))
-      rb_fill_k2_fast<G, LAT ? 32 : kRbFill>(lds, i0, j0, H, W, xn + (size_t)bc * plane, xo + (size_t)bc * plane,
+      rb_fill_k2_fast<G, LAT ? 32 : kRbFill, XT>(lds, i0, j0, H, W, xn + (size_t)bc * plane, xo + (size_t)bc * plane,
                                             (xtrue && !(ABL & 64)) ? xtrue + (size_t)bc * plane : nullptr,
                                             record != 0, e2, n2, t2, lo, hi);
     if (record) {                            // reduced here, so no fill value stays live past the fill
@@ -1969,7 +1970,8 @@ static void launch_k2_rb(int method, hipStream_t st, const float* xn, const floa
 #endif
 #define K2RBL(M)                                                                                              \
   if (lat) hipLaunchKernelGGL((k2_blur_rb<T, M, 1>), grid, dim3(256), 0, st, K2RB_ARGS);                       \
-  else hipLaunchKernelGGL((k2_blur_rb<T, M, 0>), grid, dim3(256), 0, st, K2RB_ARGS);
+  else if (xtrue) hipLaunchKernelGGL((k2_blur_rb<T, M, 0>), grid, dim3(256), 0, st, K2RB_ARGS);               \
+  else hipLaunchKernelGGL((k2_blur_rb<T, M, 0, 0, false>), grid, dim3(256), 0, st, K2RB_ARGS);
   if (method == M_A) { K2RBL(M_A) }
   else if (method == M_B) { K2RBL(M_B) }
   else { K2RBL(M_C) }
