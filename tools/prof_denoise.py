@@ -17,6 +17,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--size", type=int, default=256)
+    ap.add_argument("--height", type=int, default=0, help="image height (0 = --size)")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--chunk", type=int, default=0)
     ap.add_argument("--random", action="store_true", help="uniform-random input instead of structured images")
@@ -38,7 +39,7 @@ def main():
     if a.body_layers:
         ctx.set_body_layers(a.body_layers)
     ctx.set_fuse_ends(a.fuse_ends)
-    B, C, H, W = a.batch, 3, a.size, a.size
+    B, C, H, W = a.batch, 3, a.height or a.size, a.size
     if a.random:
         x = torch.rand((B, C, H, W), device="cuda:0")
     else:                                   # the bench's structured synthetic images (denoiser input range)
