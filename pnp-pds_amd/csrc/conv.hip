@@ -480,7 +480,7 @@ __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __re
                                                                const float* __restrict__ b1,
                                                                const uint4* __restrict__ w2,
                                                                const float* __restrict__ b2, ConvShape s,
-                                                               int strips_x, int nstrips, int sb, X8Ends ends) {
+                                                               int strips_x, int nstrips, int srows, X8Ends ends) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned char* ring = smem;
   unsigned char* mid = smem + kF2Mid;
@@ -514,17 +514,22 @@ __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __re
 #endif
   const unsigned img_bytes = (unsigned)(s.Hp * s.Wp) * 128u;
 
-  const int S = 8 * sb;
+  // strip k's row r is stream row k S + r; S = H + 1 (one zero separator row between strips,
+  // the next strip's top halo and this one's bottom halo), so a step's 8 rows may straddle two
+  // strips: masks and geometry are per row (round 5; strips were 8 ceil((H+1)/8) rows, an idle
+  // layer-l step per strip at H = 256: 1 % of the launch)
+  const int S = srows;
   // (An XCD-aware strip order, an image's neighbouring strips on CUs sharing one L2, measured
   // the same: 2.109 vs 2.108 ms, r03.)
   const int bx = (int)blockIdx.x;
   const int K = (nstrips - bx + (int)gridDim.x - 1) / (int)gridDim.x;
+  const int Jend = (K * S + 7) / 8;                      // the last step (layer l+1 only)
   auto geom = [&](int k) {
     const int st = min(bx + k * (int)gridDim.x, nstrips - 1);
     const int b = st / strips_x;
     return SGeom{b, (st - b * strips_x) * kTileW};
   };
-  int kJ = 0, jb = 0;
+  int kJ = 0;                                            // the strip of row 8 J
   int gpb, gpx, gcb, gcx, gnb, gnx;
   {
     const SGeom g0 = geom(0), g1 = geom(1);
@@ -541,6 +546,14 @@ __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __re
     k = kJ;
     r = R - kJ * S;
     if (r < 0) { --k; r += S; } else if (r >= S) { ++k; r -= S; }
+  };
+  int J = 0;                                             // the step (rows 8 J .. 8 J + 7 of layer l)
+  // layer-l row 8 J + p (p may vary by lane): whether it is an image row, and its strip's x0
+  auto rowgeom = [&](int p, int& x0r) {
+    int k, r;
+    locate(8 * J + p, kJ, k, r);
+    x0r = pick(k).x0;
+    return k < K && r < s.H;
   };
   __amdgpu_buffer_rsrc_t dsrc;
   unsigned dvo;
@@ -620,7 +633,7 @@ __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __re
   __syncthreads();
   if (MODE == kX8Pair && layer == 1) __builtin_amdgcn_s_setprio(1);   // layer l+1's waves (4-7, the second-dispatched half)
 
-  for (int J = 0; J <= K * sb; ++J) {
+  for (J = 0; J <= Jend; ++J) {
     auto side = [&](int ks) {                            // this wave's DMA row of the next step
       if constexpr (MODE == kX8Head) return;             // (HEAD: layer l's waves stage the quads)
       if (ks == 0) dma_at(8 * J + 9 + wave, kJ);
@@ -631,11 +644,11 @@ __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __re
       // every wave: a share of the head's N-tiles (intermediate rows 8J .. 8J+7), then two of L0's
       // output rows (8J-9 + 2 qr, + 1); quads of the next step's input rows staged around them
       const int qr = wave >> 1;                            // quarter: 0 .. 3
-      if (J < K * sb) stage_load(8 * J + 9, 8, kJ);
+      if (J < Jend) stage_load(8 * J + 9, 8, kJ);
       else sslot = -1;
-      const int x0 = gcx, hh = lane >> 5, col = lane & 31;
+      const int hh = lane >> 5, col = lane & 31;
       auto head_part = [&]() {
-        if (J < K * sb && 8 * jb < s.H) {
+        if (J < Jend) {
           float hbl[16];                                   // channels 32m + 16h .. (per step: short-lived)
 #pragma unroll
           for (int r = 0; r < 16; ++r) hbl[r] = ends.hb[32 * m + 16 * hh + r];
@@ -675,8 +688,10 @@ __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __re
 #pragma unroll
             for (int n = 0; n < NT; ++n) {
               half8_t v0 = bias_act8<ACT>(acc[n], 0, hbl), v1 = bias_act8<ACT>(acc[n], 8, hbl + 8);
-              const int x = x0 - 1 + pcol[n];
-              if (!(8 * jb + prow[n] < s.H && x >= 0 && x < s.W)) v0 = v1 = half8_t{};   // the next layer's zero padding
+              int x0r;
+              const bool rin_img = rowgeom(prow[n], x0r);
+              const int x = x0r - 1 + pcol[n];
+              if (!(rin_img && x >= 0 && x < s.W)) v0 = v1 = half8_t{};   // the next layer's zero padding
               if (uu[n] < 8 || col < 16) {
                 unsigned char* dst = mid + rmid(prow[n]) + pcol[n] * 16;
                 *reinterpret_cast<half8_t*>(dst + (4 * m + 2 * hh) * kF2MidPlane) = v0;
@@ -754,7 +769,7 @@ __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __re
       // tail below)
       const int x0 = gcx, qr = wave >> 1;
       auto lpart = [&]() {
-      if (J < K * sb && 8 * jb < s.H) {
+      if (J < Jend) {
         int sl = f2_slot(8 * J - 1);
         int rowoff[10];
 #pragma unroll
@@ -762,7 +777,8 @@ __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __re
           rowoff[q] = sl * (kF2InW * 16);
           sl = sl == kF2Ring - 1 ? 0 : sl + 1;
         }
-        const bool all_in = 8 * jb + 8 <= s.H && x0 + kTileW <= s.W;   // rows and columns of u < 16 inside
+        // rows and columns of u < 16 inside (one strip: its rows r0 .. r0+7 < H < S)
+        const bool all_in = 8 * J - kJ * S + 8 <= s.H && x0 + kTileW <= s.W;
         // N-subtile u < 16: row u >> 1, columns 1 + 16 (u & 1) .. +15; u == 16: the strip halo
         // (columns 0 and 33 of the 8 rows: pixel px -> row px >> 1, column px & 1 ? 33 : 0)
         // QL (qlc): the A-subtiles computed for the group's last N-subtile (the strip halo's
@@ -791,8 +807,10 @@ __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __re
           auto epi = [&](bool masked) {
 #pragma unroll
             for (int n = 0; n < NT; ++n) {
-              const int x = x0 - 1 + pcol[n];
-              const bool inside = 8 * jb + prow[n] < s.H && x >= 0 && x < s.W;
+              int x0r;
+              const bool rin_img = rowgeom(prow[n], x0r);
+              const int x = x0r - 1 + pcol[n];
+              const bool inside = rin_img && x >= 0 && x < s.W;
               if (n == NT - 1 && QL != 3) {              // one A-subtile: channels 8g + 4q .. +3
                 constexpr int q = QL == 1 ? 0 : 1;
                 const h2v_t h0 = act_h2<ACT>(f2v_t{acc[n][q][0], acc[n][q][1]});
@@ -996,8 +1014,7 @@ __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __re
       }
     }
     lds_barrier();     // the layer-l+1 stores stay in flight (vmcnt above, per role)
-    if (++jb == sb) {
-      jb = 0;
+    if (8 * (J + 1) >= (kJ + 1) * S) {                  // the next step starts in the next strip
       ++kJ;
       gpb = gcb;
       gpx = gcx;
@@ -2082,14 +2099,14 @@ void launch_conv_body_f2(const half_t* in, half_t* out, const void* w16_1, const
                          const void* w32_2, const float* b1, const float* b2, const ConvShape& s, int act,
                          int num_cus, hipStream_t st, int mode, const X8Ends* ends) {
   const int strips_x = (s.W + kTileW - 1) / kTileW, nstrips = s.B * strips_x;
-  // 8-row blocks per strip: S = 8 sb >= H + 1, and >= 16 so that a step's lookahead rows (up to
+  // rows per strip: H + 1 (the separator), at least 24 so that a step's look-ahead rows (up to
   // 8 J + 16) lie at most one strip ahead (locate())
-  const int sb = (s.H + 1 + 7) / 8 < 2 ? 2 : (s.H + 1 + 7) / 8;
+  const int srows = s.H + 1 < 24 ? 24 : s.H + 1;
   const int grid = nstrips < num_cus ? nstrips : num_cus;
   const X8Ends e = ends ? *ends : X8Ends{};
 #define F2_LAUNCH(KERN, NT, W1, W2)                                                                              \
   hipLaunchKernelGGL((KERN), dim3(grid), dim3(NT), kF2Lds, st, in, out, (const uint4*)(W1), b1, (const uint4*)(W2), \
-                     b2, s, strips_x, nstrips, sb, e)
+                     b2, s, strips_x, nstrips, srows, e)
   if (mode == kX8Head) {
     if (act == 0) F2_LAUNCH((conv_body_x8_kernel<0, kX8Head>), 512, w16_1, w16_2);
     else F2_LAUNCH((conv_body_x8_kernel<1, kX8Head>), 512, w16_1, w16_2);
