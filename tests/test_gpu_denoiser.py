@@ -370,3 +370,24 @@ def test_op_denoise_side_stream_equals_context_stream(gpu_ctx, prec):
         np.testing.assert_array_equal(d0.cpu().numpy(), d1.cpu().numpy())
     finally:
         gpu_ctx.set_precision(prev)
+
+
+def test_fused_ends_with_denoiser_passes_same_bits(gpu_ctx):
+    """The batch split into denoiser passes (PNP_TUNE_DENOISE_CHUNK 3 -> passes of 3, 3, 1) with
+    the head / tail inside the two-layer launches: every image as in one pass, and as with
+    separate head / tail launches."""
+    w = DenoiserWeights.load_npz(os.path.join(WEIGHTS_DIR, "DnCNN_nobn_nch_3_nlev_0.01.npz"))
+    x = np.random.default_rng(31).uniform(0, 1, (7, 3, 40, 72)).astype(np.float32)
+    try:
+        gpu_ctx.set_body_layers(2)
+        whole = run_denoise(gpu_ctx, w, x)
+        gpu_ctx.set_denoise_chunk(3)
+        passes = run_denoise(gpu_ctx, w, x)
+        gpu_ctx.set_fuse_ends(0)
+        apart = run_denoise(gpu_ctx, w, x)
+    finally:
+        gpu_ctx.set_denoise_chunk(0)
+        gpu_ctx.set_fuse_ends(1)
+        gpu_ctx.set_body_layers(0)
+    np.testing.assert_array_equal(passes, whole)
+    np.testing.assert_array_equal(apart, whole)
