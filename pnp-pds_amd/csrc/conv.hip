@@ -465,14 +465,17 @@ __device__ __forceinline__ half8_t x8_act(const floatx4 (&a)[2]) {
 }
 
 // MODE kX8Head: layer l is the head (C -> 64, conv_head_kernel's PREC 0 arithmetic: its packed
-// weights, three v_mfma_f32_32x32x16_f16 per output from a zero accumulator over the fp16-rounded
-// input quads, bias_act8) computed into the intermediate ring from the fp32 input, which layer l's
-// waves stage as fp16 quads (18 rows x 36 pixels x 8 B) one step ahead instead of the 64-channel
-// DMA ring; layer l + 1 is the first body layer.  MODE kX8Tail: layer l + 1 is the tail
-// (conv_tail_kernel's arithmetic: 64 -> C on v_mfma_f32_16x16x32_f16 from a zero accumulator,
-// + bias, +/- the fp32 residual, clamp), storing x+ in fp32 NCHW; layer l is the last body layer.
-// Both give the bits of the separate head / tail launches around a plain pair, without the head's
-// 2.15 GB write and the tail's 2.15 GB read at the metric.
+// weights, in LDS here, three v_mfma_f32_32x32x16_f16 per output from a zero accumulator over the
+// fp16-rounded input quads, bias_act8) computed into the intermediate ring from the fp32 input,
+// which every thread stages as fp16 quads (18 rows x 36 pixels x 8 B) one step ahead instead of the
+// 64-channel DMA ring; layer l + 1 is the first body layer.  Every wave runs both: a quarter of
+// the head's N-tiles and two of L0's output rows (the two waves of a SIMD in opposite orders).
+// MODE kX8Tail: layer l is the last body layer and layer l + 1 the tail (conv_tail_kernel's
+// arithmetic: 64 -> C on v_mfma_f32_16x16x32_f16 from a zero accumulator, + bias, +/- the fp32
+// residual, clamp), storing x+ in fp32 NCHW; every wave runs a quarter of layer l's N-subtiles and
+// one tail output row (its fragments streamed from L2).  Both give the bits of the separate head /
+// tail launches around a plain pair, without the head's 2.15 GB write and the tail's 2.15 GB read
+// at the metric.
 template <int ACT, int MODE = kX8Pair>
 __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __restrict__ in,
                                                                half_t* __restrict__ out,
