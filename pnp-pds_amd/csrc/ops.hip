@@ -1612,7 +1612,10 @@ __global__ __launch_bounds__(256) void ssim_rgb_kernel(const float* __restrict__
                                                        const float* __restrict__ mm, double* __restrict__ ps,
                                                        double* __restrict__ t2o, int C, int H, int W, int tiles_x,
                                                        int tiles, int chunks) {
-  __shared__ float v[5][kSsTH][kSsVS];             // axis-0 window means of x, y, xx, yy, xy
+  // Two LDS phases (round 5): the axis-0 means of x and y, then of xx, yy and xy, through one
+  // 3-quantity array (24 KiB instead of 40: 6 blocks per CU instead of 4); the horizontal pass
+  // keeps its 8 outputs' x / y means in registers between them.  Same arithmetic per quantity.
+  __shared__ float v[3][kSsTH][kSsVS];
   __shared__ double red[4];
   __shared__ float cst[2];
   const int tile = blockIdx.x, bc = blockIdx.y, b = bc / C;
@@ -1624,13 +1627,14 @@ __global__ __launch_bounds__(256) void ssim_rgb_kernel(const float* __restrict__
   }
   const __amdgpu_buffer_rsrc_t qa = plane_rsrc(xt + (size_t)bc * H * W, H, W);
   const __amdgpu_buffer_rsrc_t qb = plane_rsrc(x + (size_t)bc * H * W, H, W);
-  // ---- vertical: columns j0-3+c (c < 62), rows i0 + 8*wv .. +8 ----
+  // ---- vertical loads: columns j0-3+c (c < 62), rows i0 + 8*wv - 3 .. +14 ----
   float se = 0.f;                                  // this thread's own pixels' sum of (xt - x)^2
-  if (lane < kSsVW) {
-    const int c = lane;
+  const bool vcol = lane < kSsVW;
+  const int c = lane;
+  float ra[14], rb[14];
+  if (vcol) {
     const int gj = min(max(j0 - 3 + c, 0), W - 1);
     const int r0 = i0 + 8 * wv;
-    float ra[14], rb[14];
     if (__builtin_amdgcn_readfirstlane((int)(r0 >= 3 && r0 + 11 <= H))) {   // no row clamp: an index add per row
       int idx = (r0 - 3) * W + gj;
 #pragma unroll
@@ -1653,27 +1657,21 @@ __global__ __launch_bounds__(256) void ssim_rgb_kernel(const float* __restrict__
         se = r0 + k < H ? fmaf(dd, dd, se) : se;
       }
     }
-    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f, s4 = 0.f;
+    // phase A: the x and y means
+    float s0 = 0.f, s1 = 0.f;
 #pragma unroll
     for (int d = 0; d < 7; ++d) {
-      s0 += ra[d]; s1 += rb[d]; s2 = fmaf(ra[d], ra[d], s2); s3 = fmaf(rb[d], rb[d], s3); s4 = fmaf(ra[d], rb[d], s4);
+      s0 += ra[d]; s1 += rb[d];
     }
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       if (k) {
-        const float na = ra[k + 6], nb = rb[k + 6], oa = ra[k - 1], ob = rb[k - 1];
-        s0 = (s0 + na) - oa;
-        s1 = (s1 + nb) - ob;
-        s2 = fmaf(-oa, oa, fmaf(na, na, s2));
-        s3 = fmaf(-ob, ob, fmaf(nb, nb, s3));
-        s4 = fmaf(-oa, ob, fmaf(na, nb, s4));
+        s0 = (s0 + ra[k + 6]) - ra[k - 1];
+        s1 = (s1 + rb[k + 6]) - rb[k - 1];
       }
       const int r = 8 * wv + k;
       v[0][r][c] = s0 * kInv7f;
       v[1][r][c] = s1 * kInv7f;
-      v[2][r][c] = s2 * kInv7f;
-      v[3][r][c] = s3 * kInv7f;
-      v[4][r][c] = s4 * kInv7f;
     }
   }
   __syncthreads();
@@ -1682,12 +1680,54 @@ __global__ __launch_bounds__(256) void ssim_rgb_kernel(const float* __restrict__
   // conflict-free (rows-within-a-lane-group mapping t / 8 had every bank hit twice) ----
   const int r = threadIdx.x & 31, c0 = (threadIdx.x >> 5) * 8;
   const int i = i0 + r;
+  const bool hrow = c0 < kSsTW && i >= 3 && i < H - 3;
+  float ux[8], uy[8];
+  if (hrow) {
+    float h0 = 0.f, h1 = 0.f;
+#pragma unroll
+    for (int d = 0; d < 7; ++d) {
+      h0 += v[0][r][c0 + d];
+      h1 += v[1][r][c0 + d];
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (k) {
+        h0 = (h0 + v[0][r][c0 + k + 6]) - v[0][r][c0 + k - 1];
+        h1 = (h1 + v[1][r][c0 + k + 6]) - v[1][r][c0 + k - 1];
+      }
+      ux[k] = h0 * kInv7f;
+      uy[k] = h1 * kInv7f;
+    }
+  }
+  __syncthreads();
+  // phase B: the xx, yy and xy means
+  if (vcol) {
+    float s2 = 0.f, s3 = 0.f, s4 = 0.f;
+#pragma unroll
+    for (int d = 0; d < 7; ++d) {
+      s2 = fmaf(ra[d], ra[d], s2); s3 = fmaf(rb[d], rb[d], s3); s4 = fmaf(ra[d], rb[d], s4);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (k) {
+        const float na = ra[k + 6], nb = rb[k + 6], oa = ra[k - 1], ob = rb[k - 1];
+        s2 = fmaf(-oa, oa, fmaf(na, na, s2));
+        s3 = fmaf(-ob, ob, fmaf(nb, nb, s3));
+        s4 = fmaf(-oa, ob, fmaf(na, nb, s4));
+      }
+      const int rr = 8 * wv + k;
+      v[0][rr][c] = s2 * kInv7f;
+      v[1][rr][c] = s3 * kInv7f;
+      v[2][rr][c] = s4 * kInv7f;
+    }
+  }
+  __syncthreads();
   const float C1 = cst[0], C2 = cst[1];
   float acc = 0.f;
-  if (c0 < kSsTW && i >= 3 && i < H - 3) {
-    float h[5];
+  if (hrow) {
+    float h[3];
 #pragma unroll
-    for (int u = 0; u < 5; ++u) {
+    for (int u = 0; u < 3; ++u) {
       float t = 0.f;
 #pragma unroll
       for (int d = 0; d < 7; ++d) t += v[u][r][c0 + d];
@@ -1697,11 +1737,11 @@ __global__ __launch_bounds__(256) void ssim_rgb_kernel(const float* __restrict__
     for (int k = 0; k < 8; ++k) {
       if (k) {
 #pragma unroll
-        for (int u = 0; u < 5; ++u) h[u] = (h[u] + v[u][r][c0 + k + 6]) - v[u][r][c0 + k - 1];
+        for (int u = 0; u < 3; ++u) h[u] = (h[u] + v[u][r][c0 + k + 6]) - v[u][r][c0 + k - 1];
       }
       const int j = j0 + c0 + k;
       if (j >= 3 && j < W - 3)
-        acc += ssim_s(h[0] * kInv7f, h[1] * kInv7f, h[2] * kInv7f, h[3] * kInv7f, h[4] * kInv7f, 49.f / 48.f, C1, C2);
+        acc += ssim_s(ux[k], uy[k], h[0] * kInv7f, h[1] * kInv7f, h[2] * kInv7f, 49.f / 48.f, C1, C2);
     }
   }
   const double tot = block_sum((double)acc, red);
