@@ -19,8 +19,12 @@ synthetic RGB 256x256 images per GPU.  The other configurations are BASELINE.jso
     cfg4  32 x RGB 512^2 per GPU (256 over 8 GPUs), random sampling + Poisson, ours-C
     cfg5  64 x RGB 1024^2 per GPU (512 over 8), blur + Gaussian + sparse, comparisonB-2 (ADMM,
           m1 = 35, m2 = 5); one step = one outer iteration.
-Images are independent, so ranks process disjoint shards with no data-path collective (weak
-scaling).  ``value`` = image-iterations/s over the whole job (sum over ranks / max rank time).
+Images are independent, so ranks process disjoint contiguous shards of one global batch with no
+data-path collective.  ``--scaling strong`` (default) keeps the config's batch as the GLOBAL
+batch (the metric's 256 images: 256 / N per GPU); ``--scaling weak`` gives every
+rank the config's batch (256 N in all).  With N > 1 a strong line also carries a weak leg timed
+in the same run (``weak_scaling``).  ``value`` = image-iterations/s over the whole job (images
+of all ranks x K / the slowest rank's time).
 
 Also reported: ``roofline`` of the dominant kernel (at the metric conv_body_x8, two 64->64
 layers per launch, MFMA-bound at 576 FLOP/B: algorithmic FLOPs / HIP-event duration vs the
@@ -126,6 +130,41 @@ def synthetic_batch(B, C, H, W, seed):
                 img[y0:y0 + rng.integers(4, H // 4), x0:x0 + rng.integers(4, W // 4)] += rng.uniform(-0.3, 0.3)
             out[b, c] = np.clip(img, 0, 1)
     return out
+
+
+def synthetic_images(lo, hi, C, H, W, seed=1):
+    """Images lo .. hi-1 of an endless deterministic sequence of structured synthetic images in
+    [0,1] (image i from its own generator, seeded (seed, i)), float32: a rank generates only its
+    own shard, and image i is the same whatever the number of ranks or the scaling mode."""
+    yy, xx = np.meshgrid(np.linspace(0, 1, H, dtype=np.float32), np.linspace(0, 1, W, dtype=np.float32),
+                         indexing="ij")
+    out = np.empty((hi - lo, C, H, W), np.float32)
+    for b in range(lo, hi):
+        rng = np.random.default_rng([seed, b])
+        f = rng.uniform(1, 6, (C, 2)).astype(np.float32)
+        ph = rng.uniform(0, 6.28, C).astype(np.float32)
+        for c in range(C):
+            img = 0.45 + 0.25 * np.sin(2 * np.pi * f[c, 0] * xx + ph[c]) * np.cos(2 * np.pi * f[c, 1] * yy) \
+                + 0.2 * (xx - 0.5)
+            for _ in range(3):
+                y0, x0 = rng.integers(0, H - H // 4), rng.integers(0, W - W // 4)
+                img[y0:y0 + rng.integers(4, H // 4), x0:x0 + rng.integers(4, W // 4)] += rng.uniform(-0.3, 0.3)
+            out[b - lo, c] = np.clip(img, 0, 1)
+    return out
+
+
+def rank_shard(cfg_batch, world, rank, scaling):
+    """(global batch, lo, hi): the images [lo, hi) of the global batch this rank solves.  strong:
+    the config's batch is the global one, split into contiguous shards (pnppds.shard.shard_bounds:
+    256 over 8 ranks = 32 each); weak: every rank gets the config's batch, rank r images
+    [r B, (r + 1) B) of a global batch of B N."""
+    from pnppds.shard import shard_bounds
+    if scaling == "weak":
+        return cfg_batch * world, rank * cfg_batch, (rank + 1) * cfg_batch
+    if cfg_batch < world:
+        raise SystemExit(f"--scaling strong: a global batch of {cfg_batch} cannot feed {world} ranks")
+    lo, hi = shard_bounds(cfg_batch, world, rank)
+    return cfg_batch, lo, hi
 
 
 def images_per_launch(B, H, W, chunk, fp32=False, x3=False):
@@ -234,17 +273,24 @@ def host_cpu_info():
             "threads_used": usable}
 
 
-def cgroup_throttled_s():
-    """Seconds this cgroup has been throttled by its CPU quota (cgroup v2 cpu.stat), or None."""
+def cgroup_cpu_stat():
+    """(throttled seconds, throttled periods) of this cgroup (cgroup v2 cpu.stat), or (None, None)."""
+    out = {}
     try:
         with open("/sys/fs/cgroup/cpu.stat") as f:
             for line in f:
                 k, v = line.split()
-                if k == "throttled_usec":
-                    return int(v) / 1e6
+                out[k] = int(v)
     except (OSError, ValueError):
-        pass
-    return None
+        return None, None
+    if "throttled_usec" not in out:
+        return None, None
+    return out["throttled_usec"] / 1e6, out.get("nr_throttled")
+
+
+def cgroup_throttled_s():
+    """Seconds this cgroup has been throttled by its CPU quota (cgroup v2 cpu.stat), or None."""
+    return cgroup_cpu_stat()[0]
 
 
 def proc_threads():
@@ -259,6 +305,35 @@ def proc_threads():
     return None
 
 
+def one_cpu_per_core(allowed):
+    """The CPUs of `allowed` with one logical CPU per physical core (sysfs thread_siblings_list),
+    in CPU order: a leg pinned to the first t of them runs t threads on t distinct cores."""
+    seen, out = set(), []
+    for c in sorted(allowed):
+        try:
+            with open(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list") as f:
+                sib = f.read().strip()
+        except OSError:
+            sib = f"cpu{c}"
+        if sib not in seen:
+            seen.add(sib)
+            out.append(c)
+    return out or sorted(allowed)
+
+
+def pin_process(cpus):
+    """Pin every thread of this process (the torch / OpenMP pools included: threads created
+    later inherit their creator's mask) to `cpus`.  Returns the number of threads pinned."""
+    n = 0
+    for tid in os.listdir("/proc/self/task"):
+        try:
+            os.sched_setaffinity(int(tid), cpus)
+            n += 1
+        except OSError:
+            pass
+    return n
+
+
 def thread_sweep(usable):
     """torch thread counts of the CPU leg's sweep: 4, 8, 12, 16 capped at the usable CPUs."""
     ts = sorted({t for t in (4, 8, 12, 16) if t <= usable} | {usable})
@@ -267,14 +342,15 @@ def thread_sweep(usable):
 
 def cpu_baseline(cfg, x_true, x_obs, x_0, h, budget_s, max_iter):
     """Oracle restatement of test_iter (numpy FFT / mask, sort-based l1, torch-CPU conv) on
-    image 0, on this host's CPUs, after the GPU work has drained (the timed
-    region is over and the device is idle, so the GPU process's runtime threads are asleep).
-    A thread sweep (4 / 8 / 12 / 16 torch threads, capped at the CPUs this process may use) in three
-    interleaved rounds records, per run, the rate, the process's CPU use and the cgroup's
-    quota-throttled seconds.  Returns (best image-iters/s, sample description, PSNR track, info):
-    the best rate is the CPU's fair best case (r04 measured 4.05 to 12.9 for one workload on
-    16 threads in a 16-CPU quota, the throttled runs contending with the process's own runtime
-    threads); info carries the median, the sweep and the thread count at the best rate."""
+    image 0, on this host's CPUs, before the process touches the GPU.  A thread
+    sweep (4 / 8 / 12 / 16 torch threads, capped at the CPUs this process may use) in three
+    interleaved rounds; each leg pins the whole process to as many CPUs as it has threads, one per
+    physical core (one_cpu_per_core, pin_process), so a leg can never exceed the cgroup's CPU quota
+    with its own threads (r05: up to 17.7 s of quota throttling per sweep, rates 3.8-10.8 within
+    one run).  Per run: the rate, the process's CPU use, the cgroup's quota-throttled seconds and
+    periods, the 1-minute load average, and why a throttled run was throttled.  Returns (value,
+    sample description, PSNR track, info): value = the median rate at the thread count whose
+    median is highest (the sweep's repeatable figure; info also carries the best single run)."""
     import torch
     from oracle import pnp_oracle as O
     from pnppds.weights import resolve_weights
@@ -291,58 +367,82 @@ def cpu_baseline(cfg, x_true, x_obs, x_0, h, budget_s, max_iter):
         # linear in pixels; the FFT blur's N log N makes the scaled figure slightly optimistic)
         scale = (xo.shape[-1] * xo.shape[-2]) / (256.0 * 256.0)
         xo, x0, xt = xo[..., :256, :256], x0[..., :256, :256], xt[..., :256, :256]
+    allowed = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else list(range(os.cpu_count()))
+    cores = one_cpu_per_core(allowed)
+    quota = info["cgroup_quota_cpus"]
 
     def run(n, threads):
+        cpus = cores[:threads] if len(cores) >= threads else allowed[:threads]
+        pin_process(cpus)
         torch.set_num_threads(threads)
-        thr0 = cgroup_throttled_s()
+        thr0, nthr0 = cgroup_cpu_stat()
         t, c = time.perf_counter(), time.process_time()
         res = O.test_iter(x0, xo, xt, phi, adj, cfg["g1"], cfg["g2"], cfg["a_s"], cfg["a_n"], cfg["lam"], cfg["m1"],
                           cfg["m2"], 0.1, cfg["sigma"], cfg["sp"], POISSON_ALPHA, den, n, cfg["method"], C, cfg["r"])
         el = time.perf_counter() - t
-        thr1 = cgroup_throttled_s()
-        rec = {"threads": threads, "iters": n, "rate": round(n / (el * scale), 5),
-               "cpu_use_of_threads": round((time.process_time() - c) / max(el * threads, 1e-9), 3),
-               "throttled_s": round(thr1 - thr0, 3) if thr0 is not None and thr1 is not None else None}
+        cpu_s = time.process_time() - c
+        thr1, nthr1 = cgroup_cpu_stat()
+        throttled = round(thr1 - thr0, 3) if thr0 is not None and thr1 is not None else None
+        cause = None
+        if throttled:
+            cause = ("this process's threads above the cgroup quota" if quota and cpu_s / el > 0.95 * quota else
+                     "other processes of the cgroup (this process stayed within its pinned CPUs)")
+        rec = {"threads": threads, "cpus": f"{cpus[0]}-{cpus[-1]}" if cpus == list(range(cpus[0], cpus[-1] + 1))
+               else ",".join(map(str, cpus)), "iters": n, "rate": round(n / (el * scale), 5),
+               "cpu_use_of_threads": round(cpu_s / max(el * threads, 1e-9), 3),
+               "throttled_s": throttled,
+               "throttled_periods": (nthr1 - nthr0) if nthr0 is not None and nthr1 is not None else None,
+               "throttle_cause": cause, "loadavg_1m": round(os.getloadavg()[0], 2)}
         return rec, res
 
     sweep = thread_sweep(info["threads_used"])
-    run(1, sweep[-1])                                              # warm-up (thread pool, caches)
-    t_cal, _ = run(1, sweep[-1])                                   # calibration
-    per_iter = max(t_cal["iters"] / (t_cal["rate"] * scale), 1e-3)
-    # three interleaved rounds over the thread counts: the host's speed drifts within a run (r05:
-    # one box's calibration ran at 10 iterations/s, its later runs at 4-5; another box ran 4 and 8
-    # threads at ~4 and 12 and 16 at 10-12), so each count is sampled at three different times
-    rounds = 3
-    if per_iter * rounds * len(sweep) > 2 * budget_s:   # one iteration per run already exceeds the budget
-        sweep, rounds = [sweep[-1]], 2                    # (cfg5's outer iteration): all threads, two runs
-    n = int(min(max_iter, max(1, budget_s / (rounds * len(sweep)) / per_iter)))
-    recs, res = [], None
-    for _ in range(rounds):
-        for threads in sweep:
-            rec, res = run(n, threads)
-            recs.append(rec)
-    best = max(recs, key=lambda r_: r_["rate"])
-    at_best = [r_["rate"] for r_ in recs if r_["threads"] == best["threads"]]
+    try:
+        run(1, sweep[-1])                                              # warm-up (thread pool, caches)
+        t_cal, _ = run(1, sweep[-1])                                   # calibration
+        per_iter = max(t_cal["iters"] / (t_cal["rate"] * scale), 1e-3)
+        # three interleaved rounds over the thread counts: the host's speed drifts within a run, so
+        # each count is sampled at three different times
+        rounds = 3
+        if per_iter * rounds * len(sweep) > 2 * budget_s:   # one iteration per run already exceeds the budget
+            sweep, rounds = [sweep[-1]], 2                    # (cfg5's outer iteration): all threads, two runs
+        n = int(min(max_iter, max(1, budget_s / (rounds * len(sweep)) / per_iter)))
+        recs, res = [], None
+        for _ in range(rounds):
+            for threads in sweep:
+                rec, res = run(n, threads)
+                recs.append(rec)
+    finally:
+        pin_process(allowed)                                          # the GPU part runs unpinned
+    med = {t: float(np.median([r_["rate"] for r_ in recs if r_["threads"] == t])) for t in sweep}
+    best_t = max(med, key=med.get)
+    at_best = [r_["rate"] for r_ in recs if r_["threads"] == best_t]
     rates = [r_["rate"] for r_ in recs]
-    info.update({"sweep": recs, "best_threads": best["threads"], "median": round(float(np.median(rates)), 5),
-                 "median_at_best_threads": round(float(np.median(at_best)), 5),
-                 "spread": round((max(rates) - min(rates)) / max(best["rate"], 1e-12), 3),
+    best_run = max(recs, key=lambda r_: r_["rate"])
+    info.update({"sweep": recs, "best_threads": best_t, "median": round(float(np.median(rates)), 5),
+                 "median_at_best_threads": round(med[best_t], 5), "median_by_threads": {str(t): round(v, 5)
+                                                                                       for t, v in med.items()},
+                 "best_run": best_run["rate"], "best_run_threads": best_run["threads"],
+                 "spread_at_best_threads": round((max(at_best) - min(at_best)) / max(med[best_t], 1e-12), 3),
+                 "spread": round((max(rates) - min(rates)) / max(med[best_t], 1e-12), 3),
                  "cgroup_throttled_s": round(sum(r_["throttled_s"] or 0.0 for r_ in recs), 3)
                  if recs[0]["throttled_s"] is not None else None,
-                 "process_threads": proc_threads(), "torch_threads": best["threads"]})
+                 "process_threads": proc_threads(), "torch_threads": best_t,
+                 "pinning": f"each leg pinned to as many CPUs as threads, one per physical core "
+                            f"({len(cores)} cores among {len(allowed)} allowed CPUs)"})
     what = (f"oracle {cfg['method']} ({cfg['op']}) on image 0" if scale == 1.0 else
             f"oracle comparisonB-2 on the 256x256 crop of image 0 at m1={cfg['m1']}, m2={cfg['m2']}, scaled "
             f"by pixels x{scale:g} to the config's image (one step = one outer iteration)")
-    sample = (f"{what}: {n} iterations per run, {rounds} interleaved rounds over {sweep} torch threads after a "
-              f"warm-up, wall clock; value = the best run ({best['threads']} threads), median of all runs "
-              f"{info['median']:.4g}")
-    return best["rate"], sample, (res[3] if scale == 1.0 else None), info
+    sample = (f"{what}: {n} iterations per run, {rounds} interleaved rounds over {sweep} torch threads (each leg "
+              f"pinned to that many physical cores) after a warm-up, wall clock; value = the median of the "
+              f"{len(at_best)} runs at {best_t} threads (the best median; spread {info['spread_at_best_threads']:.0%}), "
+              f"best single run {best_run['rate']:.4g}")
+    return med[best_t], sample, (res[3] if scale == 1.0 else None), info
 
 
 def converge_full_run(ctx, torch, d_x0, d_obs, d_true, prm, method, B, C, H, W, iters):
     """precision='converge' over a whole solve of `iters` iterations from iteration 0 on the same
-    inputs (the experiments' 1200 for blur, main.py:136-139): the fp16 opening, the hand-over
-    when the batch's smallest c_n falls below 3e-3, and fp16a2 for the rest, so the returned c_n
+    inputs (the experiments' 1200 for blur, main.py:136-139): the fp16 opening, each image's
+    hand-over when its own c_n falls below 3e-3, and fp16a2 for the rest, so the returned c_n
     follows the reference's curve.  A short untimed converge solve first allocates
     the split-activation buffers.  Timed like the headline: synchronize, wall clock, synchronize."""
     ctx.profile_enable(False)
@@ -360,17 +460,49 @@ def converge_full_run(ctx, torch, d_x0, d_obs, d_true, prm, method, B, C, H, W, 
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
         sw = ctx.get_precision_switch()
+        sws = ctx.get_precision_switches(B)
         after = ctx.get_precision()[1]
         _, _, c, p, _ = ctx.solver_fetch()
     finally:
         ctx.set_precision("auto")
     return {"value": round(B * iters / el, 2), "unit": "image-iterations/s", "iterations": iters,
             "ms_per_iteration": round(1e3 * el / iters, 3), "switch_iteration": sw,
-            "precision": f"fp16 until iteration {sw}, then {after}",
+            "switch_span": [int(sws.min()), int(sws.max())],
+            "precision": f"per image: fp16 until iteration {int(sws.min())}-{int(sws.max())}, then {after}",
             "c_img0": [float(c[0, 0]), float(c[0, iters - 1])],
             "psnr_img0_db": [round(float(p[0, 0]), 4), round(float(p[0, iters - 1]), 4)],
             "note": "whole solve from iteration 0, c_n recorded every iteration (SSIM too); the headline "
                     "value is the fp16 steady state, whose c_n floors near 3e-4"}
+
+
+def weak_leg(ctx, torch, dist, cfg, world, rank, local, rehearsal, prm, method, K, Wm, max_over_ranks):
+    """N > 1 under --scaling strong: the weak-scaling leg in the same run, every rank solving the
+    config's batch (its images [r B, (r + 1) B) of a global batch of B N), degraded on the device as
+    the strong leg's, Wm warm-up steps, then K steps between barriers, max over ranks."""
+    _, lo, hi = rank_shard(cfg["B"], world, rank, "weak")
+    B, C, H, W = hi - lo, cfg["C"], cfg["S"], cfg["S"]
+    from pnppds import _lib
+    d_true = torch.from_numpy(synthetic_images(lo, hi, C, H, W)).cuda(local)
+    d_obs, d_x0 = torch.empty_like(d_true), torch.empty_like(d_true)
+    ctx.degrade(_lib.pnp_degrade_params(cfg["sigma"], cfg["sp"], POISSON_ALPHA, 1 if cfg["poisson"] else 0, 1234),
+                d_true.data_ptr(), B, C, H, W, xobs=d_obs.data_ptr(), x0=d_x0.data_ptr())
+    ctx.profile_enable(0)
+    ctx.solver_setup(method, prm, B, C, H, W, Wm + K)
+    ctx.solver_load_device(d_x0.data_ptr(), d_obs.data_ptr(), d_true.data_ptr())
+    ctx.solver_iterate(Wm)
+    ctx.synchronize()
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ctx.solver_iterate(K)
+    ctx.synchronize()
+    torch.cuda.synchronize()
+    t_el = time.perf_counter() - t0
+    dist.barrier()
+    t_el = max_over_ranks(t_el, device=None if rehearsal else f"cuda:{local}")
+    del d_true, d_obs, d_x0
+    return weak_fields(cfg, world, K, t_el)
 
 
 def cpu_leg_before_gpu(cfg, args):
@@ -381,7 +513,7 @@ def cpu_leg_before_gpu(cfg, args):
     from pnppds.operators import load_blur_kernel
     C, H = cfg["C"], cfg["S"]
     h = load_blur_kernel("blur_1")
-    xt = synthetic_batch(1, C, H, H, seed=1)[0]           # image 0 of rank 0's batch (seed 1000 * 0 + 1)
+    xt = synthetic_images(0, 1, C, H, H)[0]               # image 0 of the global batch (rank 0's first)
     img = xt[0] if C == 1 else xt                         # gray: the reference's (H, W) arrays
     obs, x0 = O.make_observation(img.astype(np.float64), cfg["op"], h, cfg["r"], cfg["sigma"], cfg["sp"],
                                  cfg["poisson"], POISSON_ALPHA)
@@ -461,29 +593,50 @@ DTYPES = {"fp16": "fp16-mfma/fp32-acc+state", "fp16w2": "fp16-mfma(split fp16 hi
 DTYPES_SHORT = {"fp16": "fp16", "fp16w2": "fp16w2"}
 
 
-def base_line(cfg, config_name, world, K, Wm, t_el, precision, prec_req):
+def base_line(cfg, config_name, world, K, Wm, t_el, precision, prec_req, scaling="strong", global_batch=None,
+              per_rank=None):
     """The contract fields of the JSON line: ``value`` = image-iterations/s of the whole job
-    (cfg['B'] images per rank x world ranks x K steps / the slowest rank's time), weak scaling."""
-    B, C, H, W = cfg["B"], cfg["C"], cfg["S"], cfg["S"]
-    is_metric = cfg["op"] == "blur" and cfg["method"] == "A-Proposed" and B == 256 and C == 3 and H == 256
+    (global_batch images x K steps / the slowest rank's time).  cfg['B'] is the config's batch:
+    the global batch under strong scaling (per_rank = the shard sizes), the per-rank one under
+    weak scaling (global_batch = cfg['B'] x world)."""
+    Bc, C, H, W = cfg["B"], cfg["C"], cfg["S"], cfg["S"]
+    if global_batch is None:
+        global_batch = Bc * world if scaling == "weak" else Bc
+    is_metric = cfg["op"] == "blur" and cfg["method"] == "A-Proposed" and Bc == 256 and C == 3 and H == 256
     metric = METRIC if is_metric else \
-        f"PDS iters/sec ({config_name}: {cfg['method']} {cfg['op']}, {B} x {C}x{H}x{W} per GPU); PSNR Δ vs ref"
+        f"PDS iters/sec ({config_name}: {cfg['method']} {cfg['op']}, {Bc} x {C}x{H}x{W} " \
+        f"{'per GPU' if scaling == 'weak' else 'in all'}); PSNR Δ vs ref"
     arch = f"DnCNN_nobn_nch_{C}_nlev_0.01"
+    if per_rank is None:
+        per_rank = [hi - lo for _, lo, hi in (rank_shard(Bc, world, r, scaling) for r in range(world))]
     return {
-        "metric": metric, "value": round(B * world * K / t_el, 2), "unit": "image-iterations/s",
+        "metric": metric, "value": round(global_batch * K / t_el, 2), "unit": "image-iterations/s",
         "n_gpus": world, "steps": K, "warmup": Wm,
-        "ms_per_step": round(1e3 * t_el / K, 3), "higher_is_better": True, "scaling": "weak",
+        "ms_per_step": round(1e3 * t_el / K, 3), "higher_is_better": True, "scaling": scaling,
         "vs_baseline": None,
         "dtype": DTYPES[precision],
         "data": f"synthetic structured images, x_obs from the device observation pipeline (main.py:49-64: "
                 f"{cfg['op']}, sigma={cfg['sigma']}, sp={cfg['sp']}, poisson={cfg['poisson']}, "
                 f"np.random.seed(1234) streams); real {arch} weights",
-        "config": {"workload": cfg["desc"].format(B=B, S=H), "config": config_name, "global_batch": B * world,
+        "config": {"workload": cfg["desc"].format(B=Bc, S=H).replace(
+                       "/GPU", "/GPU" if scaling == "weak" else f" in all ({'/'.join(map(str, sorted(set(per_rank))))} per GPU)"),
+                   "config": config_name, "global_batch": global_batch, "images_per_gpu": per_rank,
                    "image": f"{C}x{H}x{W}", "deg_op": "blur_1" if cfg["op"] == "blur" else cfg["op"],
                    "method": cfg["method"], "precision": precision, "precision_requested": prec_req,
-                   "parallelism": f"dp{world} (independent image shards, no collective)"},
+                   "parallelism": f"dp{world} (independent contiguous image shards, no collective; {scaling} "
+                                  f"scaling)"},
         "batch_iters_per_s": round(K / t_el, 3),
     }
+
+
+def weak_fields(cfg, world, K, t_el):
+    """The weak leg of an N > 1 strong-scaling line: every rank solving the config's batch (the
+    metric's 256 images per GPU, 256 N in all), K steps timed like the line's own."""
+    return {"value": round(cfg["B"] * world * K / t_el, 2), "unit": "image-iterations/s",
+            "ms_per_step": round(1e3 * t_el / K, 3), "global_batch": cfg["B"] * world, "images_per_gpu": cfg["B"],
+            "scaling": "weak", "steps": K,
+            "note": "timed in the same run after the strong leg: the config's batch on every rank, the same "
+                    "barrier + max-over-ranks clock"}
 
 
 def selftest_ranks(args):
@@ -503,10 +656,17 @@ def selftest_ranks(args):
     dist.barrier()
     t = max_over_ranks(0.01 * (rank + 1) * args.steps)
     dist.barrier()
+    tw = None
+    if args.scaling == "strong" and world > 1 and args.weak_leg:    # the weak leg, as the GPU path times it
+        dist.barrier()
+        tw = max_over_ranks(0.02 * (rank + 1) * args.steps)
+        dist.barrier()
     if rank == 0:
         cfg = dict(CONFIGS[args.config])
-        line = base_line(cfg, args.config, world, args.steps, args.warmup, t, "fp16", "auto")
+        line = base_line(cfg, args.config, world, args.steps, args.warmup, t, "fp16", "auto", args.scaling)
         line.update({"ranks_local": [int(os.environ["LOCAL_RANK"])], "max_t": t})
+        if tw is not None:
+            line["weak_scaling"] = weak_fields(cfg, world, args.steps, tw)
         print(json.dumps(line), flush=True)
     dist.destroy_process_group()
 
@@ -517,7 +677,13 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="metric", choices=sorted(CONFIGS))
-    ap.add_argument("--batch", type=int, default=0, help="images per GPU (0 = the config's)")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="the config's batch (0 = the config's): global under --scaling strong, per GPU under weak")
+    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
+                    help="strong (default): the config's batch is the global batch, split over the ranks "
+                         "(256 / N per GPU for the metric); weak: the config's batch on every rank")
+    ap.add_argument("--weak-leg", type=int, default=1, choices=[0, 1],
+                    help="N > 1 with --scaling strong: also time the weak-scaling leg in the same run")
     ap.add_argument("--size", type=int, default=0, help="image side (0 = the config's)")
     ap.add_argument("--op", default="", choices=["", "blur", "Id", "random_sampling"],
                     help="override the config's degradation operator (profiling the elementwise K1/K2)")
@@ -569,6 +735,7 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    glob_b, lo, hi = rank_shard(cfg["B"], world, rank, args.scaling)   # this rank's images [lo, hi)
     cpu_res = None
     if world == 1 and not args.no_cpu_baseline:
         # the CPU leg runs first, before this process initializes the GPU: r05 measured 4-5 vs
@@ -592,7 +759,7 @@ def main():
     from pnppds.shard import max_over_ranks
     from pnppds.weights import resolve_weights
 
-    B, C, H, W = cfg["B"], cfg["C"], cfg["S"], cfg["S"]
+    B, C, H, W = hi - lo, cfg["C"], cfg["S"], cfg["S"]      # B: this rank's images
     K, Wm = args.steps, args.warmup
     arch = f"DnCNN_nobn_nch_{C}_nlev_0.01"
     ctx = _lib.Context(local)
@@ -613,7 +780,7 @@ def main():
 
     # ---- synthetic inputs, degraded on the device exactly as main.py:49-64 does ---------------
     t0 = time.perf_counter()
-    x_true = synthetic_batch(B, C, H, W, seed=1000 * rank + 1)
+    x_true = synthetic_images(lo, hi, C, H, W)
     d_true = torch.from_numpy(x_true).cuda(local)
     d_obs = torch.empty_like(d_true)
     d_x0 = torch.empty_like(d_true)
@@ -664,6 +831,17 @@ def main():
     prof_timed = ctx.profile_read() if args.profile else {}
     x_out, s_out, c_hist, psnr_hist, ssim_hist = ctx.solver_fetch()
     switch_it = ctx.get_precision_switch()
+    switch_span = None
+    if prec_req == "converge":        # per image (PNP_PREC_CONVERGE): earliest and latest over every rank's images
+        sws = ctx.get_precision_switches(B)
+        never = bool((sws < 0).any())
+        first = int(sws[sws >= 0].min()) if (sws >= 0).any() else 1 << 30
+        last_sw = (1 << 30) if never else int(sws.max())
+        if world > 1:
+            dev = None if rehearsal else f"cuda:{local}"
+            first = int(-max_over_ranks(-float(first), device=dev))
+            last_sw = int(max_over_ranks(float(last_sw), device=dev))
+        switch_span = [None if first == 1 << 30 else first, None if last_sw == 1 << 30 else last_sw]
     prof = {}
     if args.profile and not args.full_run:
         ctx.profile_enable(1)              # every launch, K untimed steps (kernel_ms, prox_hbm)
@@ -680,15 +858,24 @@ def main():
         body_prec = args.precision
     last = (K if args.full_run else Wm + K) - 1
 
+    weak = None
+    if world > 1 and args.scaling == "strong" and args.weak_leg:
+        weak = weak_leg(ctx, torch, dist, cfg, world, rank, local, rehearsal, prm, resolve_method(cfg["method"]),
+                        K, Wm, max_over_ranks)
+
     if rank == 0:
-        line = base_line(cfg, args.config, world, K, Wm, t_el, args.precision, prec_req)
+        line = base_line(cfg, args.config, world, K, Wm, t_el, args.precision, prec_req, args.scaling, glob_b)
+        if weak is not None:
+            line["weak_scaling"] = weak
         line["build_id"] = _lib.build_id()
         if args.full_run:
             line["full_run"] = f"the {K} timed steps are one solve from iteration 0 (state reloaded after the warm-up)"
         if prec_req == "converge":
             line["precision_switch_iteration"] = switch_it
-            line["config"]["precision"] = (f"converge: {DTYPES_SHORT.get(prec_fast, prec_fast)} until iteration "
-                                           f"{switch_it}, then {body_prec}")
+            line["precision_switch_span"] = switch_span
+            line["config"]["precision"] = (f"converge (per image): {DTYPES_SHORT.get(prec_fast, prec_fast)} until "
+                                           f"iteration {switch_span[0]}-{switch_span[1]} (first-last image over every "
+                                           f"rank), then {body_prec}")
         if prof:
             kt = {k: round(v[0], 4) for k, v in prof.items()}
             line["kernel_ms"] = kt
@@ -797,7 +984,10 @@ def main():
             line["cpu_baseline"] = {"value": round(rate, 4), "unit": "image-iterations/s",
                                     "cores": info["best_threads"], "kind": "port", "sample": sample,
                                     "median": info["median"], "median_at_best_threads": info["median_at_best_threads"],
+                                    "median_by_threads": info["median_by_threads"], "best_run": info["best_run"],
                                     "best_threads": info["best_threads"], "spread": info["spread"],
+                                    "spread_at_best_threads": info["spread_at_best_threads"],
+                                    "pinning": info["pinning"],
                                     # per run: threads, rate, process CPU seconds / (wall x threads) and the
                                     # cgroup's quota-throttled seconds (CPU contention)
                                     "sweep": info["sweep"], "cgroup_throttled_s": info["cgroup_throttled_s"],

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define PNP_ABI_VERSION 7
+#define PNP_ABI_VERSION 8
 
 typedef struct pnp_ctx pnp_ctx;
 
@@ -102,17 +102,19 @@ enum pnp_precision {
                         the fp16 activations' rounding sets a floor where successive
                         iterates stop contracting (the reference's c_n reaches ~7e-8).
                         Use PNP_PREC_CONVERGE where the c_n curve matters.            */
-  PNP_PREC_CONVERGE = 5, /* (ABI 7) per solve: AUTO's operands while the batch's smallest
-                        c_n is above a threshold (PNP_TUNE_CONVERGE_C, default 3e-3, ten
-                        times the fp16 floor), then split activations for the rest of the
-                        solve: FP16A2 where AUTO runs FP16 / FP16W2, FP16X3 elsewhere (where
-                        AUTO already runs it), so c_n follows the reference's down to ~1e-6
-                        (within 1-2 %; ~1.6e-7 floor).  Needs the metrics (record_metrics,
-                        within metrics_capacity) to watch c_n; without them it switches at
-                        once.  The switch is decided on the host one iteration behind the
-                        device (pnp_solver_iterate then blocks per iteration until it
-                        switches) and is per batch: see pnp_get_precision_switch.  Single
-                        denoiser calls run FP16X3.                                      */
+  PNP_PREC_CONVERGE = 5, /* (ABI 7; per image since ABI 8) per solve and per image: AUTO's
+                        operands while the image's own c_n is above a threshold
+                        (PNP_TUNE_CONVERGE_C, default 3e-3, ten times the fp16 floor), then
+                        split activations for the rest of the solve: FP16A2 where AUTO runs
+                        FP16 / FP16W2, FP16X3 elsewhere (where AUTO already runs FP16X3 it
+                        switches at once).  Needs recorded metrics (record_metrics, iterations
+                        within metrics_capacity) to watch c_n; without them every image
+                        switches at once.  The switch is decided on the host one iteration
+                        behind the device (pnp_solver_iterate then blocks per iteration until
+                        every image has switched); while only some have, each denoiser pass
+                        runs the batch as runs of consecutive images of one precision, so an
+                        image's results do not depend on its batch or shard.  See
+                        pnp_get_precision_switch(es).  Single denoiser calls run FP16X3.    */
   PNP_PREC_FP16A2 = 6   /* (ABI 7) activations split into fp16 hi + lo halves, single fp16
                         weights (rounded per filter as FP16's): two fp16 MFMAs per product in
                         the 64->64 layers (hi*w + lo*w); head and tail as FP16X3           */
@@ -155,10 +157,13 @@ int pnp_set_denoiser(pnp_ctx* ctx, int channels, int depth, int width, const flo
  * pnp_get_precision: the requested value and the one the next solver step will use.   */
 int pnp_set_precision(pnp_ctx* ctx, int precision);
 int pnp_get_precision(pnp_ctx* ctx, int* requested, int* effective);
-/* (ABI 7) PNP_PREC_CONVERGE: the first iteration of the current solve that ran split
- * activations (FP16A2 / FP16X3), or -1 when it has not switched (or the solve does not run
- * PNP_PREC_CONVERGE).                                                                       */
+/* (ABI 7) PNP_PREC_CONVERGE: the first iteration of the current solve from which every image
+ * ran split activations (FP16A2 / FP16X3), or -1 while some image has not switched (or the
+ * solve does not run PNP_PREC_CONVERGE).  For B = 1, the image's switch iteration.          */
 int pnp_get_precision_switch(pnp_ctx* ctx, int* iteration);
+/* (ABI 8) PNP_PREC_CONVERGE: per image b of the current solve, the first iteration it ran split
+ * activations (-1: not yet).  n must be at least the solve's batch B (PNP_E_ARG otherwise).  */
+int pnp_get_precision_switches(pnp_ctx* ctx, int* iterations, int n);
 
 /* Performance knobs (no effect on results; PNP_TUNE_CONVERGE_C excepted).
  * PNP_TUNE_DENOISE_CHUNK: images per denoiser pass (0 = auto: the whole batch, unless its

@@ -30,7 +30,7 @@ struct PnpError {
 struct DevBuf {
   void* p = nullptr;
   size_t bytes = 0;
-  long long geom = -1;   // zero-border buffers: the (B,H,W) their padding was zeroed for
+  long long geom = -1;   // zero-border buffers: the (H,W) the whole allocation was zeroed for
   DevBuf() = default;
   DevBuf(const DevBuf&) = delete;
   DevBuf& operator=(const DevBuf&) = delete;
@@ -62,13 +62,15 @@ struct pnp_ctx {
   bool den_ready = false;
   int prec_req = PNP_PREC_AUTO;   // pnp_set_precision (default: the per-solve policy, auto_precision)
   int prec = PNP_PREC_FP16X3;     // the operands the denoiser runs with now (resolved from prec_req)
-  // PNP_PREC_CONVERGE (converge_check): auto's operands until the batch's smallest c_n falls
-  // below conv_c, split fp16 from then on.  conv_row: pinned host rows of c_n (two slots of B
-  // doubles) copied after each watched iteration, conv_ev / conv_slot_it: their events and the
-  // iteration each slot holds.
+  // PNP_PREC_CONVERGE (converge_check): per image, auto's operands until the image's own c_n
+  // falls below conv_c, split activations from then on.  conv_row: pinned host rows of c_n (two
+  // slots of B doubles) copied after each watched iteration, conv_ev / conv_slot_it: their events
+  // and the iteration each slot holds.
   double conv_c = 3e-3;
-  bool conv_switched = false;
-  int conv_switch_it = -1;        // the first iteration run with split fp16 (-1: none yet)
+  bool conv_switched = false;     // every image has switched
+  int conv_switch_it = -1;        // the first iteration every image ran split (-1: not yet)
+  std::vector<int> conv_img_it;   // per image: its first split iteration (-1: not yet)
+  int conv_nsw = 0;               // images switched
   double* conv_row = nullptr;
   int conv_row_B = 0;
   hipEvent_t conv_ev[2] = {nullptr, nullptr};
@@ -337,14 +339,17 @@ size_t act_bytes(int B, int H, int W, int ch, int pad) {
 }
 
 // Padded activation images: the one-pixel border must be zero for the geometry in use.
-// Kernels never write the border, so a buffer is zeroed once per (B, H, W) it serves;
-// reusing it for another geometry (whose border lands on stale interior data) re-zeroes.
+// Kernels never write the border, so a buffer is zeroed once per (H, W) it serves, over its
+// whole allocation: an image's slot (offset and border) does not depend on the batch size, so
+// any batch the allocation holds finds its borders zero (PNP_PREC_CONVERGE's per-image passes
+// alternate batch sizes every iteration).  Reusing it for another image size (whose border
+// lands on stale interior data) re-zeroes; growing it reallocates (ensure resets geom).
 void ensure_padded(pnp_ctx* ctx, DevBuf& b, int B, int H, int W, int ch, int pad, hipStream_t st) {
   const size_t bytes = act_bytes(B, H, W, ch, pad);
-  const long long geom = ((long long)B << 40) ^ ((long long)H << 20) ^ (long long)W;
+  const long long geom = ((long long)H << 20) ^ (long long)W;
   ensure(ctx, b, bytes);
   if (b.geom != geom) {
-    HIPCHK(ctx, hipMemsetAsync(b.p, 0, bytes, st));
+    HIPCHK(ctx, hipMemsetAsync(b.p, 0, b.bytes, st));
     b.geom = geom;
   }
 }
@@ -470,9 +475,10 @@ void run_denoiser32(pnp_ctx* ctx, const float* u32, float* xout, DevBuf (&act32)
   }
 }
 
-// Denoiser forward over B images: u32 (NCHW fp32: the head's input and the residual) -> xout.
-void run_denoiser(pnp_ctx* ctx, const float* u32, float* xout, DevBuf (&act)[2], int B, int H,
-                  int W, hipStream_t st) {
+// Denoiser forward over B images with the operands ctx->prec: u32 (NCHW fp32: the head's input
+// and the residual) -> xout.
+void run_denoiser_prec(pnp_ctx* ctx, const float* u32, float* xout, DevBuf (&act)[2], int B, int H,
+                       int W, hipStream_t st) {
   if (!ctx->den_ready) fail(ctx, PNP_E_STATE, "denoiser not set (pnp_set_denoiser)");
   if (ctx->prec == PNP_PREC_FP32) {
     run_denoiser32(ctx, u32, xout, &act[0] == &ctx->act[0] ? ctx->act32 : ctx->scr_act32, B, H, W, st);
@@ -623,6 +629,38 @@ void run_denoiser(pnp_ctx* ctx, const float* u32, float* xout, DevBuf (&act)[2],
                        P<float>(ctx->tail_b), s, C, ctx->den_residual, ctx->den_clamp, ctx->num_cus, st);
       check_launch(ctx, "conv_tail");
     }
+  }
+}
+
+int converge_precision(int fast);
+
+// Denoiser forward over B images: u32 (NCHW fp32: the head's input and the residual) -> xout.
+// A solver pass under PNP_PREC_CONVERGE while only some images have switched runs each maximal
+// run of consecutive images with one precision as its own pass (ctx->prec for the images still
+// on auto's operands, converge_precision(ctx->prec) for the switched ones).  Per-image results
+// do not depend on how a batch is split into passes (test_batch_equals_single_images), so an
+// image's bits depend only on its own c_n history, not on its batch or shard.
+void run_denoiser(pnp_ctx* ctx, const float* u32, float* xout, DevBuf (&act)[2], int B, int H,
+                  int W, hipStream_t st) {
+  if (&act[0] != &ctx->act[0] || ctx->prec_req != PNP_PREC_CONVERGE || ctx->conv_switched || ctx->conv_nsw == 0 ||
+      B != ctx->B || (int)ctx->conv_img_it.size() != B) {
+    run_denoiser_prec(ctx, u32, xout, act, B, H, W, st);
+    return;
+  }
+  const int fast = ctx->prec, slow = converge_precision(fast);
+  struct Restore {
+    pnp_ctx* c;
+    int p;
+    ~Restore() { c->prec = p; }
+  } restore{ctx, fast};
+  const size_t img = (size_t)ctx->den_C * H * W;
+  for (int b0 = 0; b0 < B;) {
+    const bool sw = ctx->conv_img_it[b0] >= 0;
+    int b1 = b0 + 1;
+    while (b1 < B && (ctx->conv_img_it[b1] >= 0) == sw) ++b1;
+    ctx->prec = sw ? slow : fast;
+    run_denoiser_prec(ctx, u32 + b0 * img, xout + b0 * img, act, b1 - b0, H, W, st);
+    b0 = b1;
   }
 }
 
@@ -1053,27 +1091,43 @@ int effective_precision(const pnp_ctx* ctx) {
 // (iteration.py:187) stalls near 3e-4 where the reference's keeps contracting.
 // CONVERGE runs auto's operands while c_n is far above that floor, then split activations
 // (fp16a2 or fp16x3, converge_precision: c_n follows the reference's down to ~1e-7) for the rest
-// of the solve.  The switch
-// happens before iteration i + 2 when the smallest c_n of the batch at iteration i is below
-// conv_c: the host reads iteration i's c_n row while iteration i + 1 runs (a fixed lag of one,
-// so the decision does not depend on timing).  Without recorded metrics (record_metrics 0, or
-// the metrics capacity reached) there is no c_n to watch, and the solve switches at once.  The
-// switch is per batch: an image's iterates depend on its batch only through the switch
-// iteration (pnp_get_precision_switch reports it).
+// of the solve.  The switch is per image: image b runs split activations from iteration i + 2
+// on once its c_n at iteration i is below conv_c (the host reads iteration i's c_n row while
+// iteration i + 1 runs: a fixed lag of one, so the decision does not depend on timing), and
+// while only some images have switched each denoiser pass is split into runs of one precision
+// (run_denoiser).  An image's iterates therefore depend only on its own c_n, whatever batch or
+// shard it is solved in.  Without recorded metrics (record_metrics 0, or the metrics capacity
+// reached) there is no c_n to watch, and the images not yet switched switch at once.
+// pnp_get_precision_switches reports each image's switch iteration, pnp_get_precision_switch
+// the iteration from which the whole batch runs split.
 void converge_reset(pnp_ctx* ctx) {
   ctx->conv_switched = false;
   ctx->conv_switch_it = -1;
   ctx->conv_slot_it[0] = ctx->conv_slot_it[1] = -1;
+  ctx->conv_img_it.assign(std::max(ctx->B, 0), -1);
+  ctx->conv_nsw = 0;
+}
+
+void converge_switch_image(pnp_ctx* ctx, int b) {
+  if (ctx->conv_img_it[b] >= 0) return;
+  ctx->conv_img_it[b] = ctx->it;
+  if (++ctx->conv_nsw == ctx->B) {
+    ctx->conv_switched = true;
+    ctx->conv_switch_it = ctx->it;
+  }
 }
 
 void converge_switch(pnp_ctx* ctx) {
+  if ((int)ctx->conv_img_it.size() != ctx->B) converge_reset(ctx);
+  for (int b = 0; b < ctx->B; ++b) converge_switch_image(ctx, b);
   ctx->conv_switched = true;
-  ctx->conv_switch_it = ctx->it;
+  if (ctx->conv_switch_it < 0) ctx->conv_switch_it = ctx->it;
 }
 
-// true when the solve has switched (before iteration ctx->it)
+// true when every image has switched (before iteration ctx->it)
 bool converge_check(pnp_ctx* ctx) {
   if (ctx->conv_switched) return true;
+  if ((int)ctx->conv_img_it.size() != ctx->B) converge_reset(ctx);
   const int i = ctx->it;
   if (auto_precision(ctx->method, ctx->op_kind, ctx->prm.gaussian_nl) == PNP_PREC_FP16X3 ||
       !ctx->prm.record_metrics || i >= ctx->cap) {
@@ -1083,17 +1137,12 @@ bool converge_check(pnp_ctx* ctx) {
   const int k = i & 1;                        // slot of iteration i - 2
   if (i >= 2 && ctx->conv_slot_it[k] == i - 2) {
     HIPCHK(ctx, hipEventSynchronize(ctx->conv_ev[k]));
-    double mn = INFINITY;
-    for (int b = 0; b < ctx->B; ++b) {
-      const double v = ctx->conv_row[(size_t)k * ctx->B + b];
-      if (v < mn) mn = v;                     // NaN compares false: never triggers a switch
-    }
-    if (mn < ctx->conv_c) {
-      converge_switch(ctx);
-      return true;
-    }
+    const int before = ctx->conv_nsw;
+    for (int b = 0; b < ctx->B; ++b)          // NaN compares false: never triggers a switch
+      if (ctx->conv_img_it[b] < 0 && ctx->conv_row[(size_t)k * ctx->B + b] < ctx->conv_c) converge_switch_image(ctx, b);
+    if (ctx->conv_nsw != before) ctx->gen++;  // the passes' split changed (no graph runs before the end anyway)
   }
-  return false;
+  return ctx->conv_switched;
 }
 
 // after a watched iteration i (ctx->it == i + 1 now): queue the copy of its c_n row
@@ -1438,6 +1487,16 @@ int pnp_get_precision_switch(pnp_ctx* ctx, int* iteration) {
   if (!ctx || !iteration) return PNP_E_ARG;
   *iteration = ctx->conv_switch_it;
   return PNP_OK;
+}
+
+int pnp_get_precision_switches(pnp_ctx* ctx, int* iterations, int n) {
+  if (!ctx) return PNP_E_ARG;
+  return guarded(ctx, [&] {
+    if (!iterations || n < ctx->B)
+      fail(ctx, PNP_E_ARG, "need room for %d switch iterations (one per image), got %d", ctx->B, n);
+    for (int b = 0; b < ctx->B; ++b)
+      iterations[b] = b < (int)ctx->conv_img_it.size() ? ctx->conv_img_it[b] : -1;
+  });
 }
 
 int pnp_set_denoiser(pnp_ctx* ctx, int channels, int depth, int width, const float* params, size_t n_params,

@@ -50,7 +50,7 @@ class pnp_params(C.Structure):
                 ("record_ssim", C.c_int32)]
 
 
-ABI_VERSION = 7   # include/pnppds.h PNP_ABI_VERSION
+ABI_VERSION = 8   # include/pnppds.h PNP_ABI_VERSION
 class pnp_degrade_params(C.Structure):
     _fields_ = [("gaussian_nl", C.c_double), ("sp_nl", C.c_double), ("poisson_alpha", C.c_double),
                 ("poisson_noise", C.c_int32), ("seed", C.c_uint32)]
@@ -74,6 +74,7 @@ _SIGS = {
     "pnp_set_precision": ([_P, C.c_int], C.c_int),
     "pnp_get_precision": ([_P, C.POINTER(C.c_int), C.POINTER(C.c_int)], C.c_int),
     "pnp_get_precision_switch": ([_P, C.POINTER(C.c_int)], C.c_int),
+    "pnp_get_precision_switches": ([_P, C.POINTER(C.c_int), C.c_int], C.c_int),
     "pnp_device_copy": ([_P, _P, _P, C.c_size_t, _P], C.c_int),
     "pnp_set_tuning": ([_P, C.c_int, C.c_int], C.c_int),
     "pnp_set_operator": ([_P, C.c_int, _D, C.c_int, C.c_int, C.POINTER(C.c_uint8), C.c_int, C.c_int], C.c_int),
@@ -253,9 +254,11 @@ class Context:
         accumulation), 'fp16w2' (fp16 activations, weights as fp16 hi + lo pairs: two MFMAs per
         product), 'fp16x3' (activations and weights as hi + lo pairs: three MFMAs per product,
         near-fp32), 'fp32' (the reference's own precision, models/denoiser.py:37; about a
-        tenth of the fp16 throughput) or 'converge' (auto's operands while the batch's smallest
-        c_n is above 3e-3, split fp16 after: c_n then follows the reference's curve, which fp16
-        activations stop following below ~3e-4; get_precision_switch() says when it switched)."""
+        tenth of the fp16 throughput) or 'converge' (per image: auto's operands while the image's
+        own c_n is above 3e-3, then split activations -- fp16a2 on the blur family, where auto runs
+        fp16 / fp16w2, fp16x3 elsewhere: c_n then follows the reference's curve, which fp16
+        activations stop following below ~3e-4; get_precision_switches() says when each image
+        switched)."""
         code = PRECISIONS[precision] if isinstance(precision, str) else int(precision)
         self._check(self.lib.pnp_set_precision(self.h, code))
         self.precision = code
@@ -267,15 +270,24 @@ class Context:
         return PRECISION_NAMES[r.value], PRECISION_NAMES[e.value]
 
     def get_precision_switch(self) -> int:
-        """precision='converge': the first iteration of the current solve that ran split fp16
-        (fp16x3), or -1 if it has not switched (pnp_get_precision_switch)."""
+        """precision='converge': the first iteration of the current solve from which every image
+        ran split activations (fp16a2 on the blur family, fp16x3 elsewhere), or -1 while some
+        image has not switched (pnp_get_precision_switch; for one image, its switch)."""
         it = C.c_int()
         self._check(self.lib.pnp_get_precision_switch(self.h, C.byref(it)))
         return it.value
 
+    def get_precision_switches(self, batch: int) -> np.ndarray:
+        """precision='converge': per image of the current solve (``batch`` = its B), the first
+        iteration it ran split activations, -1 if not yet (pnp_get_precision_switches)."""
+        out = np.full(int(batch), -1, np.int32)
+        self._check(self.lib.pnp_get_precision_switches(self.h, out.ctypes.data_as(C.POINTER(C.c_int)),
+                                                        int(batch)))
+        return out
+
     def set_converge_threshold(self, c: float):
-        """precision='converge': switch to split fp16 once the batch's smallest c_n is below c
-        (default 3e-3; set in units of 1e-6, PNP_TUNE_CONVERGE_C)."""
+        """precision='converge': an image switches to split activations once its own c_n is below
+        c (default 3e-3; set in units of 1e-6, PNP_TUNE_CONVERGE_C)."""
         self._check(self.lib.pnp_set_tuning(self.h, TUNE_CONVERGE_C, max(1, int(round(c * 1e6)))))
 
     def set_denoise_chunk(self, images: int):

@@ -70,9 +70,10 @@ BM3D_METHODS = ("A-PnPPDS-BM3D", "A-PnPFBS-BM3D", "comparisonB-1", "C-PnPPDS-BM3
 # Under fp16 / fp16w2 operands x and PSNR follow the reference but the returned c (c_n,
 # iteration.py:187) does not below ~3e-4: the fp16 activations' rounding leaves successive
 # iterates ~3e-4 apart where the reference's keep contracting (to ~7e-8 after 1200 iterations).
-# 'converge' keeps auto's operands while the batch's smallest c_n is above 3e-3 and runs split
-# fp16 after that, so c follows the reference's curve (checked to 10 % wherever it is >= 1e-6);
-# last_precision_switch() reports the iteration it switched at.
+# 'converge' keeps auto's operands, per image, while the image's own c_n is above 3e-3 and runs
+# split activations after that (fp16a2 on the blur family, fp16x3 elsewhere), so c follows the
+# reference's curve (checked to 10 % wherever it is >= 1e-6) and an image's results do not
+# depend on its batch or shard; last_precision_switch() / last_precision_switches() report when.
 def resolve_precision(precision) -> str:
     if precision not in _lib.PRECISIONS:
         raise ValueError(f"precision must be one of {sorted(_lib.PRECISIONS)}, not {precision!r}")
@@ -80,8 +81,14 @@ def resolve_precision(precision) -> str:
 
 
 def last_precision_switch(ctx=None) -> int:
-    """After a precision='converge' solve: the first iteration that ran split fp16 (-1: none)."""
+    """After a precision='converge' solve: the first iteration from which every image ran split
+    activations (-1: some image never switched)."""
     return (ctx or get_ctx()).get_precision_switch()
+
+
+def last_precision_switches(batch: int, ctx=None) -> np.ndarray:
+    """After a precision='converge' solve of ``batch`` images: each image's switch iteration."""
+    return (ctx or get_ctx()).get_precision_switches(batch)
 
 
 def resolve_method(method: str) -> int:
@@ -120,7 +127,8 @@ def test_iter_batch(x_0, x_obsrv, x_true, phi, adj_phi, gamma1, gamma2, alpha_s,
     (the reference's, about 10x slower), 'fp16x3' (split fp16: hi + lo activations and weights,
     three MFMAs per product, near-fp32) or 'auto' (default: the library's per-solve policy,
     fp16 for ours-A/B and comparisonB-2 on blur, fp16x3 otherwise: c_n floors near 3e-4 under
-    fp16) or 'converge' (auto until c_n < 3e-3, then fp16x3: the reference's c_n curve)."""
+    fp16) or 'converge' (per image, auto until its c_n < 3e-3, then split activations: the
+    reference's c_n curve)."""
     m = resolve_method(method)
     _check_ops(phi, adj_phi)
     x0 = np.asarray(x_0)

@@ -185,7 +185,7 @@ def main(ref_root="/root/reference"):
     res = iteration.test_iter(x0, obs, xt, phi, adj, 0.99, 0.99, 1.0, 0.95, 1.0, 15, 15, 0.1, 0.01, 0.0, 300,
                               os.path.join(nn_dir, "DnCNN_nobn_nch_3_nlev_0.01.pth"), 120, "A-Proposed", 3, 0.8)
     np.savez_compressed(os.path.join(HERE, "long_A_blur_256.npz"), x_true=xt, x_obs=obs.astype(np.float32),
-                        x_out=res[0].astype(np.float16), c=res[2], psnr=res[3])
+                        x_out=res[0].astype(np.float32), c=res[2], psnr=res[3])
     print(f"long_A_blur_256.npz psnr {res[3][0]:.3f} -> {res[3][-1]:.3f} ({time.perf_counter()-t:.1f}s)")
 
 
@@ -322,7 +322,8 @@ def make_long_golden(ref_root="/root/reference", only=None):
     for blur), so the 0.01 dB PSNR bound is checked over every iteration rather than
     extrapolated from 120: ours-A 3x256^2 blur for 1200 iterations (the metric's method,
     operator and image size), ours-B blur + salt-and-pepper and ours-C random sampling + Poisson
-    at 3x128^2 for 300.  Stored: inputs, the per-iteration c and PSNR, the final x in fp16."""
+    at 3x128^2 for 300.  Stored: inputs, the per-iteration c and PSNR, the final x in fp32
+    (round 6: fp16 capped the x check at half an fp16 ulp, 2.4e-4)."""
     install_shims(ref_root)
     import operators as op
     import iteration
@@ -345,7 +346,7 @@ def make_long_golden(ref_root="/root/reference", only=None):
         xs, ss, c, ps, _ssim, _t = res
         small = (lambda a: np.asarray(a, np.float32)) if n >= 256 else np.asarray   # fixture size
         np.savez_compressed(os.path.join(HERE, f"long_{name}.npz"), x_true=xt, x_obs=small(obs),
-                            x_0=small(x0), x_out=np.asarray(xs).astype(np.float16), c=c, psnr=ps,
+                            x_0=small(x0), x_out=np.asarray(xs).astype(np.float32), c=c, psnr=ps,
                             params=np.array([g1, g2, as_, an, lam, m1, m2, 0.1, sig, sp, 300, iters, ch, r]),
                             method=np.array(method), deg_op=np.array(deg), arch=np.array(arch))
         print(f"long_{name}.npz psnr {ps[0]:.3f} -> {ps[-1]:.3f} ({time.perf_counter()-t:.1f}s)", flush=True)

@@ -52,6 +52,7 @@ int main() {
   EXPECT(pnp_get_precision(nullptr, &k, &k) == PNP_E_ARG);
   EXPECT(pnp_set_precision(nullptr, PNP_PREC_CONVERGE) == PNP_E_ARG);
   EXPECT(pnp_get_precision_switch(nullptr, &k) == PNP_E_ARG);
+  EXPECT(pnp_get_precision_switches(nullptr, &k, 1) == PNP_E_ARG);
   EXPECT(pnp_set_tuning(nullptr, 0, 0) == PNP_E_ARG);
   EXPECT(pnp_set_operator(nullptr, PNP_OP_ID, nullptr, 0, 0, nullptr, 0, 0) == PNP_E_ARG);
   EXPECT(pnp_run(nullptr, PNP_METHOD_A, &prm, 1, 3, 8, 8, &f, &f, &f, 1, &f, &f, &d, &d, &d, &d) == PNP_E_ARG);

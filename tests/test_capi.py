@@ -56,7 +56,7 @@ def test_exports_are_plain_c(lib):
 
 def test_abi_version_and_errors_without_gpu(lib):
     from pnppds import _lib
-    assert lib.pnp_abi_version() == _lib.ABI_VERSION == 7
+    assert lib.pnp_abi_version() == _lib.ABI_VERSION == 8
     lib.pnp_last_error.restype = ctypes.c_char_p
     h = ctypes.c_void_p()
     rc = lib.pnp_create(0, ctypes.byref(h))
@@ -71,6 +71,7 @@ def test_null_context_is_rejected(lib):
     assert lib.pnp_synchronize(None) == -1
     it = ctypes.c_int(5)
     assert lib.pnp_get_precision_switch(None, ctypes.byref(it)) == -1 and it.value == 5
+    assert lib.pnp_get_precision_switches(None, ctypes.byref(it), 1) == -1 and it.value == 5
     assert lib.pnp_set_precision(None, 5) == -1
 
 

@@ -6,7 +6,6 @@ for i in $(seq 1 20); do
   /usr/local/graft/bin/gpurun --timeout $T -- "$@"
   rc=$?
   if [ $rc -ne 3 ] && ! grep -q '"status": "transient"' /root/repo/gpurun_out/.last_call.json 2>/dev/null; then exit $rc; fi
-  if [ $rc -ne 3 ] && [ $rc -ne 0 ] && ! grep -q '"status": "transient"' /root/repo/gpurun_out/.last_call.json; then exit $rc; fi
   sleep 100
 done
 exit $rc
