@@ -549,8 +549,9 @@ void run_denoiser_prec(pnp_ctx* ctx, const float* u32, float* xout, DevBuf (&act
     const bool head_in_stack = stack && stack16_takes_head(nbody, stack_pairs);
     // head + L0 and L(n-1) + tail in the first and last pair launches (conv_body_x8_kernel's HEAD /
     // TAIL modes): the pairs L1 .. L(n-2) between need an even body depth
+    // (HEAD / TAIL address the pass's fp32 input through one buffer resource: under 2 GB)
     const bool fuse = !w2 && pair && !stack && !ctx->ablate && ctx->fuse_ends && nbody >= 2 && nbody % 2 == 0 &&
-                      C <= kMaxC;
+                      C <= kMaxC && (size_t)mb * C * H * W * sizeof(float) < ((size_t)1 << 31);
     if (fuse) {
       ProfScope ps(ctx, "conv_body_f2h", st);
       X8Ends e;
@@ -1799,12 +1800,13 @@ int pnp_run(pnp_ctx* ctx, int method, const pnp_params* params, int B, int C, in
 
 int pnp_profile_enable(pnp_ctx* ctx, int enable) {
   if (!ctx) return PNP_E_ARG;
-  ctx->gen++;
-  if (enable < 0 || enable > 2) return PNP_E_ARG;
-  ctx->prof = enable;
-  ctx->prof_log.clear();
-  ctx->ev_used = 0;
-  return PNP_OK;
+  return guarded(ctx, [&] {
+    if (enable < 0 || enable > 2) fail(ctx, PNP_E_ARG, "profile mode must be 0 (off), 1 (every launch) or 2 (body launches)");
+    ctx->gen++;   // a captured graph holds the other mode's event packets
+    ctx->prof = enable;
+    ctx->prof_log.clear();
+    ctx->ev_used = 0;
+  });
 }
 
 int pnp_profile_read(pnp_ctx* ctx, int cap, const char** names, double* avg_ms, int* calls, int* n) {

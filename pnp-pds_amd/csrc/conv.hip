@@ -393,6 +393,7 @@ __device__ __forceinline__ int f2_slot(int row) { return (row + 1 + 18 * 64) % k
 // ------------------------------------------------------------------------------------
 constexpr int kX8KSteps = 18;
 constexpr int kX8HeadFrag = 8192;     // HEAD mode: the head's fragments in the (quad-sized) input ring's LDS
+constexpr int kX8HeadBias = kX8HeadFrag + kHeadWBytes;   // HEAD mode: the head's 64 biases after them
 // Non-temporal output stores (A/B at the metric, r03, ms per launch): the head's 0.446 -> 0.439
 // (kept); conv_body_x8 2.248 -> 2.267 and the tail unchanged (not kept).
 constexpr int kNtX8 = 0, kNtTail = 0;                          // buffer-store cache policy (2 = nt)
@@ -511,6 +512,17 @@ __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __re
   for (int r = 0; r < 8; ++r)
     bl[r] = (MODE == kX8Head ? b2 : MODE == kX8Tail ? b1 : layer ? b2 : b1)[32 * m + 8 * g + r];
   const floatx4 c0[2] = {floatx4{bl[0], bl[1], bl[2], bl[3]}, floatx4{bl[4], bl[5], bl[6], bl[7]}};   // first MFMA's C
+  // The launch-constant registers are consumed here once, so the compiler's wait for their loads
+  // sits before the step loop: its waitcnt pass does not read the inline-asm s_waitcnt below, and
+  // otherwise put an s_waitcnt vmcnt(0) before the first MFMA of every step, which also waited
+  // for that step's HEAD staging loads and the previous part's output stores (r06).
+#pragma unroll
+  for (int ks = 0; ks < kX8KSteps; ++ks) asm volatile("" ::"v"(wA[ks][0]), "v"(wA[ks][1]));
+  asm volatile("" ::"v"(c0[0]), "v"(c0[1]));
+  if (MODE == kX8Tail) {
+#pragma unroll
+    for (int c = 0; c < kMaxC; ++c) asm volatile("" ::"v"(tbl[c % (MODE == kX8Tail ? kMaxC : 1)]));
+  }
 #ifdef X8_CLOCK   // diagnostic build (tools/x8_clock.py): shader clock vs the 100 MHz real-time clock
   unsigned long long c0_, r0_;
   asm volatile("s_memtime %0\n\ts_memrealtime %1\n\ts_waitcnt lgkmcnt(0)" : "=s"(c0_), "=s"(r0_)::"memory");
@@ -579,48 +591,49 @@ __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __re
   // HEAD: the input ring holds fp16 quads of the fp32 input (channels >= C and pixels outside the
   // image 0, as conv_head_kernel's quad()): stream row R, pixel p (column x0 - 2 + p) at
   // ring + (f2_slot(R) * kF2InW + p) * 8 (5 184 B of the ring's LDS; the head's fragments follow
-  // at hfr).  stage_load: thread t loads quad t of nrows rows from R0 (nrows <= 14);
-  // stage_store writes it.
+  // at hfr).  stage_load(.., k, q): the thread loads quad q of nrows rows from R0 into slot k
+  // (q < nrows * 36); stage_store(k) writes it.  One buffer resource for the pass's whole input
+  // (the host keeps it under 2 GB): a per-lane resource (the image and the inside test vary by
+  // lane where a step straddles two strips) made every load a waterfall loop.
   unsigned char* hfr = ring + kX8HeadFrag;
-  float sv[kMaxC];
-  int sslot = -1;
-  auto stage_load = [&](int R0, int nrows, int kJ_) {
-    const unsigned plane = (unsigned)(s.H * s.W);
-    const int q = tid;
-    sslot = -1;
+  float sv[1][kMaxC];
+  int sslot[1] = {-1};
+  const unsigned plane = (unsigned)(s.H * s.W);
+  const __amdgpu_buffer_rsrc_t ru = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)ends.u32, (short)0, MODE == kX8Head ? (int)((unsigned)s.B * ends.C * plane * 4u) : 0, 0x00020000);
+  auto stage_load = [&](int R0, int nrows, int kJ_, int k, int q) {
+    sslot[k] = -1;
     if (q >= nrows * kF2InW) return;
     const int R = R0 + q / kF2InW, p = q - (q / kF2InW) * kF2InW;
-    int k, r;
-    locate(R, kJ_, k, r);
-    const SGeom G = pick(k);
+    int kk, r;
+    locate(R, kJ_, kk, r);
+    const SGeom G = pick(kk);
     const int x = G.x0 - 2 + p;
-    const bool inside = R >= 0 && k < K && r < s.H && x >= 0 && x < s.W;
-    const __amdgpu_buffer_rsrc_t ru = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(ends.u32 + (size_t)G.b * ends.C * plane), (short)0, inside ? (int)(ends.C * plane * 4u) : 0,
-        0x00020000);
-    const unsigned o = inside ? (unsigned)(r * s.W + x) : 0u;
+    const bool inside = R >= 0 && kk < K && r < s.H && x >= 0 && x < s.W;
+    const unsigned o = inside ? ((unsigned)G.b * ends.C * plane + (unsigned)(r * s.W + x)) * 4u : 0x80000000u;
 #pragma unroll
     for (int ch = 0; ch < kMaxC; ++ch)
-      sv[ch] = __builtin_bit_cast(
-          float, __builtin_amdgcn_raw_buffer_load_b32(ru, ((unsigned)min(ch, ends.C - 1) * plane + o) * 4u, 0, 0));
-    sslot = (f2_slot(R) * kF2InW + p) * 8;
-    if (!inside) sslot |= 1 << 30;                         // zero quad
+      sv[k][ch] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                ru, o + (unsigned)min(ch, ends.C - 1) * plane * 4u, 0, 0));
+    sslot[k] = (f2_slot(R) * kF2InW + p) * 8;
+    if (!inside) sslot[k] |= 1 << 30;                      // zero quad
   };
-  auto stage_store = [&]() {
-    if (sslot < 0) return;
-    const bool zero = (sslot >> 30) & 1;
+  auto stage_store = [&](int k) {
+    if (sslot[k] < 0) return;
+    const bool zero = (sslot[k] >> 30) & 1;
     _Float16 h4[4];
 #pragma unroll
-    for (int ch = 0; ch < 4; ++ch) h4[ch] = (ch < ends.C && !zero) ? (_Float16)sv[ch] : (_Float16)0;
-    *reinterpret_cast<uint2*>(ring + (sslot & ~(1 << 30))) =
+    for (int ch = 0; ch < 4; ++ch) h4[ch] = (ch < ends.C && !zero) ? (_Float16)sv[k][ch] : (_Float16)0;
+    *reinterpret_cast<uint2*>(ring + (sslot[k] & ~(1 << 30))) =
         make_uint2((uint32_t)__builtin_bit_cast(uint16_t, h4[0]) | ((uint32_t)__builtin_bit_cast(uint16_t, h4[1]) << 16),
                    (uint32_t)__builtin_bit_cast(uint16_t, h4[2]) | ((uint32_t)__builtin_bit_cast(uint16_t, h4[3]) << 16));
   };
   if (MODE == kX8Head) {
-    stage_load(-1, 10, 0);                                 // rows -1 .. 8 of the first strip: 360 quads
-    stage_store();
+    stage_load(-1, 10, 0, 0, tid);                         // rows -1 .. 8 of the first strip: 360 quads
+    stage_store(0);
     for (int i = tid; i < kHeadKSteps * 2 * 64; i += 512)  // conv_head's packed fragments, [ks][m][lane]
       *reinterpret_cast<uint4*>(hfr + 16 * i) = reinterpret_cast<const uint4*>(ends.hw)[i];
+    if (tid < kWidth) reinterpret_cast<float*>(ring + kX8HeadBias)[tid] = ends.hb[tid];
   } else {
     for (int r = wave; r < 10; r += 8) {
       dma_at(r - 1, 0);
@@ -646,15 +659,23 @@ __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __re
     if constexpr (MODE == kX8Head) {
       // every wave: a share of the head's N-tiles (intermediate rows 8J .. 8J+7), then two of L0's
       // output rows (8J-9 + 2 qr, + 1); quads of the next step's input rows staged around them
+      // (an LDS-DMA staging of fp32 rows two steps ahead measured slower, r06: 1.54 vs 1.50 ms)
       const int qr = wave >> 1;                            // quarter: 0 .. 3
-      if (J < Jend) stage_load(8 * J + 9, 8, kJ);
-      else sslot = -1;
+      if (J < Jend) stage_load(8 * J + 9, 8, kJ, 0, tid);
+      else sslot[0] = -1;
       const int hh = lane >> 5, col = lane & 31;
       auto head_part = [&]() {
         if (J < Jend) {
-          float hbl[16];                                   // channels 32m + 16h .. (per step: short-lived)
+          // channels 32m + 16h .. (per step: short-lived).  From LDS: a global load here would
+          // put an s_waitcnt vmcnt(0) in every head epilogue, which also waits for this wave's
+          // staging loads and output stores of the step (r06: the head's serial latency).
+          float hbl[16];
+          typedef const __attribute__((address_space(3))) floatx4* lds_f4p;
 #pragma unroll
-          for (int r = 0; r < 16; ++r) hbl[r] = ends.hb[32 * m + 16 * hh + r];
+          for (int r = 0; r < 16; r += 4) {
+            const floatx4 bq = *(lds_f4p)(size_t)(unsigned)(size_t)(ring + kX8HeadBias + 4 * (32 * m + 16 * hh + r));
+            hbl[r] = bq[0]; hbl[r + 1] = bq[1]; hbl[r + 2] = bq[2]; hbl[r + 3] = bq[3];
+          }
           // ring-row byte offsets of input row 8J - 1 + q and mid-ring row 8J + q (q may vary by lane)
           const int sl0 = f2_slot(8 * J - 1);
           auto rin = [&](int q) { const int t = sl0 + q; return (t >= kF2Ring ? t - kF2Ring : t) * (kF2InW * 8); };
@@ -766,7 +787,7 @@ __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __re
         l0_part();
         head_part();
       }
-      stage_store();
+      stage_store(0);
     } else if (layer == 0 || MODE == kX8Tail) {
       // (TAIL: every wave runs a quarter of L(n-1)'s N-subtiles here, then one output row of the
       // tail below)
@@ -960,6 +981,8 @@ __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __re
         tpart();
         lpart();
       }
+      // (TAIL: leaving the tail's 8 output stores in flight here, vmcnt(8) on the waves that run
+      // it last, measured no faster, r06)
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     } else {
       if (J > 0) {

@@ -176,7 +176,16 @@ def main(ref_root="/root/reference"):
                             method=np.array(method), deg_op=np.array(deg), arch=np.array(arch))
         print(f"iter_{name}.npz  psnr {ps[0]:.3f} -> {ps[-1]:.3f}  ({time.perf_counter()-t:.1f}s)")
 
-    # ---- G5: long run at 256^2 (pins the 0.01 dB target) ---------------------------------
+    make_long_256(ref_root)
+
+
+def make_long_256(ref_root="/root/reference"):
+    """G5: long run at 256^2 (pins the 0.01 dB target)."""
+    install_shims(ref_root)
+    import operators as op
+    import iteration
+    path_kernel = os.path.join(ref_root, "blur_models", "blur_1.mat")
+    nn_dir = os.path.join(ref_root, "nn")
     phi, adj = op.get_observation_operators("blur", path_kernel, 0.8)
     Id, _ = op.get_observation_operators("Id", path_kernel, 0.8)
     xt = synthetic_image(3, 256, 256, seed=7)
@@ -382,6 +391,9 @@ def make_weights_pin(ref_root="/root/reference"):
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "--weights-pin":
         make_weights_pin(*sys.argv[2:])
+        sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "--long256":
+        make_long_256(*sys.argv[2:])
         sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "--long":
         make_long_golden(only=sys.argv[2:] or None)

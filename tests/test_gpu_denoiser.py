@@ -249,7 +249,7 @@ def test_body_two_layers_per_launch_bit_identical(gpu_ctx, name, B, C, H, W):
                          [(20, 0, +1, 1, 2, 3, 256, 256), (20, 0, +1, 1, 3, 3, 50, 70), (6, 1, -1, 0, 2, 1, 37, 45),
                           (6, 0, +1, 1, 1, 1, 8, 32), (4, 1, -1, 0, 1, 3, 9, 33), (20, 1, +1, 0, 90, 3, 20, 70),
                           (6, 0, -1, 1, 300, 1, 9, 33), (8, 0, +1, 1, 5, 3, 64, 96),
-                          (6, 0, +1, 1, 40, 3, 5, 40)])      # H < 8: strips padded to 16 rows
+                          (6, 0, +1, 1, 40, 3, 5, 40)])      # H + 1 < 24: strips padded to 24 rows (a step looks ahead at most one strip)
 def test_head_tail_inside_pair_launches_bit_identical(gpu_ctx, depth, act, residual, clamp, B, C, H, W):
     """conv_body_x8_kernel's HEAD / TAIL modes (the head inside the first two-layer launch, the
     tail inside the last: PNP_TUNE_FUSE_ENDS) give the separate conv_head / conv_tail launches'

@@ -129,7 +129,10 @@ def run_long(g, precision=None):
                                             # round 5: comparisonB-2 above sigma 0.01 (auto:
                                             # fp16w2) at the 200 outer iterations that qualified fp16
                                             ("ADMM_B2_s002_200", "auto"), ("ADMM_B2_s004_200", "auto"),
-                                            ("A_blur_s004_1200", "fp16x3")])
+                                            ("A_blur_s004_1200", "fp16x3"),
+                                            # round 6: fp32 controls of the two
+                                            # split-fp16 cases with per-case x bounds
+                                            ("C_rs_3000", "fp32"), ("RED_blur_s004_1200", "fp32")])
 def test_long_trajectory_psnr(case, precision):
     """Every iteration's PSNR within 0.01 dB of the reference's trajectory.  'auto' is the
     default precision policy (PNP_PREC_AUTO, restated in expected_auto: on blur, fp16 operands up

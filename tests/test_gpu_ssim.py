@@ -54,3 +54,41 @@ def test_solver_records_ssim(case):
     assert abs(ssim[-1] - O.ssim(g["x_true"], x)) < TOL
     # and within the x tolerance of the reference's own final iterate
     assert abs(ssim[-1] - O.ssim(g["x_true"], g["x_out"])) < 5e-3
+
+
+@pytest.mark.parametrize("method,op,B,C,H,W", [("A-Proposed", "blur", 2, 3, 50, 70), ("A-Proposed", "blur", 3, 3, 57, 33),
+                                               ("A-Proposed", "blur", 1, 1, 37, 45), ("A-Proposed", "Id", 2, 3, 41, 29),
+                                               ("B-Proposed", "blur", 2, 3, 61, 37),
+                                               ("C-Proposed", "random_sampling", 2, 3, 45, 58)])
+def test_psnr_same_with_and_without_ssim(method, op, B, C, H, W):
+    """With SSIM recorded the PSNR's squared-error sum moves from K2's fp64 partials into the SSIM
+    pass (fp32 sums over 8 pixels per RGB thread or a whole gray row, then fp64): the recorded
+    PSNR must not depend on record_ssim.  Ragged H / W, partial 56 x 32 SSIM tiles,
+    gray and RGB, the fused (blur A / B) and plain K2 paths; the iterates themselves are the same
+    bits either way, so the two PSNR tracks differ only by summation order."""
+    from pnppds import operators as ops
+    from pnppds.iteration import test_iter_batch
+    from pnppds.operators import load_blur_kernel
+    rng = np.random.default_rng(H * W + C)
+    xt = rng.uniform(0.1, 0.9, (B, C, H, W)).astype(np.float32)
+    xt = (0.5 * xt + 0.5 * np.cumsum(xt, axis=-1) / np.arange(1, W + 1)).astype(np.float32)
+    phi, adj = ops.get_observation_operators(op, "blur_1", 0.8)
+    pois = method == "C-Proposed"
+    phi_o = O.observation_operators(op, load_blur_kernel("blur_1"), 0.8)[0]
+    xo = np.stack([np.asarray(phi_o(xt[b].astype(np.float64) if C > 1 else xt[b, 0].astype(np.float64))).reshape(C, H, W)
+                   for b in range(B)])
+    if pois:
+        xo = np.round(xo * 300) / 300.0
+    else:
+        xo = xo + 0.01 * rng.standard_normal(xo.shape)
+    xo = xo.astype(np.float32)
+    g1, g2 = (0.00035, 1 / 0.00035) if pois else (0.99, 0.99)
+    args = (g1, g2, 1.0, 0.95, 1.0, 15, 15, 0.1, 0.0 if pois else 0.01, 0.1 if method == "B-Proposed" else 0.0, 300,
+            f"DnCNN_nobn_nch_{C}_nlev_0.01", 6, method, C, 0.8)
+    x1, _, _, p1, s1, _ = test_iter_batch(xo, xo, xt, phi, adj, *args, record_ssim=True)
+    x0, _, _, p0, _, _ = test_iter_batch(xo, xo, xt, phi, adj, *args, record_ssim=False)
+    np.testing.assert_array_equal(x1, x0)
+    assert np.isfinite(s1).all()
+    d = np.abs(p1 - p0).max()
+    print(f"{method} {op} {B}x{C}x{H}x{W}: max |PSNR(ssim on) - PSNR(ssim off)| = {d:.2e} dB")
+    assert d < 1e-7, d          # r06: 1.1e-8 .. 2.7e-8 dB over these six cases
