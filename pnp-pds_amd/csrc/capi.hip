@@ -81,6 +81,7 @@ struct pnp_ctx {
   DevBuf head_wlo, body_wlo, tail_wlo;   // fp16 low halves W - fp16(W) (PNP_PREC_FP16W2 / FP16X3)
   DevBuf body_s3h, body_s3l;             // conv_s3 body fragments, hi / lo (PNP_PREC_FP16X3)
   DevBuf body_s3f;                       // conv_s3 body fragments of the fp16 weights (PNP_PREC_FP16A2)
+  DevBuf head_wx3, head_wlox3, tail_wx3, tail_wlox3;   // split head / tail weights at kSplitWScale (FP16X3 / A2)
 
   // operator
   int op_kind = PNP_OP_ID;
@@ -498,7 +499,7 @@ void run_denoiser_prec(pnp_ctx* ctx, const float* u32, float* xout, DevBuf (&act
       float* xo = xout + (size_t)b0 * C * H * W;
       {
         ProfScope ps(ctx, "conv_head", st);
-        launch_conv_head(xin, C, P<half_t>(act[0]), ctx->head_w.p, ctx->head_wlo.p, P<float>(ctx->head_b), s,
+        launch_conv_head(xin, C, P<half_t>(act[0]), ctx->head_wx3.p, ctx->head_wlox3.p, P<float>(ctx->head_b), s,
                          ctx->den_act, ctx->num_cus, 4, st, P<half_t>(alo[0]));
         check_launch(ctx, "conv_head");
       }
@@ -527,7 +528,7 @@ void run_denoiser_prec(pnp_ctx* ctx, const float* u32, float* xout, DevBuf (&act
       }
       {
         ProfScope ps(ctx, "conv_tail_s3", st);
-        launch_conv_s3_tail(P<half_t>(act[cur]), P<half_t>(alo[cur]), xin, xo, ctx->tail_w.p, ctx->tail_wlo.p,
+        launch_conv_s3_tail(P<half_t>(act[cur]), P<half_t>(alo[cur]), xin, xo, ctx->tail_wx3.p, ctx->tail_wlox3.p,
                             P<float>(ctx->tail_b), s, C, ctx->den_residual, ctx->den_clamp, ctx->num_cus, st);
         check_launch(ctx, "conv_tail_s3");
       }
@@ -1561,9 +1562,11 @@ int pnp_set_denoiser(pnp_ctx* ctx, int channels, int depth, int width, const flo
       std::vector<uint16_t> sf(bw.size()), sz(bw.size());   // ... of the fp16 weights (FP16A2; lo = 0)
       q = params + n_head;
       for (int l = 0; l < depth - 2; ++l, q += n_body) {
-        pack_body_weights_s3(q, sh.data() + (size_t)l * kBodyWBytes / 2, sl.data() + (size_t)l * kBodyWBytes / 2);
+        // fp16x3 at kSplitWScale x the weights (the low halves stay normal fp16)
+        pack_body_weights_s3(q, sh.data() + (size_t)l * kBodyWBytes / 2, sl.data() + (size_t)l * kBodyWBytes / 2,
+                             kSplitWScale);
         pack_body_weights_s3(rp.data() + (q - params), sf.data() + (size_t)l * kBodyWBytes / 2,
-                             sz.data() + (size_t)l * kBodyWBytes / 2);
+                             sz.data() + (size_t)l * kBodyWBytes / 2, 1.f);
       }
       ensure(ctx, ctx->body_s3f, sf.size() * 2);
       HIPCHK(ctx, hipMemcpy(ctx->body_s3f.p, sf.data(), sf.size() * 2, hipMemcpyHostToDevice));
@@ -1571,6 +1574,29 @@ int pnp_set_denoiser(pnp_ctx* ctx, int channels, int depth, int width, const flo
       ensure(ctx, ctx->body_s3l, sl.size() * 2);
       HIPCHK(ctx, hipMemcpy(ctx->body_s3h.p, sh.data(), sh.size() * 2, hipMemcpyHostToDevice));
       HIPCHK(ctx, hipMemcpy(ctx->body_s3l.p, sl.data(), sl.size() * 2, hipMemcpyHostToDevice));
+      {                                      // the split (FP16X3 / A2) head and tail at kSplitWScale
+        auto scaled = [&](const float* w, size_t n, bool lo_half) {
+          const float* hi = rp.data() + (w - params);
+          std::vector<float> v(n);
+          for (size_t i = 0; i < n; ++i) v[i] = (lo_half ? w[i] - hi[i] : hi[i]) * kSplitWScale;
+          return v;
+        };
+        std::vector<uint16_t> hx(hw.size()), hlx(hw.size()), tx(tw.size()), tlx(tw.size());
+        const size_t nh = (size_t)kWidth * channels * 9, nt = (size_t)channels * kWidth * 9;
+        const float* tail_p = params + n_head + (size_t)(depth - 2) * n_body;
+        pack_head_weights(scaled(params, nh, false).data(), channels, hx.data());
+        pack_head_weights(scaled(params, nh, true).data(), channels, hlx.data());
+        pack_tail_weights(scaled(tail_p, nt, false).data(), channels, tx.data());
+        pack_tail_weights(scaled(tail_p, nt, true).data(), channels, tlx.data());
+        ensure(ctx, ctx->head_wx3, hx.size() * 2);
+        ensure(ctx, ctx->head_wlox3, hlx.size() * 2);
+        ensure(ctx, ctx->tail_wx3, tx.size() * 2);
+        ensure(ctx, ctx->tail_wlox3, tlx.size() * 2);
+        HIPCHK(ctx, hipMemcpy(ctx->head_wx3.p, hx.data(), hx.size() * 2, hipMemcpyHostToDevice));
+        HIPCHK(ctx, hipMemcpy(ctx->head_wlox3.p, hlx.data(), hlx.size() * 2, hipMemcpyHostToDevice));
+        HIPCHK(ctx, hipMemcpy(ctx->tail_wx3.p, tx.data(), tx.size() * 2, hipMemcpyHostToDevice));
+        HIPCHK(ctx, hipMemcpy(ctx->tail_wlox3.p, tlx.data(), tlx.size() * 2, hipMemcpyHostToDevice));
+      }
       ensure(ctx, ctx->head_wlo, hl.size() * 2);
       ensure(ctx, ctx->body_wlo, bl.size() * 2);
       ensure(ctx, ctx->tail_wlo, tl.size() * 2);

@@ -29,6 +29,10 @@ constexpr int kHaloPix = kHaloH * kHaloW;          // 340
 constexpr int kBodyKSteps = 36;                    // 9 taps x 64 cin / 16
 constexpr int kBodyWBytes = kBodyKSteps * 2 * kWave * 16;   // 73728: [s][m][lane][8 x f16]
 constexpr int kHeadKSteps = 3;                     // 9 taps x 4 ch = 36 -> 48 / 16
+// Split fp16 (PNP_PREC_FP16X3) weights are split at 2^8 times their value: |w_lo| <= 2^-11 |w|
+// is an fp16 subnormal below |w| = 2^-3 at scale 1 (most DnCNN weights), so it kept fewer bits;
+// the kernels unscale the accumulator by 2^-8 (exact) before the bias (conv_s3.hip, r06).
+constexpr float kSplitWScale = 256.f, kSplitWInv = 1.f / 256.f;
 constexpr int kHeadWBytes = kHeadKSteps * 2 * kWave * 16;   // 6144
 constexpr int kTailKSteps = 18;                    // 9 taps x 64 cin / 32
 constexpr int kTailWBytes = kTailKSteps * kWave * 16;       // 18432: [s][lane][8 x f16]

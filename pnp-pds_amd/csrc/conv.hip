@@ -701,10 +701,11 @@ __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __re
               const half8_t ha = *(lds_h8p)(size_t)(unsigned)(size_t)(hfr + ((ks * 2 + m) * 64 + lane) * 16);
 #pragma unroll
               for (int n = 0; n < NT; ++n) {
-                uint2 q0 = make_uint2(0, 0), q1 = make_uint2(0, 0);
-                if (t0 < 9) q0 = *reinterpret_cast<const uint2*>(ring + rin(prow[n] + t0 / 3) + (pcol[n] + t0 % 3) * 8);
-                if (t0 + 1 < 9)
-                  q1 = *reinterpret_cast<const uint2*>(ring + rin(prow[n] + (t0 + 1) / 3) + (pcol[n] + (t0 + 1) % 3) * 8);
+                // taps past 8 (k >= 36) meet zero weights: read tap 8's (finite) quad there instead
+                // of branching around the read (0 x finite adds nothing: the separate head's bits)
+                const int ta = min(t0, 8), tb = min(t0 + 1, 8);
+                const uint2 q0 = *reinterpret_cast<const uint2*>(ring + rin(prow[n] + ta / 3) + (pcol[n] + ta % 3) * 8);
+                const uint2 q1 = *reinterpret_cast<const uint2*>(ring + rin(prow[n] + tb / 3) + (pcol[n] + tb % 3) * 8);
                 const uint4 q = make_uint4(q0.x, q0.y, q1.x, q1.y);
                 acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ha, *reinterpret_cast<const half8_t*>(&q), acc[n], 0, 0, 0);
               }
@@ -1792,7 +1793,7 @@ __global__ __launch_bounds__(256) void conv_head_kernel(const float* __restrict_
 #pragma unroll
             for (int r = 0; r < 8; ++r) {
               const floatx16& a = q < 2 ? a0 : a1;
-              float f = a[8 * (q & 1) + r] + bias_r[q >> 1][8 * (q & 1) + r];
+              float f = a[8 * (q & 1) + r] * kSplitWInv + bias_r[q >> 1][8 * (q & 1) + r];   // weights at 2^8
               f = act == 0 ? fmaxf(f, f * 0.01f) : fmaxf(f, 0.f);
               const _Float16 fh = (_Float16)f;
               v[q][r] = part == 0 ? fh : (_Float16)(f - (float)fh);

@@ -78,7 +78,8 @@ void launch_conv_body_w2(const half_t* in, half_t* out, const void* w, const voi
 constexpr int kS3TileH = 8, kS3TileW = 16;
 hipError_t conv_s3_kernels_init();
 // W [64][64][3][3] -> hi / lo fragments, kBodyWBytes each
-void pack_body_weights_s3(const float* W, uint16_t* hi, uint16_t* lo);
+// scale: fp16x3's body weights are split at kS3WScale (256) times their value, fp16a2's at 1
+void pack_body_weights_s3(const float* W, uint16_t* hi, uint16_t* lo, float scale);
 void launch_conv_s3_body(const half_t* in_hi, const half_t* in_lo, half_t* out_hi, half_t* out_lo, const void* w_hi,
                          const void* w_lo, const float* bias, const ConvShape& s, int act, int num_cus,
                          hipStream_t st);

@@ -9,7 +9,9 @@ is split into contiguous shards with no collective on the data path.  torch.dist
 
 The reference runs its images one after another in one process (main.py:36-69); a batch
 split over G ranks gives per-image results bit-identical to G = 1 (tests/test_shard.py,
-tests/test_gpu_iter.py::test_batch_equals_single_images).
+tests/test_gpu_iter.py::test_batch_equals_single_images), for every precision: under
+precision='converge' each image switches on its own c_n (ABI 8), so a gloo world-2 sharded
+converge solve equals world 1 bit for bit (tests/test_gpu_converge.py).
 """
 from __future__ import annotations
 

@@ -123,16 +123,20 @@ def test_cpu_baseline_fields_on_cpu():
     h = load_blur_kernel("blur_1")
     xt = np.random.default_rng(0).random((3, 32, 32)).astype(np.float32)
     obs, x0 = O.make_observation(xt, "blur", h, 0.8, 0.01, 0.0, False, 300.0)
-    rate, sample, psnr, info = bench.cpu_baseline(cfg, xt, obs.astype(np.float32), x0.astype(np.float32), h, 1.0, 8)
+    rate, sample, psnr, info = bench.cpu_baseline(cfg, xt, obs.astype(np.float32), x0.astype(np.float32), h, 2.0, 8)
     sweep = bench.thread_sweep(info["threads_used"])
-    assert len(info["sweep"]) == 3 * len(sweep) and [r["threads"] for r in info["sweep"]] == 3 * sweep
+    if len(info["sweep"]) == 2:    # a loaded host: one iteration per run exceeds the budget -> all threads, 2 runs
+        sweep, rounds = [sweep[-1]], 2
+    else:
+        rounds = 3
+    assert len(info["sweep"]) == rounds * len(sweep) and [r["threads"] for r in info["sweep"]] == rounds * sweep
     at_best = [r["rate"] for r in info["sweep"] if r["threads"] == info["best_threads"]]
-    assert rate == float(np.median(at_best)) and rate > 0 and len(at_best) == 3
+    assert rate == float(np.median(at_best)) and rate > 0 and len(at_best) == rounds
     assert rate == max(info["median_by_threads"].values()) and info["best_run"] >= rate
     assert info["best_threads"] in sweep and info["spread"] >= 0 and info["spread_at_best_threads"] >= 0
     assert all(r["cpu_use_of_threads"] > 0 and "loadavg_1m" in r and "throttle_cause" in r for r in info["sweep"])
     assert all(len(r["cpus"]) > 0 for r in info["sweep"])
-    assert "cgroup_throttled_s" in info and "3 interleaved rounds" in sample and "pinned" in sample
+    assert "cgroup_throttled_s" in info and f"{rounds} interleaved rounds" in sample and "pinned" in sample
     assert psnr is not None and len(psnr) == info["sweep"][-1]["iters"]
     assert os.sched_getaffinity(0) == before
 

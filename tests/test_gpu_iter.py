@@ -25,8 +25,12 @@ def test_trajectory_matches_reference(case):
     x, s, c, psnr, ssim, t = run_case(g)
     assert x.shape == g["x_out"].shape and x.dtype == np.float32
     # PSNR within the north-star tolerance (0.01 dB) at every iteration
+    from pnppds._device import get_ctx
+    print(f"{case} ({get_ctx().get_precision()[1]}): max|dx| {np.abs(x - g['x_out']).max():.2e}, "
+          f"max|dPSNR| {np.abs(psnr - g['psnr']).max():.2e} dB")
     np.testing.assert_allclose(psnr, g["psnr"], atol=0.01)
-    np.testing.assert_allclose(x, g["x_out"], atol=5e-3)
+    # r06 measured: fp16 2.5-3.8e-4, split fp16 1.8-3.6e-7 (5e-3 for every precision before)
+    np.testing.assert_allclose(x, g["x_out"], atol={"fp16": 1e-3, "fp16w2": 1e-3}.get(get_ctx().get_precision()[1], 1e-6))
     np.testing.assert_allclose(c, g["c"], rtol=0.05, atol=2e-4)
     s_is_zero = case.startswith(("A_", "C_"))          # A / C never touch s: s + 0.5 exactly
     np.testing.assert_allclose(s, g["s_out"], atol=1e-7 if s_is_zero else 5e-3)
@@ -43,8 +47,9 @@ def test_long_run_psnr_within_001db():
                                        15, 15, 0.1, 0.01, 0.0, 300, "DnCNN_nobn_nch_3_nlev_0.01.pth", 120,
                                        "ours-A", 3, 0.8)
     d = np.abs(psnr - g["psnr"])
+    print(f"long_A_blur_256: max|dx| {np.abs(x - g['x_out']).max():.2e}, max|dPSNR| {d.max():.2e} dB")
     assert d.max() < 0.01, (d.max(), int(d.argmax()))
-    np.testing.assert_allclose(x, g["x_out"].astype(np.float32), atol=2e-3)
+    np.testing.assert_allclose(x, g["x_out"], atol=1e-3)          # r06: 4.5e-4 (fp16)
 
 
 def test_batch_equals_single_images():

@@ -36,15 +36,25 @@ AUTO_FP16_MARGIN_DB = 0.005  # where PNP_PREC_AUTO picks plain fp16 operands: ha
 C_RTOL = 0.10
 FP16_C_FLOOR = 5e-4
 C_MIN = {"fp16": 3e-3, "fp16w2": 3e-3, "fp16x3": 1e-6, "fp32": 1e-6, "fp16a2": 1e-6}   # fp16: ~10x its floor
-# x against the reference's final iterate (stored as fp16 in the golden: up to 2.4e-4 of the
-# error is the fixture's own rounding).  Measured max |dx| (r04 parity.txt, r05): fp16 / fp16w2
-# 5e-4 - 1e-3 on every non-chaotic golden (ours-B at 300 iterations: 1.9e-3, its l1-ball support
-# moving with the rounding), split fp16 / fp32 2.0-3.0e-4: bounds about 2-3x that.  Two
-# goldens sit above that under split fp16 (r05 pytest_all.log): ours-C x 3000 (2.2e-3: 3000 primal
-# steps of gamma1 = 3.5e-4 integrate the split's residual error through the dual; PSNR 0.0018 dB)
-# and RED at sigma 0.04 (1.25e-3: the grid's ill-conditioned noise level, as CHAOTIC's two).
-X_TOL = {"fp16": 1.5e-3, "fp16w2": 1.5e-3, "fp16x3": 5e-4, "fp32": 5e-4, "fp16a2": 1.5e-3}
-X_TOL_CASE = {("B_blur_300", "fp16"): 4e-3, ("C_rs_3000", "fp16x3"): 4e-3, ("RED_blur_s004_1200", "fp16x3"): 2.5e-3}
+# x against the reference's final iterate (stored in fp32 since round 6: the fp16 fixture of
+# rounds 2-5 capped the check at half an fp16 ulp, 2.4e-4).  Measured max |dx| on the fp32
+# fixtures (r06, gpurun_out/r06/f/pytest.log; the bounds are 2-3x the largest of each group):
+#  * fp32 operands: 7.8e-7 (ours-A blur x 1200) and 3.6e-6 (ours-B x 300);
+#  * split fp16 (fp16x3): 3.6e-7 .. 4.8e-6 on the well-conditioned goldens, ours-B sigma 0.02
+#    x 1200 3.6e-5 (its l1-ball support moving), ours-C x 300 1.7e-5;
+#  * fp16 / fp16w2 activations: 3.7e-4 .. 8.7e-4 / 3.9e-4 .. 4.2e-4 (ours-B x 300: 1.9e-3);
+#  * fp16a2 (converge after its hand-over): 8.6e-5 .. 4.4e-4, ours-A sigma 0.04 1.3e-3.
+# Two trajectories are ill-conditioned (a perturbation of the iterate grows over the run): ours-C
+# x 3000 (random sampling + Poisson, gamma2 = 1 / gamma1 = 2857) and RED at sigma 0.04.  There
+# the fp32 control lands 5.3e-5 / 2.6e-4 from the reference (the device's fp32 summation order
+# alone) and split fp16 1.6e-4 / 2.1e-4.  (Before round 6 split fp16 landed 2.2e-3 / 1.2e-3 there
+# and had per-case bounds of 4e-3 / 2.5e-3: its weights' low halves were fp16 subnormals; they are
+# split at 2^8 times the weights now, common.h kSplitWScale)
+X_TOL = {"fp16": 2e-3, "fp16w2": 1e-3, "fp16x3": 1e-4, "fp32": 1e-5, "fp16a2": 3e-3}
+X_TOL_CASE = {("B_blur_300", "fp16"): 4e-3,
+              # the ill-conditioned pair, each with its fp32 control beside it
+              ("C_rs_3000", "fp16x3"): 5e-4, ("C_rs_3000", "fp32"): 1.5e-4,                 # 1.6e-4 / 5.3e-5
+              ("RED_blur_s004_1200", "fp16x3"): 6e-4, ("RED_blur_s004_1200", "fp32"): 7e-4}  # 2.1e-4 / 2.6e-4
 
 
 def check_c(case, c, gc, prec):
