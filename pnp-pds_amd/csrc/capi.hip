@@ -1562,9 +1562,9 @@ int pnp_set_denoiser(pnp_ctx* ctx, int channels, int depth, int width, const flo
       std::vector<uint16_t> sf(bw.size()), sz(bw.size());   // ... of the fp16 weights (FP16A2; lo = 0)
       q = params + n_head;
       for (int l = 0; l < depth - 2; ++l, q += n_body) {
-        // fp16x3 at kSplitWScale x the weights (the low halves stay normal fp16)
+        // fp16x3 at kS3BodyScale x the weights (the low halves stay normal fp16)
         pack_body_weights_s3(q, sh.data() + (size_t)l * kBodyWBytes / 2, sl.data() + (size_t)l * kBodyWBytes / 2,
-                             kSplitWScale);
+                             kS3BodyScale);
         pack_body_weights_s3(rp.data() + (q - params), sf.data() + (size_t)l * kBodyWBytes / 2,
                              sz.data() + (size_t)l * kBodyWBytes / 2, 1.f);
       }

@@ -33,6 +33,7 @@ constexpr int kHeadKSteps = 3;                     // 9 taps x 4 ch = 36 -> 48 /
 // is an fp16 subnormal below |w| = 2^-3 at scale 1 (most DnCNN weights), so it kept fewer bits;
 // the kernels unscale the accumulator by 2^-8 (exact) before the bias (conv_s3.hip, r06).
 constexpr float kSplitWScale = 256.f, kSplitWInv = 1.f / 256.f;
+constexpr float kS3BodyScale = kSplitWScale;     // the 64 -> 64 layers' split (conv_s3 body, stack)
 constexpr int kHeadWBytes = kHeadKSteps * 2 * kWave * 16;   // 6144
 constexpr int kTailKSteps = 18;                    // 9 taps x 64 cin / 32
 constexpr int kTailWBytes = kTailKSteps * kWave * 16;       // 18432: [s][lane][8 x f16]

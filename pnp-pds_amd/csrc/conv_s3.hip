@@ -118,7 +118,7 @@ __device__ __forceinline__ floatx4 s3_c0(const float* bl) {
 // 5.3e-5; the CPU emulation of the split, tools/split_scale_emu.py, gives 2.0e-3 at scale 1 and
 // 2.5e-4 with the weights scaled).  The bias enters the accumulator scaled too and the
 // epilogue multiplies by 2^-8: powers of two, so the hi * hi terms round as at scale 1.
-constexpr float kS3WScale = kSplitWScale, kS3WInv = kSplitWInv;
+constexpr float kS3WScale = kS3BodyScale, kS3WInv = 1.f / kS3BodyScale;
 template <int WLO>
 __device__ __forceinline__ float s3_bias_scale() { return WLO ? kS3WScale : 1.f; }
 
@@ -331,7 +331,7 @@ __global__ __launch_bounds__(512, 1) void conv_s3_kernel(const half_t* __restric
       // lanes 0..15 hold channels 0..3 of pixel (row0, px): D rows 4 (l >> 4) + i
 #pragma unroll
       for (int c = 0; c < kMaxC; ++c) {
-        const float nc = acc[0][0][c] * kS3WInv + bl[0][c];   // the tail's split weights are scaled too
+        const float nc = acc[0][0][c] * kSplitWInv + bl[0][c];   // the tail's split weights are scaled too
         float o = residual_sign > 0 ? nc + xi[c] : xi[c] - nc;
         if (clamp_out) o = fminf(fmaxf(o, 0.f), 1.f);
         __builtin_amdgcn_raw_buffer_store_b32(
