@@ -193,7 +193,7 @@ def conv_bytes_per_launch(m, H, W, elem=2):
     return 2 * m * H * W * 64 * elem
 
 
-TRAFFIC_JSON = "profiles/r05/bench/traffic.json"
+TRAFFIC_JSON = "profiles/r06/bench/traffic.json"
 
 
 def measured_traffic(kernel, cfg_name, B):

@@ -115,7 +115,12 @@ def main():
         "last 4 convs (16-19)": set(range(n - 4, n)),
         "every other conv (0, 2, .., 18)": set(range(0, n, 2)),
         "all but the last 2 (0-17)": set(range(n - 2)),
+        "head only (0)": {0},
+        "tail only (19)": {n - 1},
+        "head and tail (0, 19)": {0, n - 1},
     }
+    if len(sys.argv) > 3:                       # a subset of the modes, by name prefix
+        modes = {k: v for k, v in modes.items() if any(k.startswith(p) for p in sys.argv[3].split(","))}
     m = c_ref >= 1e-6
     for name, sp in modes.items():
         t = time.time()
