@@ -536,7 +536,10 @@ __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __re
   const int S = srows;
   // (An XCD-aware strip order, an image's neighbouring strips on CUs sharing one L2, measured
   // the same: 2.109 vs 2.108 ms, r03.)
-  const int bx = (int)blockIdx.x;
+#ifndef X8_HEAD_XCD
+#define X8_HEAD_XCD 0
+#endif
+  const int bx = (MODE == kX8Head && X8_HEAD_XCD) ? xcd_block((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
   const int K = (nstrips - bx + (int)gridDim.x - 1) / (int)gridDim.x;
   const int Jend = (K * S + 7) / 8;                      // the last step (layer l+1 only)
   auto geom = [&](int k) {

@@ -51,7 +51,7 @@ C_MIN = {"fp16": 3e-3, "fp16w2": 3e-3, "fp16x3": 1e-6, "fp32": 1e-6, "fp16a2": 1
 # and had per-case bounds of 4e-3 / 2.5e-3: its weights' low halves were fp16 subnormals; they are
 # split at 2^8 times the weights now, common.h kSplitWScale)
 X_TOL = {"fp16": 2e-3, "fp16w2": 1e-3, "fp16x3": 1e-4, "fp32": 1e-5, "fp16a2": 3e-3}
-X_TOL_CASE = {("B_blur_300", "fp16"): 4e-3,
+X_TOL_CASE = {("B_blur_300", "fp16"): 4e-3,   # 1.9e-3: fp16 activations; its fp32 control is 3.6e-6 (fp32 row)
               # the ill-conditioned pair, each with its fp32 control beside it
               ("C_rs_3000", "fp16x3"): 5e-4, ("C_rs_3000", "fp32"): 1.5e-4,                 # 1.6e-4 / 5.3e-5
               ("RED_blur_s004_1200", "fp16x3"): 6e-4, ("RED_blur_s004_1200", "fp32"): 7e-4}  # 2.1e-4 / 2.6e-4
