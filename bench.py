@@ -321,41 +321,6 @@ def one_cpu_per_core(allowed):
     return out or sorted(allowed)
 
 
-def cpu_busy(cpus, dt=0.25):
-    """Busy fraction of each CPU in `cpus` over `dt` seconds (/proc/stat), or None: the host is
-    shared, so the CPU leg runs on the cores other tenants are leaving idle."""
-    def snap():
-        out = {}
-        with open("/proc/stat") as f:
-            for line in f:
-                if line.startswith("cpu") and line[3].isdigit():
-                    v = line.split()
-                    t = [int(x) for x in v[1:]]
-                    out[int(v[0][3:])] = (sum(t), t[3] + (t[4] if len(t) > 4 else 0))   # total, idle + iowait
-        return out
-    try:
-        a = snap()
-        time.sleep(dt)
-        b = snap()
-    except (OSError, ValueError, IndexError):
-        return None
-    busy = {}
-    for c in cpus:
-        if c in a and c in b:
-            tot, idle = b[c][0] - a[c][0], b[c][1] - a[c][1]
-            busy[c] = 1.0 - idle / tot if tot > 0 else 0.0
-    return busy
-
-
-def idlest(cores, k):
-    """The k least busy of `cores` right now (in CPU order), and their mean busy fraction."""
-    busy = cpu_busy(cores)
-    if not busy or len(cores) <= k:
-        return sorted(cores[:k]), None
-    pick = sorted(sorted(cores, key=lambda c: (busy.get(c, 1.0), c))[:k])
-    return pick, round(float(np.mean([busy.get(c, 1.0) for c in pick])), 3)
-
-
 def pin_process(cpus):
     """Pin every thread of this process (the torch / OpenMP pools included: threads created
     later inherit their creator's mask) to `cpus`.  Returns the number of threads pinned."""
@@ -380,8 +345,7 @@ def cpu_baseline(cfg, x_true, x_obs, x_0, h, budget_s, max_iter):
     image 0, on this host's CPUs, before the process touches the GPU.  A thread
     sweep (4 / 8 / 12 / 16 torch threads, capped at the CPUs this process may use) in three
     interleaved rounds; each leg pins the whole process to as many CPUs as it has threads, one per
-    physical core, the least busy ones just before the leg (one_cpu_per_core, idlest, pin_process:
-    the 256-CPU host is shared with other tenants), so a leg can never exceed the cgroup's CPU quota
+    physical core (one_cpu_per_core, pin_process), so a leg can never exceed the cgroup's CPU quota
     with its own threads (r05: up to 17.7 s of quota throttling per sweep, rates 3.8-10.8 within
     one run).  Per run: the rate, the process's CPU use, the cgroup's quota-throttled seconds and
     periods, the 1-minute load average, and why a throttled run was throttled.  Returns (value,
@@ -408,10 +372,7 @@ def cpu_baseline(cfg, x_true, x_obs, x_0, h, budget_s, max_iter):
     quota = info["cgroup_quota_cpus"]
 
     def run(n, threads):
-        if len(cores) >= threads:
-            cpus, busy = idlest(cores, threads)
-        else:
-            cpus, busy = allowed[:threads], None
+        cpus = cores[:threads] if len(cores) >= threads else allowed[:threads]
         pin_process(cpus)
         torch.set_num_threads(threads)
         thr0, nthr0 = cgroup_cpu_stat()
@@ -431,8 +392,7 @@ def cpu_baseline(cfg, x_true, x_obs, x_0, h, budget_s, max_iter):
                "cpu_use_of_threads": round(cpu_s / max(el * threads, 1e-9), 3),
                "throttled_s": throttled,
                "throttled_periods": (nthr1 - nthr0) if nthr0 is not None and nthr1 is not None else None,
-               "throttle_cause": cause, "loadavg_1m": round(os.getloadavg()[0], 2),
-               "cpus_busy_before": busy}
+               "throttle_cause": cause, "loadavg_1m": round(os.getloadavg()[0], 2)}
         return rec, res
 
     sweep = thread_sweep(info["threads_used"])
@@ -467,9 +427,8 @@ def cpu_baseline(cfg, x_true, x_obs, x_0, h, budget_s, max_iter):
                  "cgroup_throttled_s": round(sum(r_["throttled_s"] or 0.0 for r_ in recs), 3)
                  if recs[0]["throttled_s"] is not None else None,
                  "process_threads": proc_threads(), "torch_threads": best_t,
-                 "pinning": f"each leg pinned to as many CPUs as threads, one per physical core, the least "
-                            f"busy ones over the 0.25 s before the leg (/proc/stat; {len(cores)} cores among "
-                            f"{len(allowed)} allowed CPUs)"})
+                 "pinning": f"each leg pinned to as many CPUs as threads, one per physical core "
+                            f"({len(cores)} cores among {len(allowed)} allowed CPUs)"})
     what = (f"oracle {cfg['method']} ({cfg['op']}) on image 0" if scale == 1.0 else
             f"oracle comparisonB-2 on the 256x256 crop of image 0 at m1={cfg['m1']}, m2={cfg['m2']}, scaled "
             f"by pixels x{scale:g} to the config's image (one step = one outer iteration)")

@@ -535,11 +535,11 @@ __global__ __launch_bounds__(512, 1) void conv_body_x8_kernel(const half_t* __re
   // layer-l step per strip at H = 256: 1 % of the launch)
   const int S = srows;
   // (An XCD-aware strip order, an image's neighbouring strips on CUs sharing one L2, measured
-  // the same: 2.109 vs 2.108 ms, r03.)
-#ifndef X8_HEAD_XCD
-#define X8_HEAD_XCD 0
-#endif
-  const int bx = (MODE == kX8Head && X8_HEAD_XCD) ? xcd_block((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
+  // the same: 2.109 vs 2.108 ms, r03.)  HEAD takes it: its fp32 NCHW input rows are 144 B per
+  // strip and channel over three 128-B lines, so strips on different XCDs fetched each line
+  // about three times (0.55 GB per launch for 0.20 GB of input; 0.20 GB with this order, the
+  // same time: 1.366-1.372 vs 1.359-1.366 ms, r06).
+  const int bx = MODE == kX8Head ? xcd_block((int)blockIdx.x, (int)gridDim.x) : (int)blockIdx.x;
   const int K = (nstrips - bx + (int)gridDim.x - 1) / (int)gridDim.x;
   const int Jend = (K * S + 7) / 8;                      // the last step (layer l+1 only)
   auto geom = [&](int k) {
