@@ -229,6 +229,29 @@ __global__ __launch_bounds__(512, 1) void conv_s3_kernel(const half_t* __restric
   __syncthreads();
   const unsigned plane = (unsigned)(s.H * s.W);
   int cur = 0;
+  // MODE 0 (r06): tile t - 1's epilogue (activation, hi / lo split, 8 stores) runs inside tile t's
+  // K-steps 1 .. MW NT, one (M-subtile, row) per K-step, so its VALU and stores issue between
+  // MFMAs; at the end of the tile both waves of a SIMD used to sit in the epilogue together.  A
+  // workgroup's first tile stores its (empty) predecessor through zero-size buffer resources, so
+  // every tile issues 8 stores and the vmcnt at its end stays exact.  Same arithmetic, same bits.
+  floatx4 pacc[MODE == 0 ? MW : 1][MODE == 0 ? NT : 1] = {};
+  int pb = 0, pty0 = 0, ptx0 = 0;
+  bool pv = false;
+  auto store_mn = [&](int m, int n) {
+    const int y = pty0 + row0 + n;
+    h4_t hi, lo;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) s3_split<ACT, WLO>(pacc[m][n][i], bl[m][i], hi, lo, i);
+    const size_t rowb = (((size_t)pb * s.Hp + y + s.pad) * s.Wp + ptx0 + s.pad) * kWidth;
+    const int nrec = (pv && y < s.H) ? min(kS3TileW, s.W - ptx0) * 128 : 0;
+    const unsigned off = (unsigned)(px * 128 + (16 * (mt0 + m) + 4 * grp) * 2);
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2i_t, hi),
+                                          __builtin_amdgcn_make_buffer_rsrc(out_hi + rowb, (short)0, nrec, 0x00020000),
+                                          off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2i_t, lo),
+                                          __builtin_amdgcn_make_buffer_rsrc(out_lo + rowb, (short)0, nrec, 0x00020000),
+                                          off, 0, 0);
+  };
   for (; t < g.tiles; t += G) {
     const int b = it.b, ty0 = it.ty * kS3TileH, tx0 = it.tx * kS3TileW;
     it.next(G);
@@ -303,28 +326,21 @@ __global__ __launch_bounds__(512, 1) void conv_s3_kernel(const half_t* __restric
         }
         if (WLO) __builtin_amdgcn_sched_group_barrier(0x008, NT, 0);
       }
+      if constexpr (MODE == 0) {
+        if (ks >= 1 && ks <= MW * NT) store_mn((ks - 1) / NT, (ks - 1) % NT);   // tile t - 1's epilogue
+      }
       __builtin_amdgcn_sched_barrier(0);
     }
     if constexpr (MODE == 0) {
 #pragma unroll
       for (int m = 0; m < MW; ++m)
 #pragma unroll
-        for (int n = 0; n < NT; ++n) {
-          const int y = ty0 + row0 + n;
-          h4_t hi, lo;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) s3_split<ACT, WLO>(acc[m][n][i], bl[m][i], hi, lo, i);
-          const size_t rowb = (((size_t)b * s.Hp + y + s.pad) * s.Wp + tx0 + s.pad) * kWidth;
-          const int nrec = y < s.H ? min(kS3TileW, s.W - tx0) * 128 : 0;
-          const unsigned off = (unsigned)(px * 128 + (16 * (mt0 + m) + 4 * grp) * 2);
-          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2i_t, hi),
-                                                __builtin_amdgcn_make_buffer_rsrc(out_hi + rowb, (short)0, nrec, 0x00020000),
-                                                off, 0, 0);
-          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2i_t, lo),
-                                                __builtin_amdgcn_make_buffer_rsrc(out_lo + rowb, (short)0, nrec, 0x00020000),
-                                                off, 0, 0);
-        }
-      // tile t+1 landed: younger than its DMA are the DMA of t+2 (6) and this tile's 8 stores
+        for (int n = 0; n < NT; ++n) pacc[m][n] = acc[m][n];
+      pb = b;
+      pty0 = ty0;
+      ptx0 = tx0;
+      pv = true;
+      // tile t+1 landed: younger than its DMA are the DMA of t+2 (6) and tile t-1's 8 stores
       static_assert(2 * MW * NT == 8, "the vmcnt below counts 8 stores per tile");
       asm volatile("s_waitcnt vmcnt(14) lgkmcnt(0)" ::: "memory");
     } else {
@@ -345,6 +361,14 @@ __global__ __launch_bounds__(512, 1) void conv_s3_kernel(const half_t* __restric
     }
     __builtin_amdgcn_s_barrier();
     cur = cur == 2 ? 0 : cur + 1;
+  }
+  if constexpr (MODE == 0) {
+    if (pv) {                                           // the last tile's epilogue
+#pragma unroll
+      for (int m = 0; m < MW; ++m)
+#pragma unroll
+        for (int n = 0; n < NT; ++n) store_mn(m, n);
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA may land after the workgroup ends
 }
