@@ -190,21 +190,25 @@ __global__ __launch_bounds__(512, 1) void conv_s3_kernel(const half_t* __restric
     const int pr = p / kS3HaloW, pc = p - pr * kS3HaloW;
     doff[j] = (unsigned)(((pr * s.Wp + pc) * kWidth + 8 * ((lane & 7) ^ s3_swz(pc))) * 2);
   }
-  auto issue = [&](const S3Iter& ti, int bi) {          // clamped: always kS3Pieces instructions
+  __amdgpu_buffer_rsrc_t drh, drl;                     // the tile being fetched: hi / lo images, LDS buffer
+  unsigned char* ddst;
+  auto dma_at = [&](const S3Iter& ti, int bi) {        // clamped: always kS3Pieces pieces
     const int b = ti.b, ty0 = ti.ty * kS3TileH, tx0 = ti.tx * kS3TileW;
     const size_t base = (((size_t)b * s.Hp + ty0 + s.pad - 1) * s.Wp + tx0 + s.pad - 1) * kWidth;
-    const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc((void*)(in_hi + base), (short)0, 0x7fffffff,
-                                                                        0x00020000);
-    const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc((void*)(in_lo + base), (short)0, 0x7fffffff,
-                                                                        0x00020000);
-    unsigned char* dst = smem + bi * kS3Buf;
+    drh = __builtin_amdgcn_make_buffer_rsrc((void*)(in_hi + base), (short)0, 0x7fffffff, 0x00020000);
+    drl = __builtin_amdgcn_make_buffer_rsrc((void*)(in_lo + base), (short)0, 0x7fffffff, 0x00020000);
+    ddst = smem + bi * kS3Buf;
+  };
+  auto dma_piece = [&](int j) {
+    const int q = 8 * j + wave, h = q / 24, k = q - 24 * h;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(h ? drl : drh,
+                                             (__attribute__((address_space(3))) void*)(ddst + h * kS3Half + k * 1024),
+                                             16, doff[j], 0, 0, 0);
+  };
+  auto issue = [&](const S3Iter& ti, int bi) {
+    dma_at(ti, bi);
 #pragma unroll
-    for (int j = 0; j < kS3Pieces; ++j) {
-      const int q = 8 * j + wave, h = q / 24, k = q - 24 * h;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(h ? rl : rh,
-                                               (__attribute__((address_space(3))) void*)(dst + h * kS3Half + k * 1024),
-                                               16, doff[j], 0, 0, 0);
-    }
+    for (int j = 0; j < kS3Pieces; ++j) dma_piece(j);
   };
 
   // per-lane part of the B-fragment addresses: tap column dx, channel half hs
@@ -271,7 +275,14 @@ __global__ __launch_bounds__(512, 1) void conv_s3_kernel(const half_t* __restric
       }
       __builtin_amdgcn_sched_barrier(0);
     }
-    issue(itd, cur >= 1 ? cur - 1 : 2);
+    // MODE 0 (r06): tile t+2's pieces issue one per K-step after the deferred epilogue's stores,
+    // between MFMAs, instead of in a burst before the first MFMA of the tile
+    static_assert(MODE != 0 || MW * NT + kS3Pieces < kS3KSteps, "the pieces fit in the K-loop");
+    dma_at(itd, cur >= 1 ? cur - 1 : 2);
+    if constexpr (MODE != 0) {
+#pragma unroll
+      for (int j = 0; j < kS3Pieces; ++j) dma_piece(j);
+    }
     itd.next(G);
     const unsigned char* fb = smem + cur * kS3Buf + row0 * kS3HaloW * 128;
     auto ldB = [&](int ks, int n, int lo) {
@@ -280,6 +291,7 @@ __global__ __launch_bounds__(512, 1) void conv_s3_kernel(const half_t* __restric
     };
     // B fragments are read PD K-steps ahead (the body's 12 MFMAs per K-step cover one step of LDS
     // latency; the tail's 3 do not); per K-step the next reads are interleaved with the MFMAs.
+    // (fp16a2 at depth 2, r06: 2.361-2.365 vs 2.356-2.363 ms per layer, no change)
     constexpr int PD = MODE == 0 ? 1 : 3;
     floatx4 acc[MW][NT];
     half8_t bh[PD + 1][NT], bo[PD + 1][NT];
@@ -328,6 +340,7 @@ __global__ __launch_bounds__(512, 1) void conv_s3_kernel(const half_t* __restric
       }
       if constexpr (MODE == 0) {
         if (ks >= 1 && ks <= MW * NT) store_mn((ks - 1) / NT, (ks - 1) % NT);   // tile t - 1's epilogue
+        if (ks > MW * NT && ks <= MW * NT + kS3Pieces) dma_piece(ks - MW * NT - 1);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -340,7 +353,7 @@ __global__ __launch_bounds__(512, 1) void conv_s3_kernel(const half_t* __restric
       pty0 = ty0;
       ptx0 = tx0;
       pv = true;
-      // tile t+1 landed: younger than its DMA are the DMA of t+2 (6) and tile t-1's 8 stores
+      // tile t+1 landed: younger than its DMA are tile t-1's 8 stores and the DMA of t+2 (6)
       static_assert(2 * MW * NT == 8, "the vmcnt below counts 8 stores per tile");
       asm volatile("s_waitcnt vmcnt(14) lgkmcnt(0)" ::: "memory");
     } else {
