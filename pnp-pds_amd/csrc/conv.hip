@@ -162,6 +162,20 @@ struct RingDma {                                               // one wave's sha
       off[j] = (unsigned)(((pr * s.Wp + pc) * kWidth + c * 8) * 2);
     }
   }
+  // one slot of the DMA of tile t (issue() = every slot), for spreading the slots over a K-loop
+  __device__ __forceinline__ static __amdgpu_buffer_rsrc_t rsrc(const half_t* __restrict__ in, const ConvShape& s,
+                                                                int t) {
+    int b, ty0, tx0;
+    decode_tile(t, s, b, ty0, tx0);
+    const half_t* base = in + (((size_t)b * s.Hp + ty0 + s.pad - 1) * s.Wp + tx0 + s.pad - 1) * kWidth;
+    return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, 0x7fffffff, 0x00020000);
+  }
+  __device__ __forceinline__ void issue_slot(unsigned char* hl, __amdgpu_buffer_rsrc_t rs, int j, int wave) const {
+    const int g = NW * j + wave;
+    if (UNIFORM || g < kDmaSlots - 1 || (g == kDmaSlots - 1 && (threadIdx.x & 63) < 32))
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(hl + g * 1024), 16,
+                                               off[j], 0, 0, 0);
+  }
   template <int CPOL = 0>
   __device__ __forceinline__ void issue(unsigned char* hl, const half_t* __restrict__ in, const ConvShape& s, int t,
                                         int wave) const {
@@ -1133,10 +1147,35 @@ __global__ __launch_bounds__(256, 1) void conv_body_w2_kernel(const half_t* __re
   }
   __syncthreads();
   int cur = 0;
+  // (r06) One wave per SIMD, so nothing overlapped the burst of DMA slots before a tile's K-loop
+  // or the epilogue after it: tile t+1's slots now issue one per K-step (1 .. kSlots) and tile
+  // t-1's epilogue (bias, activation, 2 stores per N-tile) runs at K-steps kSlots+1 .. +4; a
+  // workgroup's first tile stores its empty predecessor through zero-size buffer resources, so
+  // every tile issues its slots and then 8 stores and the vmcnt(8) below stays exact.  The
+  // accumulators of the previous tile live on (64 more registers: AGPRs at one wave per SIMD).
+  constexpr int kW2Slots = RingDma<4, true>::kSlots;
+  static_assert(kW2Slots + 4 < kBodyKSteps, "slots and stores fit in the K-loop");
+  floatx16 pacc[4];
+#pragma unroll
+  for (int n = 0; n < 4; ++n) pacc[n] = floatx16{};
+  int pb = 0, pty0 = 0, ptx0 = 0;
+  bool pv = false;
+  auto store_n = [&](int n) {
+    const int y = pty0 + 4 * rq + n;
+    const half8_t v0 = bias_act8<ACT>(pacc[n], 0, bl), v1 = bias_act8<ACT>(pacc[n], 8, bl + 8);
+    half_t* row = out + (((size_t)pb * s.Hp + y + s.pad) * s.Wp + ptx0 + s.pad) * kWidth;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        row, (short)0, (pv && y < s.H) ? min(kTileW, s.W - ptx0) * 128 : 0, 0x00020000);
+    const unsigned off = (unsigned)(col * 128 + 64 * m + 32 * h);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i_t, v0), rs, off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i_t, v1), rs, off + 16, 0, 0);
+  };
   for (; t < s.tiles; t += gridDim.x) {
     int b, ty0, tx0;
     decode_tile(t, s, b, ty0, tx0);
-    issue_dma(t + gridDim.x, cur ^ 1);        // buffer cur ^ 1 was last read by tile t - 1
+    const int tn = t + gridDim.x;             // buffer cur ^ 1 was last read by tile t - 1
+    const __amdgpu_buffer_rsrc_t drs = RingDma<4, true>::rsrc(in, s, tn < s.tiles ? tn : s.tiles - 1);
+    unsigned char* dbuf = buf(cur ^ 1);
     const unsigned char* hl = buf(cur);
     auto ldB = [&](int ks, int n) {
       const int tap = ks >> 2, sub = ks & 3;
@@ -1161,23 +1200,24 @@ __global__ __launch_bounds__(256, 1) void conv_body_w2_kernel(const half_t* __re
         acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(lo, fb[n], acc[n], 0, 0, 0);
         if (ks + 1 < kBodyKSteps) fb[n] = ldB(ks + 1, n);
       }
+      if (ks >= 1 && ks <= kW2Slots) dma.issue_slot(dbuf, drs, ks - 1, wave);          // tile t+1's halo
+      if (ks > kW2Slots && ks <= kW2Slots + 4) store_n(ks - kW2Slots - 1);             // tile t-1's rows
     }
-    // epilogue: lane (col, h) holds channels 32m + 16h .. +15 of pixel (row 4rq + n, column col)
+    // epilogue (deferred): lane (col, h) holds channels 32m + 16h .. +15 of pixel (row 4rq + n, column col)
 #pragma unroll
-    for (int n = 0; n < 4; ++n) {
-      const int y = ty0 + 4 * rq + n;
-      const half8_t v0 = bias_act8<ACT>(acc[n], 0, bl), v1 = bias_act8<ACT>(acc[n], 8, bl + 8);
-      half_t* row = out + (((size_t)b * s.Hp + y + s.pad) * s.Wp + tx0 + s.pad) * kWidth;
-      const __amdgpu_buffer_rsrc_t rs =
-          __builtin_amdgcn_make_buffer_rsrc(row, (short)0, y < s.H ? min(kTileW, s.W - tx0) * 128 : 0, 0x00020000);
-      const unsigned off = (unsigned)(col * 128 + 64 * m + 32 * h);
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i_t, v0), rs, off, 0, 0);
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i_t, v1), rs, off + 16, 0, 0);
-    }
-    // tile t+1 landed: only this tile's 8 stores are younger than its DMA
+    for (int n = 0; n < 4; ++n) pacc[n] = acc[n];
+    pb = b;
+    pty0 = ty0;
+    ptx0 = tx0;
+    pv = true;
+    // tile t+1 landed: only tile t-1's 8 stores are younger than its DMA
     asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     cur ^= 1;
+  }
+  if (pv) {                                   // the last tile's rows
+#pragma unroll
+    for (int n = 0; n < 4; ++n) store_n(n);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA may land after the workgroup ends
 }
