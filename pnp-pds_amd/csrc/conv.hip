@@ -1945,7 +1945,12 @@ __global__ __launch_bounds__(256, 1) void conv_tail_kernel(const half_t* __restr
     }
     __builtin_amdgcn_sched_barrier(0);       // residual loads stay older than the DMA
     const int nxt2 = cur >= 1 ? cur - 1 : 2;
-    issue_dma(t + 2 * gridDim.x, nxt2);
+    // (r06) tile t+2's 11 slots issue one per K-step (1 .. 11) between MFMAs: one wave per SIMD,
+    // so a burst before the K-loop had nothing to hide behind
+    const int tn2 = t + 2 * gridDim.x;
+    const __amdgpu_buffer_rsrc_t drs = RingDma<4, true>::rsrc(in, s, tn2 < s.tiles ? tn2 : s.tiles - 1);
+    unsigned char* dbuf = buf(nxt2);
+    static_assert(RingDma<4, true>::kSlots < kTailKSteps, "the slots fit in the K-loop");
     const unsigned char* hl = buf(cur);
     auto ldB = [&](int ks, int n) {
       const int tap = ks >> 1;
@@ -1970,6 +1975,7 @@ __global__ __launch_bounds__(256, 1) void conv_tail_kernel(const half_t* __restr
         for (int n = 0; n < 4; ++n)
           acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wL[W2 ? ks : 0], fb[r][n], acc[n], 0, 0, 0);
       }
+      if (ks >= 1 && ks <= RingDma<4, true>::kSlots) dma.issue_slot(dbuf, drs, ks - 1, wave);
     }
     // C/D map of 16x16: col = lane & 15 (pixel of N-tile n), row = 4*(lane>>4) + r (channel):
     // lanes 0..15 hold channels 0..3 of N-tile n.  Store-layout lane l wants N-tile l>>4,
